@@ -1,0 +1,718 @@
+// C-ABI implementation (include/mppi.h): context, buffers, launch planning, host<->device copies.
+//
+// Host arithmetic that feeds the kernels (path-follow branch, intermediate
+// goal, window bounds) is float32 in the reference's operation order; this
+// file is compiled with -ffp-contract=off like the kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "mppi.h"
+#include "mppi_kernels.h"
+
+using namespace mppi;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(MPPI_EHIP, std::string(#expr) + " failed: " + hipGetErrorString(e_));    \
+  } while (0)
+
+constexpr size_t kLdsBytes = 160 * 1024;
+
+struct Plan {
+  bool lds = false;       // rollout kernel DEM path
+  bool fin_lds = false;   // finish kernel DEM path
+  int block = 256, blocks = 0;
+  int wx0 = 0, wy0 = 0, W = 1, Wr = 1;
+  size_t lds_bytes = 0, fin_lds_bytes = 0;
+  int fin_win_offset = 0;
+};
+
+}  // namespace
+
+struct mppi_ctx {
+  mppi_params p{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  // DEM
+  float* Z = nullptr;
+  bool Z_owned = false;
+  size_t Z_cap = 0;
+  int rows = 0, cols = 0;
+  float x_min = 0, y_min = 0, res = 0;
+  // costmap
+  float* cm = nullptr;
+  size_t cm_cap = 0;
+  int cm_size = 0;
+  float cm_hw = 0, cm_res = 0;
+  // state
+  mppi_state st{};
+  bool have_state = false;
+  // nominal sequence double buffer: u_nom[cur] is read by the next step
+  float* u_nom[2] = {nullptr, nullptr};
+  int cur = 0;
+  // step buffers
+  float* cost = nullptr;
+  double* nodes = nullptr;
+  size_t nodes_cap = 0;
+  double* scratch0 = nullptr;
+  double* scratch1 = nullptr;
+  double* record = nullptr;  // single-rank root record (unused output)
+  float* out_dev = nullptr;
+  float* out_host = nullptr;  // pinned
+  float* inj1 = nullptr;
+  float* inj2 = nullptr;
+  int dem_path = 0;
+  // last step (for dump)
+  bool have_last = false;
+  int last_proj = 3, last_mode = 0;
+  uint64_t last_step = 0;
+  mppi_state last_state{};
+  int last_nominal = 0;
+  // timing
+  bool timing = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool ev_roll_pending = false, ev_fin_pending = false;
+  double t_roll = 0, t_fin = 0;
+  int64_t launches = 0;
+  Plan last_plan;
+};
+
+namespace {
+
+int H_of(const mppi_ctx* c) { return c->p.num_iterations; }
+int E_of(const mppi_ctx* c) { return 2 * c->p.num_iterations + 2; }
+
+int check_ready(mppi_ctx* c) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  if (!c->Z) return fail(MPPI_ESTATE, "no DEM: call mppi_set_dem first");
+  if (!c->cm) return fail(MPPI_ESTATE, "no costmap: call mppi_set_costmap first");
+  if (!c->have_state) return fail(MPPI_ESTATE, "no state: call mppi_set_state first");
+  HIP_TRY(hipSetDevice(c->device));
+  return MPPI_OK;
+}
+
+// DEM cell of a point, float32 like Dem::cell (projection_warp.py:39-40).
+void host_cell(const mppi_ctx* c, float x, float y, int& i, int& j) {
+  float fi = (x - c->x_min) / c->res;
+  fi = std::fmin(std::fmax(fi, -1.0f), (float)c->cols);
+  i = (int)fi;
+  float fj = (y + c->y_min) / c->res;
+  fj = std::fmin(std::fmax(fj, -(float)c->rows), 1.0f);
+  j = -(int)fj;
+}
+
+// Launch geometry: the rollouts of one step stay within H*dt*|v|max (+ wheel
+// offset) of the robot, so a square DEM window of that radius holds every
+// cell any lane can touch; it is staged into LDS when it fits.
+Plan make_plan(const mppi_ctx* c) {
+  Plan pl;
+  const int H = H_of(c);
+  const double vabs = std::max(std::fabs((double)c->p.v_min_linear), std::fabs((double)c->p.v_max_linear));
+  const double reach = (double)H * (double)c->p.dt * vabs + std::fabs((double)c->p.wheel_offset) * 1.01 + 0.01;
+  const int Rc = (int)std::ceil(reach / (double)c->res) + 3;
+  int i0, j0;
+  host_cell(c, c->st.x, c->st.y, i0, j0);
+  const int64_t span = 2 * (int64_t)Rc + 2;
+  pl.W = (int)std::min<int64_t>(span, c->cols);
+  pl.Wr = (int)std::min<int64_t>(span, c->rows);
+  pl.wx0 = std::min(std::max(i0 - Rc, 0), c->cols - pl.W);
+  pl.wy0 = std::min(std::max(j0 - Rc, 0), c->rows - pl.Wr);
+  const size_t win = (size_t)pl.W * pl.Wr * sizeof(float);
+  const int64_t K = c->p.num_trajectories;
+
+  bool lds_fits = win <= kLdsBytes;
+  pl.lds = (c->dem_path == 1) || (c->dem_path == 0 && lds_fits);
+  if (c->dem_path == 2) pl.lds = false;
+  if (pl.lds) {
+    // one workgroup per CU holds the window: size the workgroup so ~256 of them cover K
+    pl.block = K <= 256 * 256 ? 256 : (K <= 512 * 256 ? 512 : 1024);
+  } else {
+    pl.block = 256;
+  }
+  pl.blocks = (int)((K + pl.block - 1) / pl.block);
+  const int NW = pl.block / 64;
+  const size_t scratch = (size_t)NW * (2 * H + 1) * sizeof(double) + NW * sizeof(float);
+  pl.lds_bytes = std::max(pl.lds ? win : (size_t)0, scratch);
+  // finish kernel: PairScale[1024] (16 B) during the tree, then u_opt[2H] + window
+  pl.fin_win_offset = (int)(((size_t)2 * H * sizeof(float) + 15) / 16 * 16);
+  pl.fin_lds = lds_fits && c->dem_path != 2 && (pl.fin_win_offset + win) <= kLdsBytes;
+  pl.fin_lds_bytes = std::max((size_t)16 * 1024, (size_t)pl.fin_win_offset + (pl.fin_lds ? win : 0));
+  return pl;
+}
+
+int ensure_nodes(mppi_ctx* c, int blocks) {
+  const size_t need = (size_t)std::max(blocks, 1) * E_of(c);
+  if (need <= c->nodes_cap) return MPPI_OK;
+  if (c->nodes) hipFree(c->nodes);
+  if (c->scratch0) hipFree(c->scratch0);
+  if (c->scratch1) hipFree(c->scratch1);
+  c->nodes = c->scratch0 = c->scratch1 = nullptr;
+  HIP_TRY(hipMalloc(&c->nodes, need * sizeof(double)));
+  const size_t half = ((size_t)std::max(blocks, 1) + 1) / 2 * E_of(c);
+  HIP_TRY(hipMalloc(&c->scratch0, half * sizeof(double)));
+  HIP_TRY(hipMalloc(&c->scratch1, half * sizeof(double)));
+  c->nodes_cap = need;
+  return MPPI_OK;
+}
+
+void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint64_t step,
+                  const float* unom, RolloutArgs& a) {
+  const mppi_params& p = c->p;
+  const int H = p.num_iterations;
+  std::memset(&a, 0, sizeof(a));
+  a.K = p.num_trajectories;
+  a.k_offset = p.k_offset;
+  a.H = H;
+  a.Z = c->Z;
+  a.rows = c->rows;
+  a.grid = c->cols;
+  a.x_min = c->x_min;
+  a.y_min = c->y_min;
+  a.res = c->res;
+  a.wx0 = pl.wx0;
+  a.wy0 = pl.wy0;
+  a.W = pl.W;
+  a.Wr = pl.Wr;
+  a.cm = c->cm;
+  a.cm_size = c->cm_size;
+  a.hw = c->cm_hw;
+  a.res_c = c->cm_res;
+  a.x0 = st.x;
+  a.y0 = st.y;
+  a.h0x = st.heading[0];
+  a.h0y = st.heading[1];
+  a.h0z = st.heading[2];
+  a.wl = st.left_wheel_speed;
+  a.wr = st.right_wheel_speed;
+  a.gx = st.goal_x;
+  a.gy = st.goal_y;
+  a.s1 = st.std_dev_u1;
+  a.s2 = st.std_dev_u2;
+  a.seed = p.seed;
+  a.n_base = step * (uint64_t)((H + 1) / 2);
+  a.u_nom1 = unom;
+  a.u_nom2 = unom + H;
+  a.min_u1 = p.min_u1;
+  a.max_u1 = p.max_u1;
+  a.min_u2 = p.min_u2;
+  a.max_u2 = p.max_u2;
+  a.fk = p.filter_k;
+  a.fa = p.filter_a;
+  a.rwheel = p.robot_radius;
+  a.vmin = p.v_min_linear;
+  a.vmax = p.v_max_linear;
+  a.wmin = p.v_min_angular;
+  a.wmax = p.v_max_angular;
+  a.dt = p.dt;
+  a.off = p.wheel_offset;
+  // _path_follow_critic / _maximise_speed scalar parts (critics_warp.py:111-123, :281-286)
+  const float xd = st.goal_x - st.x;
+  const float yd = st.goal_y - st.y;
+  const float dist = std::sqrt(xd * xd + yd * yd);
+  const float horizon = p.horizon;
+  a.pf_far = dist > horizon ? 1 : 0;
+  a.igx = st.x + (xd * horizon) / (dist + 1e-6f);
+  a.igy = st.y + (yd * horizon) / (dist + 1e-6f);
+  a.pf_scale = 1.0f + (2.0f * horizon) / dist;
+  a.speed_on = (dist < 2.0f) ? 0 : 1;
+  a.w_path = p.w_path;
+  a.w_slope = p.w_slope;
+  a.w_speed = p.w_speed;
+  a.w_obs = p.w_obstacle;
+  a.thr = p.collision_threshold;
+  a.pen = p.collision_penalty;
+  a.T = p.temperature;
+  a.cost_out = c->cost;
+  a.nodes = c->nodes;
+  a.inj_u1 = c->inj1;
+  a.inj_u2 = c->inj2;
+}
+
+void fill_finish(const mppi_ctx* c, const Plan& pl, const mppi_state& st, FinishArgs& f) {
+  const mppi_params& p = c->p;
+  std::memset(&f, 0, sizeof(f));
+  f.H = p.num_iterations;
+  f.T = p.temperature;
+  f.scratch0 = c->scratch0;
+  f.scratch1 = c->scratch1;
+  f.u_nom_next = c->u_nom[c->cur ^ 1];
+  f.out = c->out_dev;
+  f.Z = c->Z;
+  f.rows = c->rows;
+  f.grid = c->cols;
+  f.x_min = c->x_min;
+  f.y_min = c->y_min;
+  f.res = c->res;
+  f.wx0 = pl.wx0;
+  f.wy0 = pl.wy0;
+  f.W = pl.W;
+  f.Wr = pl.Wr;
+  f.win_offset = pl.fin_win_offset;
+  f.x0 = st.x;
+  f.y0 = st.y;
+  f.h0x = st.heading[0];
+  f.h0y = st.heading[1];
+  f.h0z = st.heading[2];
+  f.wl = st.left_wheel_speed;
+  f.wr = st.right_wheel_speed;
+  f.ok = p.opt_filter_k;
+  f.oa = p.opt_filter_a;
+  f.rwheel = p.robot_radius;
+  f.vmin = p.v_min_linear;
+  f.vmax = p.v_max_linear;
+  f.wmin = p.v_min_angular;
+  f.wmax = p.v_max_angular;
+  f.dt = p.dt;
+  f.off = p.wheel_offset;
+}
+
+void collect_timing(mppi_ctx* c) {
+  float ms = 0.f;
+  if (c->ev_roll_pending && hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) {
+    c->t_roll += ms;
+    c->launches += 1;
+  }
+  if (c->ev_fin_pending && hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess) c->t_fin += ms;
+  c->ev_roll_pending = c->ev_fin_pending = false;
+}
+
+// Enqueue the rollout kernel for the current state / nominal sequence.
+int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl,
+                    const float* unom, const mppi_state& st, const RolloutArgs* dump_args) {
+  if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
+  int rc = ensure_nodes(c, pl.blocks);
+  if (rc) return rc;
+  RolloutArgs a;
+  fill_rollout(c, pl, st, step, unom, a);
+  if (dump_args) {
+    a.d_traj = dump_args->d_traj;
+    a.d_hv = dump_args->d_hv;
+    a.d_lw = dump_args->d_lw;
+    a.d_rw = dump_args->d_rw;
+    a.d_v = dump_args->d_v;
+    a.d_w = dump_args->d_w;
+    a.d_u1 = dump_args->d_u1;
+    a.d_u2 = dump_args->d_u2;
+  }
+  if (pl.blocks == 0) return MPPI_OK;
+  if (c->timing && !dump_args) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  HIP_TRY(launch_rollout(a, pl.block, pl.blocks, pl.lds_bytes, c->stream, pl.lds, proj, mode,
+                         dump_args != nullptr));
+  if (c->timing && !dump_args) {
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    c->ev_roll_pending = true;
+  }
+  return MPPI_OK;
+}
+
+int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const double* recs, int n,
+                   int mode, double* record_out, bool timed) {
+  FinishArgs f;
+  fill_finish(c, pl, st, f);
+  f.recs = recs;
+  f.n_recs = n;
+  f.mode = mode;
+  f.record_out = record_out;
+  if (n > 1) {
+    int rc = ensure_nodes(c, n);
+    if (rc) return rc;
+    f.scratch0 = c->scratch0;
+    f.scratch1 = c->scratch1;
+  }
+  if (timed && c->timing) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  HIP_TRY(launch_finish(f, mode == 0 ? (size_t)16 * 1024 : pl.fin_lds_bytes, c->stream,
+                        mode == 1 && pl.fin_lds));
+  if (timed && c->timing) {
+    HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+    c->ev_fin_pending = true;
+  }
+  return MPPI_OK;
+}
+
+int copy_outputs(mppi_ctx* c, mppi_outputs* out) {
+  const int H = H_of(c);
+  HIP_TRY(hipMemcpyAsync(c->out_host, c->out_dev, (size_t)16 * H * sizeof(float),
+                         hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  collect_timing(c);
+  c->cur ^= 1;  // the finish kernel wrote the new nominal sequence into u_nom[cur^1]
+  if (out) {
+    const float* o = c->out_host;
+    if (out->u1_opt) std::memcpy(out->u1_opt, o, H * sizeof(float));
+    if (out->u2_opt) std::memcpy(out->u2_opt, o + H, H * sizeof(float));
+    if (out->lin_vel) std::memcpy(out->lin_vel, o + 2 * H, H * sizeof(float));
+    if (out->ang_vel) std::memcpy(out->ang_vel, o + 3 * H, H * sizeof(float));
+    if (out->traj_sim) std::memcpy(out->traj_sim, o + 4 * H, 3 * H * sizeof(float));
+    if (out->heading_sim) std::memcpy(out->heading_sim, o + 7 * H, 3 * H * sizeof(float));
+    if (out->left_wheel_sim) std::memcpy(out->left_wheel_sim, o + 10 * H, 3 * H * sizeof(float));
+    if (out->right_wheel_sim) std::memcpy(out->right_wheel_sim, o + 13 * H, 3 * H * sizeof(float));
+  }
+  return MPPI_OK;
+}
+
+void remember(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
+  c->have_last = true;
+  c->last_proj = proj;
+  c->last_step = step;
+  c->last_mode = mode;
+  c->last_state = c->st;
+  c->last_nominal = c->cur;  // nominal buffer the rollout read (before the swap)
+  c->last_plan = pl;
+}
+
+int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out) {
+  int rc = check_ready(c);
+  if (rc) return rc;
+  const Plan pl = make_plan(c);
+  if (c->dem_path == 1 && (size_t)pl.W * pl.Wr * sizeof(float) > kLdsBytes)
+    return fail(MPPI_EINVAL, "DEM window does not fit in LDS");
+  rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr);
+  if (rc) return rc;
+  remember(c, proj, step, mode, pl);
+  rc = enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 1, nullptr, true);
+  if (rc) return rc;
+  return copy_outputs(c, out);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mppi_abi_version(void) { return MPPI_ABI_VERSION; }
+
+const char* mppi_last_error(void) { return g_err.c_str(); }
+
+int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
+  if (!params || !out) return fail(MPPI_EINVAL, "null argument");
+  *out = nullptr;
+  const mppi_params& p = *params;
+  if (p.num_iterations < 1) return fail(MPPI_EINVAL, "num_iterations must be >= 1");
+  if (p.num_trajectories < 0 || p.num_trajectories > ((int64_t)1 << 31) * 64)
+    return fail(MPPI_EINVAL, "num_trajectories out of range");
+  if (p.k_offset < 0) return fail(MPPI_EINVAL, "k_offset must be >= 0");
+  if (!(p.temperature > 0.0f)) return fail(MPPI_EINVAL, "temperature must be > 0");
+  if (!(p.dt > 0.0f)) return fail(MPPI_EINVAL, "dt must be > 0");
+  if (p.robot_radius == 0.0f) return fail(MPPI_EINVAL, "robot_radius must be non-zero");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev)
+    return fail(MPPI_EHIP, "device " + std::to_string(device) + " not available (" +
+                               std::to_string(ndev) + " HIP devices)");
+  HIP_TRY(hipSetDevice(device));
+  mppi_ctx* c = new mppi_ctx();
+  c->p = p;
+  c->device = device;
+  const int H = p.num_iterations;
+  auto cleanup = [&](int rc) {
+    mppi_destroy(c);
+    return rc;
+  };
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(MPPI_EHIP, "hipStreamCreate failed"));
+  c->own_stream = true;
+  if (hipMalloc(&c->u_nom[0], 2 * H * sizeof(float)) != hipSuccess ||
+      hipMalloc(&c->u_nom[1], 2 * H * sizeof(float)) != hipSuccess ||
+      hipMalloc(&c->cost, std::max<int64_t>(p.num_trajectories, 1) * sizeof(float)) != hipSuccess ||
+      hipMalloc(&c->out_dev, 16 * H * sizeof(float)) != hipSuccess ||
+      hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
+      hipHostMalloc(&c->out_host, 16 * H * sizeof(float), hipHostMallocDefault) != hipSuccess)
+    return cleanup(fail(MPPI_EHIP, "device allocation failed"));
+  if (hipMemset(c->u_nom[0], 0, 2 * H * sizeof(float)) != hipSuccess ||
+      hipMemset(c->u_nom[1], 0, 2 * H * sizeof(float)) != hipSuccess ||
+      hipMemset(c->cost, 0, std::max<int64_t>(p.num_trajectories, 1) * sizeof(float)) != hipSuccess)
+    return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
+  for (auto& e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(MPPI_EHIP, "hipEventCreate failed"));
+  if (hipDeviceSynchronize() != hipSuccess) return cleanup(fail(MPPI_EHIP, "device sync failed"));
+  *out = c;
+  return MPPI_OK;
+}
+
+void mppi_destroy(mppi_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->Z_owned && c->Z) hipFree(c->Z);
+  if (c->cm) hipFree(c->cm);
+  for (float* u : c->u_nom)
+    if (u) hipFree(u);
+  if (c->cost) hipFree(c->cost);
+  if (c->nodes) hipFree(c->nodes);
+  if (c->scratch0) hipFree(c->scratch0);
+  if (c->scratch1) hipFree(c->scratch1);
+  if (c->record) hipFree(c->record);
+  if (c->out_dev) hipFree(c->out_dev);
+  if (c->out_host) hipHostFree(c->out_host);
+  if (c->inj1) hipFree(c->inj1);
+  if (c->inj2) hipFree(c->inj2);
+  for (auto& e : c->ev)
+    if (e) hipEventDestroy(e);
+  if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int mppi_set_stream(mppi_ctx* c, void* s) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->own_stream && c->stream) HIP_TRY(hipStreamDestroy(c->stream));
+  if (s) {
+    c->stream = (hipStream_t)s;
+    c->own_stream = false;
+  } else {
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->own_stream = true;
+  }
+  return MPPI_OK;
+}
+
+static int check_grid(int32_t rows, int32_t cols, float res) {
+  if (rows < 2 || cols < 2) return fail(MPPI_EINVAL, "DEM must be at least 2x2");
+  if (!(res > 0.0f)) return fail(MPPI_EINVAL, "DEM resolution must be > 0");
+  return MPPI_OK;
+}
+
+int mppi_set_dem(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float x_min, float y_min,
+                 float resolution) {
+  if (!c || !z) return fail(MPPI_EINVAL, "null argument");
+  int rc = check_grid(rows, cols, resolution);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t bytes = (size_t)rows * cols * sizeof(float);
+  if (!c->Z_owned || bytes > c->Z_cap) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->Z_owned && c->Z) HIP_TRY(hipFree(c->Z));
+    c->Z = nullptr;
+    HIP_TRY(hipMalloc(&c->Z, bytes));
+    c->Z_owned = true;
+    c->Z_cap = bytes;
+  }
+  HIP_TRY(hipMemcpyAsync(c->Z, z, bytes, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->rows = rows;
+  c->cols = cols;
+  c->x_min = x_min;
+  c->y_min = y_min;
+  c->res = resolution;
+  return MPPI_OK;
+}
+
+int mppi_set_dem_device(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float x_min,
+                        float y_min, float resolution) {
+  if (!c || !z) return fail(MPPI_EINVAL, "null argument");
+  int rc = check_grid(rows, cols, resolution);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->Z_owned && c->Z) HIP_TRY(hipFree(c->Z));
+  c->Z = const_cast<float*>(z);
+  c->Z_owned = false;
+  c->Z_cap = 0;
+  c->rows = rows;
+  c->cols = cols;
+  c->x_min = x_min;
+  c->y_min = y_min;
+  c->res = resolution;
+  return MPPI_OK;
+}
+
+int mppi_set_costmap(mppi_ctx* c, const float* cm, int32_t size, float half_width, float resolution) {
+  if (!c || !cm) return fail(MPPI_EINVAL, "null argument");
+  if (size < 1) return fail(MPPI_EINVAL, "costmap size must be >= 1");
+  if (!(resolution > 0.0f)) return fail(MPPI_EINVAL, "costmap resolution must be > 0");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t bytes = (size_t)size * size * sizeof(float);
+  if (bytes > c->cm_cap) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->cm) HIP_TRY(hipFree(c->cm));
+    c->cm = nullptr;
+    HIP_TRY(hipMalloc(&c->cm, bytes));
+    c->cm_cap = bytes;
+  }
+  HIP_TRY(hipMemcpyAsync(c->cm, cm, bytes, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->cm_size = size;
+  c->cm_hw = half_width;
+  c->cm_res = resolution;
+  return MPPI_OK;
+}
+
+int mppi_set_state(mppi_ctx* c, const mppi_state* s) {
+  if (!c || !s) return fail(MPPI_EINVAL, "null argument");
+  c->st = *s;
+  c->have_state = true;
+  return MPPI_OK;
+}
+
+int mppi_set_nominal(mppi_ctx* c, const float* u1, const float* u2) {
+  if (!c || !u1 || !u2) return fail(MPPI_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  const int H = H_of(c);
+  HIP_TRY(hipMemcpyAsync(c->u_nom[c->cur], u1, H * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->u_nom[c->cur] + H, u2, H * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPPI_OK;
+}
+
+int mppi_get_nominal(mppi_ctx* c, float* u1, float* u2) {
+  if (!c || !u1 || !u2) return fail(MPPI_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  const int H = H_of(c);
+  HIP_TRY(hipMemcpyAsync(u1, c->u_nom[c->cur], H * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(u2, c->u_nom[c->cur] + H, H * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPPI_OK;
+}
+
+int mppi_step(mppi_ctx* c, int32_t proj, uint64_t step, mppi_outputs* out) {
+  return step_impl(c, proj, step, 0, out);
+}
+
+int mppi_step_injected(mppi_ctx* c, int32_t proj, const float* u1, const float* u2,
+                       mppi_outputs* out) {
+  if (!c || !u1 || !u2) return fail(MPPI_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t n = (size_t)std::max<int64_t>(c->p.num_trajectories, 1) * H_of(c);
+  if (!c->inj1) {
+    HIP_TRY(hipMalloc(&c->inj1, n * sizeof(float)));
+    HIP_TRY(hipMalloc(&c->inj2, n * sizeof(float)));
+  }
+  const size_t bytes = (size_t)c->p.num_trajectories * H_of(c) * sizeof(float);
+  HIP_TRY(hipMemcpyAsync(c->inj1, u1, bytes, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->inj2, u2, bytes, hipMemcpyHostToDevice, c->stream));
+  return step_impl(c, proj, 0, 1, out);
+}
+
+int64_t mppi_record_len(mppi_ctx* c) { return c ? E_of(c) : -1; }
+
+int mppi_step_partial(mppi_ctx* c, int32_t proj, uint64_t step, double* record_dev) {
+  int rc = check_ready(c);
+  if (rc) return rc;
+  if (!record_dev) return fail(MPPI_EINVAL, "null record buffer");
+  const Plan pl = make_plan(c);
+  rc = enqueue_rollout(c, proj, step, 0, pl, c->u_nom[c->cur], c->st, nullptr);
+  if (rc) return rc;
+  remember(c, proj, step, 0, pl);
+  return enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 0, record_dev, false);
+}
+
+int mppi_step_finish(mppi_ctx* c, const double* records_dev, int32_t n, mppi_outputs* out) {
+  int rc = check_ready(c);
+  if (rc) return rc;
+  if (!records_dev || n < 1) return fail(MPPI_EINVAL, "records required");
+  const Plan pl = c->have_last ? c->last_plan : make_plan(c);
+  rc = enqueue_finish(c, pl, c->st, records_dev, n, 1, nullptr, true);
+  if (rc) return rc;
+  return copy_outputs(c, out);
+}
+
+int mppi_get_costs(mppi_ctx* c, float* costs, int64_t n) {
+  if (!c || !costs) return fail(MPPI_EINVAL, "null argument");
+  if (n < 0 || n > c->p.num_trajectories) return fail(MPPI_EINVAL, "n out of range");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpyAsync(costs, c->cost, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPPI_OK;
+}
+
+int mppi_dump_rollouts(mppi_ctx* c, float* traj, float* hv, float* lw, float* rw, float* v, float* w,
+                       float* u1, float* u2) {
+  int rc = check_ready(c);
+  if (rc) return rc;
+  if (!c->have_last) return fail(MPPI_ESTATE, "no step to dump");
+  const size_t KH = (size_t)c->p.num_trajectories * H_of(c);
+  if (KH == 0) return MPPI_OK;
+  float* host[8] = {traj, hv, lw, rw, v, w, u1, u2};
+  const size_t cnt[8] = {3 * KH, 3 * KH, 3 * KH, 3 * KH, KH, KH, KH, KH};
+  float* dev[8] = {nullptr};
+  int out_rc = MPPI_OK;
+  for (int i = 0; i < 8 && out_rc == MPPI_OK; ++i)
+    if (host[i] && hipMalloc(&dev[i], cnt[i] * sizeof(float)) != hipSuccess)
+      out_rc = fail(MPPI_EHIP, "dump allocation failed");
+  if (out_rc == MPPI_OK) {
+    RolloutArgs d;
+    std::memset(&d, 0, sizeof(d));
+    d.d_traj = dev[0];
+    d.d_hv = dev[1];
+    d.d_lw = dev[2];
+    d.d_rw = dev[3];
+    d.d_v = dev[4];
+    d.d_w = dev[5];
+    d.d_u1 = dev[6];
+    d.d_u2 = dev[7];
+    // re-run the last step (deterministic: costs/records are rewritten with identical values)
+    out_rc = enqueue_rollout(c, c->last_proj, c->last_step, c->last_mode, c->last_plan,
+                             c->u_nom[c->last_nominal], c->last_state, &d);
+    for (int i = 0; i < 8 && out_rc == MPPI_OK; ++i)
+      if (host[i] && hipMemcpyAsync(host[i], dev[i], cnt[i] * sizeof(float), hipMemcpyDeviceToHost,
+                                    c->stream) != hipSuccess)
+        out_rc = fail(MPPI_EHIP, "dump copy failed");
+    if (out_rc == MPPI_OK && hipStreamSynchronize(c->stream) != hipSuccess)
+      out_rc = fail(MPPI_EHIP, "dump sync failed");
+  }
+  for (float* p : dev)
+    if (p) hipFree(p);
+  return out_rc;
+}
+
+int mppi_set_timing(mppi_ctx* c, int32_t enable) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  c->timing = enable != 0;
+  c->t_roll = c->t_fin = 0.0;
+  c->launches = 0;
+  return MPPI_OK;
+}
+
+int mppi_get_timing(mppi_ctx* c, double* roll, double* fin, int64_t* n) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  if (roll) *roll = c->t_roll;
+  if (fin) *fin = c->t_fin;
+  if (n) *n = c->launches;
+  return MPPI_OK;
+}
+
+int mppi_set_dem_path(mppi_ctx* c, int32_t mode) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  if (mode < 0 || mode > 2) return fail(MPPI_EINVAL, "dem path must be 0, 1 or 2");
+  c->dem_path = mode;
+  return MPPI_OK;
+}
+
+int mppi_get_launch_info(mppi_ctx* c, int64_t* info, int32_t n) {
+  if (!c || !info) return fail(MPPI_EINVAL, "null argument");
+  const Plan& pl = c->last_plan;
+  const int64_t v[6] = {pl.lds ? 1 : 0, pl.block, pl.blocks, pl.W, pl.Wr, (int64_t)pl.lds_bytes};
+  for (int i = 0; i < n && i < 6; ++i) info[i] = v[i];
+  return MPPI_OK;
+}
+
+int mppi_bilinear_query(mppi_ctx* c, const float* x, const float* y, float* h, int64_t n) {
+  if (!c || !x || !y || !h) return fail(MPPI_EINVAL, "null argument");
+  if (!c->Z) return fail(MPPI_ESTATE, "no DEM");
+  if (n < 0) return fail(MPPI_EINVAL, "n < 0");
+  HIP_TRY(hipSetDevice(c->device));
+  if (n == 0) return MPPI_OK;
+  HIP_TRY(launch_bilinear(c->Z, c->rows, c->cols, c->x_min, c->y_min, c->res, x, y, h, n, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPPI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,165 @@
+// Deterministic float32 math + Philox4x32-10 for the MPPI engine (gfx950).
+//
+// The reference evaluates wp.sin/wp.cos/wp.exp/wp.randn with CUDA libdevice
+// (projection_warp.py:236-237, critics_warp.py:347, sampling_warp.py:73-91).
+// This engine DEFINES each transcendental as a fixed sequence of IEEE float32
+// + - * / operations (Cephes minimax polynomials).  The file must be compiled
+// with -ffp-contract=off so that no a*b+c is fused: the numpy restatement in
+// oracle/dmath.py runs the identical sequence and matches bit for bit.
+//
+// Noise: Philox4x32-10, the generator of rocrand_philox4x32_10.h
+// (ten_rounds / single_round), keyed by the 64-bit seed, counter
+// (n_lo, n_hi, k_lo, k_hi)  ==  rocrand_init(seed, subsequence = k,
+// offset = 4 n).  One block feeds two rollout-steps of one trajectory.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MPPI_HD __host__ __device__ __forceinline__
+
+namespace mppi {
+
+MPPI_HD float bits_f(uint32_t u) { return __builtin_bit_cast(float, u); }
+MPPI_HD uint32_t f_bits(float f) { return __builtin_bit_cast(uint32_t, f); }
+
+// ------------------------------------------------------------------ log
+// Cephes logf; x must be a positive normal float (Box-Muller: x in [2^-24, 1]).
+MPPI_HD float dm_logf(float x) {
+  const uint32_t b = f_bits(x);
+  int e = (int)((b >> 23) & 0xFFu) - 126;
+  float m = bits_f((b & 0x807FFFFFu) | 0x3F000000u);  // [0.5, 1)
+  if (m < 0.707106781186547524f) {
+    e -= 1;
+    m = (m + m) - 1.0f;
+  } else {
+    m = m - 1.0f;
+  }
+  const float z = m * m;
+  float y = 7.0376836292e-2f;
+  y = y * m + -1.1514610310e-1f;
+  y = y * m + 1.1676998740e-1f;
+  y = y * m + -1.2420140846e-1f;
+  y = y * m + 1.4249322787e-1f;
+  y = y * m + -1.6668057665e-1f;
+  y = y * m + 2.0000714765e-1f;
+  y = y * m + -2.4999993993e-1f;
+  y = y * m + 3.3333331174e-1f;
+  y = y * m;
+  y = y * z;
+  const float fe = (float)e;
+  y = y + -2.12194440e-4f * fe;
+  y = y + -0.5f * z;
+  float r = m + y;
+  r = r + 0.693359375f * fe;
+  return r;
+}
+
+// ------------------------------------------------------------------ exp
+// Cephes expf; DEFINED as 0 for x < -87 (keeps the 2^n scale a normal float).
+MPPI_HD float dm_expf(float x) {
+  if (x < -87.0f) return 0.0f;
+  float t = 1.44269504088896341f * x;
+  t = t + 0.5f;
+  const float z = floorf(t);
+  float r = x - z * 0.693359375f;
+  r = r - z * -2.12194440e-4f;
+  const int n = (int)z;
+  const float zz = r * r;
+  float p = 1.9875691500e-4f;
+  p = p * r + 1.3981999507e-3f;
+  p = p * r + 8.3334519073e-3f;
+  p = p * r + 4.1665795894e-2f;
+  p = p * r + 1.6666665459e-1f;
+  p = p * r + 5.0000001201e-1f;
+  float y = p * zz;
+  y = y + r;
+  y = y + 1.0f;
+  return y * bits_f((uint32_t)(n + 127) << 23);
+}
+
+// ------------------------------------------------------------------ sincos
+// Cephes sinf/cosf with a shared Cody-Waite reduction (accurate for |x| < 8192).
+MPPI_HD void dm_sincosf(float x, float* s_out, float* c_out) {
+  const float ax = fabsf(x);
+  int j = (int)(ax * 1.27323954473516f);
+  float y = (float)j;
+  if (j & 1) {
+    j += 1;
+    y = y + 1.0f;
+  }
+  j &= 7;
+  float r = ax - y * 0.78515625f;
+  r = r - y * 2.4187564849853515625e-4f;
+  r = r - y * 3.77489497744594108e-8f;
+  const float z = r * r;
+  float ps = -1.9515295891e-4f * z;
+  ps = ps + 8.3321608736e-3f;
+  ps = ps * z;
+  ps = ps + -1.6666654611e-1f;
+  ps = ps * z;
+  ps = ps * r;
+  ps = ps + r;
+  float pc = 2.443315711809948e-5f * z;
+  pc = pc + -1.388731625493765e-3f;
+  pc = pc * z;
+  pc = pc + 4.166664568298827e-2f;
+  pc = pc * z;
+  pc = pc * z;
+  pc = pc - 0.5f * z;
+  pc = pc + 1.0f;
+  const int q = j >> 1;
+  float s, c;
+  if (q == 0) {
+    s = ps;  c = pc;
+  } else if (q == 1) {
+    s = pc;  c = -ps;
+  } else if (q == 2) {
+    s = -ps; c = -pc;
+  } else {
+    s = -pc; c = ps;
+  }
+  *s_out = (x < 0.0f) ? -s : s;
+  *c_out = c;
+}
+
+// ------------------------------------------------------------------ Philox4x32-10
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+MPPI_HD U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Two uint32 -> two N(0,1) float32 (Box-Muller, DEFINED op sequence).
+MPPI_HD void dm_box_muller(uint32_t ra, uint32_t rb, float* z0, float* z1) {
+  const float u = ((float)(ra >> 8) + 1.0f) * 5.9604644775390625e-8f;  // (0, 1]
+  const float v = (float)(rb >> 8) * 5.9604644775390625e-8f;           // [0, 1)
+  const float rad = sqrtf(-2.0f * dm_logf(u));
+  float s, c;
+  dm_sincosf(6.2831853071795864769f * v, &s, &c);
+  *z0 = rad * c;
+  *z1 = rad * s;
+}
+
+// Noise block n of trajectory k: e1[t], e2[t], e1[t+1], e2[t+1] (t = 2(n mod ceil(H/2))).
+MPPI_HD void noise_block(uint64_t seed, uint64_t n, uint64_t k, float* a1, float* a2, float* b1,
+                         float* b2) {
+  const U4 r = philox4x32_10(U4{(uint32_t)n, (uint32_t)(n >> 32), (uint32_t)k, (uint32_t)(k >> 32)},
+                             (uint32_t)seed, (uint32_t)(seed >> 32));
+  dm_box_muller(r.x, r.y, a1, a2);
+  dm_box_muller(r.z, r.w, b1, b2);
+}
+
+}  // namespace mppi

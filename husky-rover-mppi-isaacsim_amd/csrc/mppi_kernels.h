@@ -1,0 +1,76 @@
+// Kernel argument blocks and launchers shared by mppi_kernels.hip and mppi_capi.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mppi {
+
+// Everything one rollout launch needs, passed by value (uniform per launch).
+struct RolloutArgs {
+  // sizes / ids
+  int64_t K;         // trajectories in this launch (shard-local)
+  int64_t k_offset;  // global index of trajectory 0 (Philox subsequence)
+  int H;
+  // DEM
+  const float* Z;
+  int rows, grid;
+  float x_min, y_min, res;
+  int wx0, wy0, W, Wr;  // LDS window (cols x rows)
+  // costmap
+  const float* cm;
+  int cm_size;
+  float hw, res_c;
+  // robot / goal state (MPPI_isaac.py:489-497, :611-613)
+  float x0, y0, h0x, h0y, h0z, wl, wr, gx, gy, s1, s2;
+  // sampling
+  uint64_t seed, n_base;  // Philox key, block index of (step, t=0)
+  const float* u_nom1;
+  const float* u_nom2;
+  float min_u1, max_u1, min_u2, max_u2;
+  // filter (sampling_warp.py:96-138)
+  float fk, fa, rwheel, vmin, vmax, wmin, wmax;
+  // rollout
+  float dt, off;
+  // critics (critics_warp.py:85-329); pf_far/igx/igy/pf_scale/speed_on precomputed in f32
+  int pf_far, speed_on;
+  float igx, igy, pf_scale;
+  float w_path, w_slope, w_speed, w_obs, thr, pen, T;
+  // outputs
+  float* cost_out;   // [K]
+  double* nodes;     // [blocks][2H+2]
+  // injected controls (MODE 1), trajectory-major [K*H]
+  const float* inj_u1;
+  const float* inj_u2;
+  // dump (DUMP)
+  float *d_traj, *d_hv, *d_lw, *d_rw, *d_v, *d_w, *d_u1, *d_u2;
+};
+
+struct FinishArgs {
+  int H;
+  int mode;  // 0: write root record, 1: finish (u_opt + optimal rollout)
+  const double* recs;
+  int n_recs;
+  double* scratch0;
+  double* scratch1;
+  double* record_out;  // mode 0
+  float T;
+  // finish
+  float* u_nom_next;  // [2H]
+  float* out;         // [16H] u1,u2,v,w,traj,hv,lw,rw
+  const float* Z;
+  int rows, grid;
+  float x_min, y_min, res;
+  int wx0, wy0, W, Wr;
+  int win_offset;  // LDS byte offset of the window
+  float x0, y0, h0x, h0y, h0z, wl, wr;
+  float ok, oa, rwheel, vmin, vmax, wmin, wmax, dt, off;
+};
+
+hipError_t launch_rollout(const RolloutArgs& a, int block, int blocks, size_t lds, hipStream_t st,
+                          bool use_lds, int proj, int mode, bool dump);
+hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool use_lds);
+hipError_t launch_bilinear(const float* Z, int rows, int grid, float x_min, float y_min, float res,
+                           const float* xs, const float* ys, float* hs, int64_t n, hipStream_t st);
+
+}  // namespace mppi

@@ -1,0 +1,316 @@
+"""ctypes binding of libmppi_hip.so (include/mppi.h).
+
+The product path has no fallback: if the HIP library is missing or no GPU is
+visible, every entry point raises.  Build it with ``python -c "import
+__graft_entry__ as g; g.build()"`` (or ``make -C husky-rover-mppi-isaacsim_amd/csrc``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmppi_hip.so")
+
+MPPI_OK = 0
+PROJ = {"2d": 2, "3d": 3, 2: 2, 3: 3}
+
+
+class MppiParams(C.Structure):
+    _fields_ = [
+        ("num_trajectories", C.c_int64),
+        ("k_offset", C.c_int64),
+        ("num_iterations", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("dt", C.c_float),
+        ("robot_radius", C.c_float),
+        ("min_u1", C.c_float), ("max_u1", C.c_float),
+        ("min_u2", C.c_float), ("max_u2", C.c_float),
+        ("v_min_linear", C.c_float), ("v_max_linear", C.c_float),
+        ("v_min_angular", C.c_float), ("v_max_angular", C.c_float),
+        ("temperature", C.c_float),
+        ("filter_k", C.c_float), ("filter_a", C.c_float),
+        ("opt_filter_k", C.c_float), ("opt_filter_a", C.c_float),
+        ("wheel_offset", C.c_float),
+        ("w_path", C.c_float), ("w_slope", C.c_float), ("w_speed", C.c_float),
+        ("w_obstacle", C.c_float),
+        ("collision_threshold", C.c_float), ("collision_penalty", C.c_float),
+        ("horizon", C.c_float),
+        ("seed", C.c_uint64),
+    ]
+
+
+class MppiState(C.Structure):
+    _fields_ = [
+        ("x", C.c_float), ("y", C.c_float),
+        ("heading", C.c_float * 3),
+        ("left_wheel_speed", C.c_float), ("right_wheel_speed", C.c_float),
+        ("goal_x", C.c_float), ("goal_y", C.c_float),
+        ("std_dev_u1", C.c_float), ("std_dev_u2", C.c_float),
+    ]
+
+
+_FP = C.POINTER(C.c_float)
+
+
+class MppiOutputs(C.Structure):
+    _fields_ = [(n, _FP) for n in ("u1_opt", "u2_opt", "lin_vel", "ang_vel", "traj_sim",
+                                   "heading_sim", "left_wheel_sim", "right_wheel_sim")]
+
+
+# name -> (restype, argtypes); must match include/mppi.h (tests/test_lib_symbols.py checks both ways)
+_PROTOS = {
+    "mppi_abi_version": (C.c_int, []),
+    "mppi_last_error": (C.c_char_p, []),
+    "mppi_create": (C.c_int, [C.POINTER(MppiParams), C.c_int32, C.POINTER(C.c_void_p)]),
+    "mppi_destroy": (None, [C.c_void_p]),
+    "mppi_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mppi_set_dem": (C.c_int, [C.c_void_p, _FP, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float]),
+    "mppi_set_dem_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_float,
+                                      C.c_float, C.c_float]),
+    "mppi_set_costmap": (C.c_int, [C.c_void_p, _FP, C.c_int32, C.c_float, C.c_float]),
+    "mppi_set_state": (C.c_int, [C.c_void_p, C.POINTER(MppiState)]),
+    "mppi_set_nominal": (C.c_int, [C.c_void_p, _FP, _FP]),
+    "mppi_get_nominal": (C.c_int, [C.c_void_p, _FP, _FP]),
+    "mppi_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.POINTER(MppiOutputs)]),
+    "mppi_step_injected": (C.c_int, [C.c_void_p, C.c_int32, _FP, _FP, C.POINTER(MppiOutputs)]),
+    "mppi_record_len": (C.c_int64, [C.c_void_p]),
+    "mppi_step_partial": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.c_void_p]),
+    "mppi_step_finish": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(MppiOutputs)]),
+    "mppi_get_costs": (C.c_int, [C.c_void_p, _FP, C.c_int64]),
+    "mppi_dump_rollouts": (C.c_int, [C.c_void_p] + [_FP] * 8),
+    "mppi_set_timing": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mppi_get_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                  C.POINTER(C.c_int64)]),
+    "mppi_set_dem_path": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mppi_get_launch_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]),
+    "mppi_bilinear_query": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
+}
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libmppi_hip.so and declare its prototypes (raises if it is missing)."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"HIP engine library not found at {path}; build it with "
+            "`make -C husky-rover-mppi-isaacsim_amd/csrc` (no CPU fallback exists)")
+    lib = C.CDLL(path)
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.mppi_abi_version() != 1:
+        raise RuntimeError("libmppi_hip.so ABI mismatch")
+    if path == LIB_PATH:
+        _lib = lib
+    return lib
+
+
+def _fp(a):
+    return a.ctypes.data_as(_FP)
+
+
+def _check(lib, rc, what):
+    if rc != MPPI_OK:
+        msg = lib.mppi_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def make_params(K, H, k_offset=0, **kw):
+    """Fill mppi_params; float fields are rounded to float32 by ctypes."""
+    p = MppiParams()
+    p.num_trajectories = int(K)
+    p.k_offset = int(k_offset)
+    p.num_iterations = int(H)
+    defaults = dict(dt=0.045, robot_radius=1.2, min_u1=-1.0, max_u1=1.0, min_u2=-1.0, max_u2=1.0,
+                    v_min_linear=0.0, v_max_linear=2.0, v_min_angular=-1.0, v_max_angular=1.0,
+                    temperature=0.3, filter_k=3.5, filter_a=0.96, opt_filter_k=3.0, opt_filter_a=0.92,
+                    wheel_offset=0.2, w_path=100.5, w_slope=50.5, w_speed=0.5, w_obstacle=25.0,
+                    collision_threshold=0.99, collision_penalty=100000.0, horizon=None, seed=42)
+    defaults.update({k: v for k, v in kw.items() if v is not None or k != "horizon"})
+    if defaults["horizon"] is None:
+        defaults["horizon"] = float(defaults["dt"]) * float(defaults["v_max_linear"]) * int(H)
+    for k, v in defaults.items():
+        if k == "seed":
+            p.seed = int(v) & 0xFFFFFFFFFFFFFFFF
+        else:
+            setattr(p, k, float(v))
+    return p
+
+
+def make_state(x, y, heading=(1.0, 0.0, 0.0), left_wheel_speed=0.0, right_wheel_speed=0.0,
+               goal_x=0.0, goal_y=0.0, std_dev_u1=0.25, std_dev_u2=0.25):
+    """Fill mppi_state; the heading is normalised in float64 first (MPPI_isaac.py:493)."""
+    s = MppiState()
+    s.x, s.y = float(x), float(y)
+    h = np.asarray(heading, dtype=np.float64)
+    h = (h / np.linalg.norm(h)).astype(np.float32)
+    for i in range(3):
+        s.heading[i] = float(h[i])
+    s.left_wheel_speed = float(left_wheel_speed)
+    s.right_wheel_speed = float(right_wheel_speed)
+    s.goal_x, s.goal_y = float(goal_x), float(goal_y)
+    s.std_dev_u1, s.std_dev_u2 = float(std_dev_u1), float(std_dev_u2)
+    return s
+
+
+class Engine:
+    """One device context of the HIP MPPI engine (thin, allocation-free per step)."""
+
+    OUT_NAMES = ("u1_opt", "u2_opt", "lin_vel", "ang_vel", "traj_sim", "heading_sim",
+                 "left_wheel_sim", "right_wheel_sim")
+
+    def __init__(self, params: MppiParams, device: int = 0):
+        self.lib = load_library()
+        self.params = params
+        self.H = int(params.num_iterations)
+        self.K = int(params.num_trajectories)
+        self.device = int(device)
+        ctx = C.c_void_p()
+        _check(self.lib, self.lib.mppi_create(C.byref(params), self.device, C.byref(ctx)), "mppi_create")
+        self.ctx = ctx
+        H = self.H
+        self._buf = {n: np.zeros(3 * H if n.endswith("_sim") else H, np.float32) for n in self.OUT_NAMES}
+        self._out = MppiOutputs(*[_fp(self._buf[n]) for n in self.OUT_NAMES])
+        self._keep = []
+
+    # ------------------------------------------------------------ lifetime
+    def close(self):
+        if getattr(self, "ctx", None) and self.ctx.value:
+            self.lib.mppi_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _c(self, rc, what):
+        _check(self.lib, rc, what)
+
+    # ------------------------------------------------------------ scene / state
+    def set_stream(self, stream_handle):
+        self._c(self.lib.mppi_set_stream(self.ctx, C.c_void_p(stream_handle or None)), "mppi_set_stream")
+
+    def set_dem(self, Z, half_width=None, resolution=None, x_min=None, y_min=None):
+        Z = np.ascontiguousarray(Z, dtype=np.float32)
+        rows, cols = Z.shape
+        if resolution is None:
+            resolution = 2.0 * half_width / cols
+        if x_min is None:
+            x_min = -half_width
+        if y_min is None:
+            y_min = -half_width
+        self._c(self.lib.mppi_set_dem(self.ctx, _fp(Z), rows, cols, x_min, y_min, resolution), "mppi_set_dem")
+
+    def set_dem_device(self, ptr, rows, cols, half_width, resolution=None, keepalive=None):
+        if resolution is None:
+            resolution = 2.0 * half_width / cols
+        self._c(self.lib.mppi_set_dem_device(self.ctx, C.c_void_p(int(ptr)), rows, cols, -half_width,
+                                             -half_width, resolution), "mppi_set_dem_device")
+        self._keep = [keepalive]
+
+    def set_costmap(self, cm, half_width, resolution=None):
+        cm = np.ascontiguousarray(cm, dtype=np.float32)
+        size = cm.shape[1]
+        if resolution is None:
+            resolution = 2.0 * half_width / size
+        self._c(self.lib.mppi_set_costmap(self.ctx, _fp(cm), size, half_width, resolution), "mppi_set_costmap")
+
+    def set_state(self, state: MppiState):
+        self._c(self.lib.mppi_set_state(self.ctx, C.byref(state)), "mppi_set_state")
+
+    def set_nominal(self, u1, u2):
+        u1 = np.ascontiguousarray(u1, dtype=np.float32)
+        u2 = np.ascontiguousarray(u2, dtype=np.float32)
+        assert u1.size == self.H and u2.size == self.H
+        self._c(self.lib.mppi_set_nominal(self.ctx, _fp(u1), _fp(u2)), "mppi_set_nominal")
+
+    def get_nominal(self):
+        u1 = np.zeros(self.H, np.float32)
+        u2 = np.zeros(self.H, np.float32)
+        self._c(self.lib.mppi_get_nominal(self.ctx, _fp(u1), _fp(u2)), "mppi_get_nominal")
+        return u1, u2
+
+    def set_dem_path(self, mode):
+        self._c(self.lib.mppi_set_dem_path(self.ctx, {"auto": 0, "lds": 1, "global": 2}.get(mode, mode)),
+                "mppi_set_dem_path")
+
+    # ------------------------------------------------------------ steps
+    def _outputs(self):
+        H = self.H
+        b = self._buf
+        return dict(u1_opt=b["u1_opt"].copy(), u2_opt=b["u2_opt"].copy(), lin_vel=b["lin_vel"].copy(),
+                    ang_vel=b["ang_vel"].copy(), traj_sim=b["traj_sim"].reshape(H, 3).copy(),
+                    heading_sim=b["heading_sim"].reshape(H, 3).copy(),
+                    left_wheel_sim=b["left_wheel_sim"].reshape(H, 3).copy(),
+                    right_wheel_sim=b["right_wheel_sim"].reshape(H, 3).copy())
+
+    def step(self, proj="3d", step=0, copy=True):
+        self._c(self.lib.mppi_step(self.ctx, PROJ[proj], int(step), C.byref(self._out)), "mppi_step")
+        return self._outputs() if copy else None
+
+    def step_injected(self, u1, u2, proj="3d"):
+        u1 = np.ascontiguousarray(u1, dtype=np.float32).reshape(-1)
+        u2 = np.ascontiguousarray(u2, dtype=np.float32).reshape(-1)
+        assert u1.size == self.K * self.H and u2.size == self.K * self.H
+        self._c(self.lib.mppi_step_injected(self.ctx, PROJ[proj], _fp(u1), _fp(u2), C.byref(self._out)),
+                "mppi_step_injected")
+        return self._outputs()
+
+    def record_len(self):
+        return int(self.lib.mppi_record_len(self.ctx))
+
+    def step_partial(self, record_ptr, proj="3d", step=0):
+        self._c(self.lib.mppi_step_partial(self.ctx, PROJ[proj], int(step), C.c_void_p(int(record_ptr))),
+                "mppi_step_partial")
+
+    def step_finish(self, records_ptr, n, copy=True):
+        self._c(self.lib.mppi_step_finish(self.ctx, C.c_void_p(int(records_ptr)), int(n), C.byref(self._out)),
+                "mppi_step_finish")
+        return self._outputs() if copy else None
+
+    # ------------------------------------------------------------ introspection
+    def costs(self):
+        c = np.zeros(self.K, np.float32)
+        self._c(self.lib.mppi_get_costs(self.ctx, _fp(c), self.K), "mppi_get_costs")
+        return c
+
+    def dump(self):
+        K, H = self.K, self.H
+        arrs = dict(traj=np.zeros((K, H, 3), np.float32), hv=np.zeros((K, H, 3), np.float32),
+                    lw=np.zeros((K, H, 3), np.float32), rw=np.zeros((K, H, 3), np.float32),
+                    v=np.zeros((K, H), np.float32), w=np.zeros((K, H), np.float32),
+                    u1=np.zeros((K, H), np.float32), u2=np.zeros((K, H), np.float32))
+        self._c(self.lib.mppi_dump_rollouts(self.ctx, *[_fp(arrs[n]) for n in
+                                                        ("traj", "hv", "lw", "rw", "v", "w", "u1", "u2")]),
+                "mppi_dump_rollouts")
+        return arrs
+
+    def set_timing(self, on=True):
+        self._c(self.lib.mppi_set_timing(self.ctx, 1 if on else 0), "mppi_set_timing")
+
+    def timing(self):
+        r = C.c_double()
+        f = C.c_double()
+        n = C.c_int64()
+        self._c(self.lib.mppi_get_timing(self.ctx, C.byref(r), C.byref(f), C.byref(n)), "mppi_get_timing")
+        return r.value, f.value, n.value
+
+    def launch_info(self):
+        info = (C.c_int64 * 6)()
+        self._c(self.lib.mppi_get_launch_info(self.ctx, info, 6), "mppi_get_launch_info")
+        keys = ("dem_in_lds", "block", "blocks", "window_cols", "window_rows", "lds_bytes")
+        return dict(zip(keys, [int(v) for v in info]))
+
+    def bilinear_query(self, x_ptr, y_ptr, h_ptr, n):
+        self._c(self.lib.mppi_bilinear_query(self.ctx, C.c_void_p(int(x_ptr)), C.c_void_p(int(y_ptr)),
+                                             C.c_void_p(int(h_ptr)), int(n)), "mppi_bilinear_query")

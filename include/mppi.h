@@ -1,0 +1,185 @@
+/*
+ * mppi.h — C-ABI of the MI355X MPPI rollout-and-cost engine (libmppi_hip.so).
+ *
+ * Drop-in boundary for the Warp MPPI step of
+ * thesis_master/warp_implementation/MPPI_isaac.py (reference, read-only).
+ * Plain C types only: host pointers + sizes, device pointers only where the
+ * caller already owns device memory (zero-copy DEM binding, rank records).
+ *
+ * Conventions
+ *   status:   every int-returning call returns MPPI_OK (0) or a negative
+ *             code; mppi_last_error() (thread-local) holds the message.
+ *   memory:   the caller owns host buffers (copied in/out); the library owns
+ *             its device buffers and pinned staging.
+ *   threads:  one context per device; calls on one context are serialised
+ *             by the caller (the reference is single-threaded, driven from
+ *             the Isaac main loop, visual_terrain_stack_full_terrain.py:466).
+ *   sync:     mppi_step / mppi_step_finish / mppi_step_injected return with
+ *             the outputs in host memory (the reference's .numpy() reads,
+ *             MPPI_isaac.py:769-775 / visual_terrain_stack_full_terrain.py:471-472).
+ */
+#ifndef HUSKY_MPPI_H
+#define HUSKY_MPPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPPI_ABI_VERSION 1
+
+enum mppi_status {
+  MPPI_OK = 0,
+  MPPI_EINVAL = -1, /* bad argument (reference: Warp raises on bad launch inputs) */
+  MPPI_EHIP = -2,   /* HIP runtime error (device fault, OOM, no device) */
+  MPPI_ESTATE = -3, /* call out of order (e.g. step before set_dem) */
+};
+
+enum mppi_proj {
+  MPPI_PROJ_2D = 2, /* projection_warp.py:353-382 (_generate_trajectories_2D_kernel) */
+  MPPI_PROJ_3D = 3, /* projection_warp.py:284-350 (_generate_trajectories_kernel)    */
+};
+
+typedef struct mppi_ctx mppi_ctx;
+
+/* Controller parameters.  Replaces MPPI_Controller.__init__ config parsing
+ * (MPPI_isaac.py:404-440, config.yaml) and the constants hard-coded at
+ * MPPI_isaac.py:548-549,688-689, projection_warp.py:333,
+ * critics_warp.py:251-253,325-329.  Float fields are used as float32, the
+ * precision the Warp kernels receive them in. */
+typedef struct mppi_params {
+  int64_t num_trajectories; /* trajectories of THIS context (its shard of K)         */
+  int64_t k_offset;         /* global index of this shard's first trajectory          */
+  int32_t num_iterations;   /* H (config.yaml controller.number_of_iterations)        */
+  int32_t reserved0;
+  float dt;                 /* config.yaml controller.dt                              */
+  float robot_radius;       /* r_wheels of _convert_inputs_to_velocities (frame_work.robot_radius) */
+  float min_u1, max_u1, min_u2, max_u2;                    /* config.yaml inputs.*       */
+  float v_min_linear, v_max_linear, v_min_angular, v_max_angular; /* velocities.*        */
+  float temperature;        /* cost_evaluation.temperature                            */
+  float filter_k, filter_a;         /* rollout wheel filter, MPPI_isaac.py:548-549 (3.5, 0.96) */
+  float opt_filter_k, opt_filter_a; /* optimal-sequence filter, MPPI_isaac.py:688-689 (3.0, 0.92) */
+  float wheel_offset;       /* projection_warp.py:333 (0.2)                           */
+  float w_path, w_slope, w_speed, w_obstacle; /* critics_warp.py:325-329               */
+  float collision_threshold, collision_penalty; /* critics_warp.py:251-253 (0.99, 1e5) */
+  float horizon;            /* MPPI_isaac.py:440 dt*v_max*H (computed by the caller in float64) */
+  uint64_t seed;            /* Philox key (replaces default_rng(42).integers, MPPI_isaac.py:409,517) */
+} mppi_params;
+
+/* Per-step robot / goal state: the values MPPI_step reads from the controller
+ * (MPPI_isaac.py:489-503 reset("controller"), :538-539, :611-613, :510-511 of
+ * the Isaac loop).  heading is normalised by the caller (MPPI_isaac.py:493). */
+typedef struct mppi_state {
+  float x, y;
+  float heading[3];
+  float left_wheel_speed, right_wheel_speed;
+  float goal_x, goal_y;
+  float std_dev_u1, std_dev_u2;
+} mppi_state;
+
+/* Host output pointers (any may be NULL).  Each replaces one Warp array the
+ * caller reads with .numpy() after MPPI_step (MPPI_isaac.py:446-487). */
+typedef struct mppi_outputs {
+  float* u1_opt;          /* [H]   optimal_u1_wp                         */
+  float* u2_opt;          /* [H]   optimal_u2_wp                         */
+  float* lin_vel;         /* [H]   optimal_lin_vel_wp                    */
+  float* ang_vel;         /* [H]   optimal_ang_vel_wp                    */
+  float* traj_sim;        /* [H*3] trajectories_sim                      */
+  float* heading_sim;     /* [H*3] heading_vectors_sim                   */
+  float* left_wheel_sim;  /* [H*3] left_wheel_pos_sim                    */
+  float* right_wheel_sim; /* [H*3] right_wheel_pos_sim                   */
+} mppi_outputs;
+
+int mppi_abi_version(void);
+const char* mppi_last_error(void);
+
+/* MPPI_Controller.__init__ + warp_setup (MPPI_isaac.py:404-487): allocate
+ * device buffers on `device`; nominal controls start at zero (:446-447). */
+int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out);
+void mppi_destroy(mppi_ctx* ctx);
+
+/* Run on the caller's HIP stream (e.g. torch.cuda.current_stream()); NULL = own stream. */
+int mppi_set_stream(mppi_ctx* ctx, void* hip_stream);
+
+/* self.Z_wp = wp.array(surface.Z.flatten()) (MPPI_isaac.py:460): copies the
+ * row-major rows x cols DEM to the device.  x_min = y_min = -half_width and
+ * resolution = 2*half_width/grid_size as in the launch args (:560-564). */
+int mppi_set_dem(mppi_ctx* ctx, const float* z_host, int32_t rows, int32_t cols, float x_min,
+                 float y_min, float resolution);
+
+/* controller.Z_wp = DEM_warp rebinding (visual_terrain_stack_full_terrain.py:567):
+ * binds a DEM already resident in device memory (zero copy; the caller keeps
+ * it alive and unchanged while steps run). */
+int mppi_set_dem_device(mppi_ctx* ctx, const float* z_device, int32_t rows, int32_t cols,
+                        float x_min, float y_min, float resolution);
+
+/* self.costmap_wp (MPPI_isaac.py:461) / costmap_wp.assign(...)
+ * (visual_terrain_stack_full_terrain.py:563): size x size row-major costmap;
+ * half_width and costmap resolution as passed at MPPI_isaac.py:622-624. */
+int mppi_set_costmap(mppi_ctx* ctx, const float* costmap_host, int32_t size, float half_width,
+                     float resolution);
+
+/* reset("controller") (MPPI_isaac.py:489-497) + the robot/goal/sigma fields MPPI_step reads. */
+int mppi_set_state(mppi_ctx* ctx, const mppi_state* state);
+
+/* optimal_u1_wp / optimal_u2_wp as the next step's nominal sequence (MPPI_isaac.py:518-519). */
+int mppi_set_nominal(mppi_ctx* ctx, const float* u1, const float* u2);
+int mppi_get_nominal(mppi_ctx* ctx, float* u1, float* u2);
+
+/* MPPI_step(proj) (MPPI_isaac.py:505-720) for a single-rank controller:
+ * sample -> filter -> rollout -> critics -> softmax-weighted update -> optimal
+ * filter -> optimal (3D) rollout; outputs copied to host.  `step` is the
+ * Philox step counter (noise offset); the new nominal sequence replaces the
+ * old one, as reset("sim") + _compute_weighted_sum do (:655-670). */
+int mppi_step(mppi_ctx* ctx, int32_t proj, uint64_t step, mppi_outputs* out);
+
+/* Same with caller-supplied sampled controls u1,u2 [K*H] trajectory-major
+ * (the injected-input experiment of compare_3d_2d.py:324-533,668-688). */
+int mppi_step_injected(mppi_ctx* ctx, int32_t proj, const float* u1_host, const float* u2_host,
+                       mppi_outputs* out);
+
+/* ---- K-sharded multi-GPU step (no reference equivalent) ----
+ * Record = [m, S, V1[H], V2[H]] float64 (mppi_record_len() doubles).
+ * mppi_step_partial enqueues this rank's rollout and writes its record to
+ * record_dev (device memory, async on the context stream); the caller
+ * all-gathers the G records (RCCL) and mppi_step_finish combines them in rank
+ * order and runs the optimal rollout, returning outputs in host memory. */
+int64_t mppi_record_len(mppi_ctx* ctx);
+int mppi_step_partial(mppi_ctx* ctx, int32_t proj, uint64_t step, double* record_dev);
+int mppi_step_finish(mppi_ctx* ctx, const double* records_dev, int32_t n_records,
+                     mppi_outputs* out);
+
+/* ---- introspection (self.costs_wp / self.trajectories .numpy(), MPPI_isaac.py:466-470) ---- */
+/* costs of the last step's trajectories of this context [n <= K] */
+int mppi_get_costs(mppi_ctx* ctx, float* costs_host, int64_t n);
+/* re-run the last step with per-rollout-step outputs (bitwise identical; [K*H] / [K*H*3]
+ * trajectory-major like the reference arrays); any pointer may be NULL. */
+int mppi_dump_rollouts(mppi_ctx* ctx, float* traj, float* heading, float* left_wheel,
+                       float* right_wheel, float* lin_vel, float* ang_vel, float* u1, float* u2);
+
+/* HIP-event timing of the rollout kernel and of the combine/optimal-rollout
+ * kernel, measured on the context stream around each launch. */
+int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
+int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_t* launches);
+
+/* DEM access path of the rollout kernel: 0 = auto (LDS window when it fits),
+ * 1 = LDS window (error if it does not fit), 2 = global memory (L2/MALL). */
+int mppi_set_dem_path(mppi_ctx* ctx, int32_t mode);
+
+/* Layout/launch facts for the last step (for tests and the bench):
+ * info[0]=dem_in_lds, [1]=block threads, [2]=blocks, [3]=window cols,
+ * [4]=window rows, [5]=lds bytes. */
+int mppi_get_launch_info(mppi_ctx* ctx, int64_t* info, int32_t n);
+
+/* Standalone DEM bilinear kernel: for n query points
+ * (x[i], y[i]) in device memory, heights[i] = corner lookup + bilinear exactly
+ * as projection_warp.py:8-100, on the context's DEM. */
+int mppi_bilinear_query(mppi_ctx* ctx, const float* x_dev, const float* y_dev, float* h_dev,
+                        int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HUSKY_MPPI_H */
