@@ -1,0 +1,214 @@
+"""MPPI steps/s at K=65536, H=100 on the 750x750 costmap (BASELINE.json metric), 1..N GPUs.
+
+One "step" = one full MPPI_step("3d") (thesis_master/warp_implementation/MPPI_isaac.py:505-720):
+Philox sampling, wheel filter, 2.5D rollout, four critics, softmax-weighted
+update, optimal filter and optimal rollout, with the outputs copied to host
+memory.  Inputs (DEM, costmap, state) are resident in HBM before timing.
+
+Scaling: weak.  Each rank owns K_per_gpu = 65536 trajectories (the headline
+shard); the global sample count is 65536*N, exchanged once per step by one
+RCCL all-gather of the per-rank softmax records.  `value` counts
+K=65536-trajectory MPPI steps per second over the whole job (= N x global
+steps/s).
+
+Launch: python bench.py [--steps K --warmup W]  (N=1), or
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "husky-rover-mppi-isaacsim_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+BYTES_PER_ROLLOUT_STEP = 28   # 6 DEM f32 gathers + 1 costmap f32 gather
+HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
+START = (-60.0, -5.0)
+GOAL = (65.0, 10.0)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--k-per-gpu", type=int, default=65536)
+    ap.add_argument("--horizon", type=int, default=100)
+    ap.add_argument("--proj", default="3d")
+    ap.add_argument("--dem-path", default="auto", choices=["auto", "lds", "global", "ws"])
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
+                    help="bounded oracle sample on the host (rank 0, N=1); 0 disables")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(Z, hw, cm, H, seconds):
+    """Oracle (numpy, float32, one core) on the same workload: whole C3 steps until `seconds` elapse."""
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from oracle import mppi_ref as R
+    K = 65536
+    p = R.Params(K=K, H=H)
+    sc = R.Scene(Z, hw, cm)
+    st = R.State(x=START[0], y=START[1], goal_x=GOAL[0], goal_y=GOAL[1])
+    u1 = np.zeros(H, np.float32)
+    u2 = np.zeros(H, np.float32)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        out = R.mppi_step(p, sc, st, u1, u2, n)
+        u1, u2 = out["u1_opt"], out["u2_opt"]
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 20:
+            break
+    return {"value": n / el, "unit": "MPPI steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} full C3 steps (K={K}, H={H}) of oracle/mppi_ref.py in {el:.1f} s on 1 core "
+                      f"of {cpu_model()} (os.cpu_count()={os.cpu_count()})"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from mppi_amd import _lib, scene
+    Z, hw, cm = scene.scene_c3()
+    H = args.horizon
+    Kl = args.k_per_gpu
+    params = _lib.make_params(Kl, H, k_offset=rank * Kl)
+    eng = _lib.Engine(params, local_rank)
+    eng.set_dem_path(args.dem_path)
+    eng.set_dem(Z, hw)
+    eng.set_costmap(cm, hw)
+    eng.set_state(_lib.make_state(START[0], START[1], (1.0, 0.0, 0.0), goal_x=GOAL[0], goal_y=GOAL[1]))
+
+    if world > 1:
+        stream = torch.cuda.Stream()        # non-default stream shared by the engine and RCCL
+        torch.cuda.set_stream(stream)
+        eng.set_stream(stream.cuda_stream)
+        E = eng.record_len()
+        rec = torch.empty(E, dtype=torch.float64, device="cuda")
+        gathered = torch.empty(world * E, dtype=torch.float64, device="cuda")
+
+        def one_step(i):
+            eng.step_partial(rec.data_ptr(), args.proj, i)
+            dist.all_gather_into_tensor(gathered, rec)
+            eng.step_finish(gathered.data_ptr(), world, copy=False)
+    else:
+        def one_step(i):
+            eng.step(args.proj, i, copy=False)
+
+    for i in range(args.warmup):
+        one_step(i)
+    eng.set_timing(True)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one_step(args.warmup + i)
+    barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    roll_ms, fin_ms, n_roll = eng.timing()
+    info = eng.launch_info()
+
+    if rank == 0:
+        steps_per_s = args.steps / el
+        value = steps_per_s * world * Kl / 65536.0
+        k_avg_ms = roll_ms / max(n_roll, 1)
+        alg_bytes = BYTES_PER_ROLLOUT_STEP * Kl * H
+        achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.pmc_json):
+            try:
+                with open(args.pmc_json) as f:
+                    pm = json.load(f)
+                if pm.get("K") == Kl and pm.get("H") == H:
+                    traffic = pm.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        rec = {
+            "metric": "MPPI steps/sec at K=65536 H=100 on 750x750 costmap; 1/2/4/8-GPU scaling",
+            "value": round(value, 3),
+            "unit": "MPPI steps/s (K=65536-trajectory steps)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (reference crater + obstacle recipes; reference .npy blobs are absent)",
+            "config": {
+                "workload": f"C3: K={Kl} per GPU (global K={Kl * world}), H={H}, 1500^2 DEM @0.1 m, "
+                            f"750^2 costmap @0.2 m, proj={args.proj}, outputs in host memory each step",
+                "global_K": Kl * world,
+                "H": H,
+                "parallelism": f"K-sharded dp{world}, one RCCL all_gather per step" if world > 1 else "single GPU",
+                "rollout_kernel": info,
+                "global_steps_per_s": round(steps_per_s, 3),
+                "finish_kernel_avg_ms": round(fin_ms / max(n_roll, 1), 5),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "mppi_rollout_kernel",
+                "kernel_avg_ms": round(k_avg_ms, 5),
+                "algorithmic_bytes_per_launch": alg_bytes,
+            },
+        }
+        if world == 1 and args.cpu_baseline_seconds > 0:
+            rec["cpu_baseline"] = cpu_baseline(Z, hw, cm, H, args.cpu_baseline_seconds)
+        print(json.dumps(rec), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

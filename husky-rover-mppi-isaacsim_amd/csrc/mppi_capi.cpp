@@ -37,10 +37,12 @@ constexpr size_t kLdsBytes = 160 * 1024;
 
 struct Plan {
   bool lds = false;       // rollout kernel DEM path
+  bool ws = false;        // warp-specialised rollout kernel (chain + side waves)
+  int traj_per_block = 256;
   bool fin_lds = false;   // finish kernel DEM path
   int block = 256, blocks = 0;
   int wx0 = 0, wy0 = 0, W = 1, Wr = 1;
-  size_t lds_bytes = 0, fin_lds_bytes = 0;
+  size_t lds_bytes = 0, fin_lds_bytes = 0, fin_tree_bytes = 0;
   int fin_win_offset = 0;
 };
 
@@ -75,6 +77,8 @@ struct mppi_ctx {
   double* scratch0 = nullptr;
   double* scratch1 = nullptr;
   double* record = nullptr;  // single-rank root record (unused output)
+  float* ustore = nullptr;   // sampled controls of the current step [blocks][2][H][block]
+  size_t ustore_cap = 0;
   float* out_dev = nullptr;
   float* out_host = nullptr;  // pinned
   float* inj1 = nullptr;
@@ -147,14 +151,33 @@ Plan make_plan(const mppi_ctx* c) {
   } else {
     pl.block = 256;
   }
+  pl.traj_per_block = pl.block;
   pl.blocks = (int)((K + pl.block - 1) / pl.block);
   const int NW = pl.block / 64;
-  const size_t scratch = (size_t)NW * (2 * H + 1) * sizeof(double) + NW * sizeof(float);
+  // reduction scratch (mppi_rollout_kernel): w[block] + wave minima, then [leaves][2H+2] doubles
+  const size_t scratch = ((size_t)(pl.block + NW) * sizeof(float) + 15) / 16 * 16 +
+                         (size_t)(NW / 4) * (2 * H + 2) * sizeof(double);
   pl.lds_bytes = std::max(pl.lds ? win : (size_t)0, scratch);
-  // finish kernel: PairScale[1024] (16 B) during the tree, then u_opt[2H] + window
-  pl.fin_win_offset = (int)(((size_t)2 * H * sizeof(float) + 15) / 16 * 16);
-  pl.fin_lds = lds_fits && c->dem_path != 2 && (pl.fin_win_offset + win) <= kLdsBytes;
-  pl.fin_lds_bytes = std::max((size_t)16 * 1024, (size_t)pl.fin_win_offset + (pl.fin_lds ? win : 0));
+  if (c->dem_path == 3 || c->dem_path == 0) {
+    // default: warp-specialised kernel (rings [2][7][TB] + cost[TB] + scratch in LDS, DEM via
+    // L1/L2): measured fastest at C3 (profiles/r01_notes.md)
+    const int TB = WS_TRAJ;
+    pl.ws = true;
+    pl.lds = false;
+    pl.traj_per_block = TB;
+    pl.block = 2 * TB;
+    pl.blocks = (int)((K + TB - 1) / TB);
+    pl.lds_bytes = (size_t)15 * TB * sizeof(float) + ((size_t)(TB + TB / 64) * 4 + 15) / 16 * 16 +
+                   (size_t)(TB / 256) * (2 * H + 2) * sizeof(double);
+  }
+  // finish kernel: tree phase [32][2H+2] doubles + 128*7 PairScale (16 B); tail phase
+  // uo[2H] v[H] w[H] sin[H] cos[H] chain[12H] floats, then the DEM window
+  pl.fin_tree_bytes = (size_t)32 * (2 * H + 2) * sizeof(double) + (size_t)128 * 7 * 16;
+  pl.fin_win_offset = (int)(((size_t)18 * H * sizeof(float) + 15) / 16 * 16);
+  // the optimal rollout stages the window only on request: one workgroup loading 150 KB costs
+  // more than the L2 latency it saves on 100 serial steps (measured, profiles/r01_notes.md)
+  pl.fin_lds = lds_fits && c->dem_path == 1 && (pl.fin_win_offset + win) <= kLdsBytes;
+  pl.fin_lds_bytes = std::max(pl.fin_tree_bytes, (size_t)pl.fin_win_offset + (pl.fin_lds ? win : 0));
   return pl;
 }
 
@@ -242,6 +265,7 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   a.T = p.temperature;
   a.cost_out = c->cost;
   a.nodes = c->nodes;
+  a.ustore = c->ustore;
   a.inj_u1 = c->inj1;
   a.inj_u2 = c->inj2;
 }
@@ -300,6 +324,13 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
   int rc = ensure_nodes(c, pl.blocks);
   if (rc) return rc;
+  const size_t ucount = (size_t)pl.blocks * pl.traj_per_block * 2 * H_of(c);
+  if (ucount > c->ustore_cap) {
+    if (c->ustore) HIP_TRY(hipFree(c->ustore));
+    c->ustore = nullptr;
+    HIP_TRY(hipMalloc(&c->ustore, ucount * sizeof(float)));
+    c->ustore_cap = ucount;
+  }
   RolloutArgs a;
   fill_rollout(c, pl, st, step, unom, a);
   if (dump_args) {
@@ -314,8 +345,11 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   }
   if (pl.blocks == 0) return MPPI_OK;
   if (c->timing && !dump_args) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-  HIP_TRY(launch_rollout(a, pl.block, pl.blocks, pl.lds_bytes, c->stream, pl.lds, proj, mode,
-                         dump_args != nullptr));
+  if (pl.ws)
+    HIP_TRY(launch_rollout_ws(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr));
+  else
+    HIP_TRY(launch_rollout(a, pl.block, pl.blocks, pl.lds_bytes, c->stream, pl.lds, proj, mode,
+                           dump_args != nullptr));
   if (c->timing && !dump_args) {
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     c->ev_roll_pending = true;
@@ -338,7 +372,7 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
     f.scratch1 = c->scratch1;
   }
   if (timed && c->timing) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-  HIP_TRY(launch_finish(f, mode == 0 ? (size_t)16 * 1024 : pl.fin_lds_bytes, c->stream,
+  HIP_TRY(launch_finish(f, mode == 0 ? pl.fin_tree_bytes : pl.fin_lds_bytes, c->stream,
                         mode == 1 && pl.fin_lds));
   if (timed && c->timing) {
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
@@ -404,7 +438,8 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   if (!params || !out) return fail(MPPI_EINVAL, "null argument");
   *out = nullptr;
   const mppi_params& p = *params;
-  if (p.num_iterations < 1) return fail(MPPI_EINVAL, "num_iterations must be >= 1");
+  if (p.num_iterations < 1 || p.num_iterations > 255)
+    return fail(MPPI_EINVAL, "num_iterations must be in [1, 255]");
   if (p.num_trajectories < 0 || p.num_trajectories > ((int64_t)1 << 31) * 64)
     return fail(MPPI_EINVAL, "num_trajectories out of range");
   if (p.k_offset < 0) return fail(MPPI_EINVAL, "k_offset must be >= 0");
@@ -459,6 +494,7 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->scratch0) hipFree(c->scratch0);
   if (c->scratch1) hipFree(c->scratch1);
   if (c->record) hipFree(c->record);
+  if (c->ustore) hipFree(c->ustore);
   if (c->out_dev) hipFree(c->out_dev);
   if (c->out_host) hipHostFree(c->out_host);
   if (c->inj1) hipFree(c->inj1);
@@ -691,7 +727,7 @@ int mppi_get_timing(mppi_ctx* c, double* roll, double* fin, int64_t* n) {
 
 int mppi_set_dem_path(mppi_ctx* c, int32_t mode) {
   if (!c) return fail(MPPI_EINVAL, "null context");
-  if (mode < 0 || mode > 2) return fail(MPPI_EINVAL, "dem path must be 0, 1 or 2");
+  if (mode < 0 || mode > 3) return fail(MPPI_EINVAL, "dem path must be 0, 1, 2 or 3");
   c->dem_path = mode;
   return MPPI_OK;
 }
@@ -699,7 +735,8 @@ int mppi_set_dem_path(mppi_ctx* c, int32_t mode) {
 int mppi_get_launch_info(mppi_ctx* c, int64_t* info, int32_t n) {
   if (!c || !info) return fail(MPPI_EINVAL, "null argument");
   const Plan& pl = c->last_plan;
-  const int64_t v[6] = {pl.lds ? 1 : 0, pl.block, pl.blocks, pl.W, pl.Wr, (int64_t)pl.lds_bytes};
+  const int64_t v[6] = {pl.ws ? 3 : (pl.lds ? 1 : 0), pl.block, pl.blocks, pl.W, pl.Wr,
+                        (int64_t)pl.lds_bytes};
   for (int i = 0; i < n && i < 6; ++i) info[i] = v[i];
   return MPPI_OK;
 }
@@ -712,6 +749,23 @@ int mppi_bilinear_query(mppi_ctx* c, const float* x, const float* y, float* h, i
   if (n == 0) return MPPI_OK;
   HIP_TRY(launch_bilinear(c->Z, c->rows, c->cols, c->x_min, c->y_min, c->res, x, y, h, n, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPPI_OK;
+}
+
+int mppi_selftest(mppi_ctx* c, int32_t what, int64_t n, uint64_t seed, int64_t* mismatches) {
+  if (!c || !mismatches) return fail(MPPI_EINVAL, "null argument");
+  if (what < 0 || what > 1 || n < 0) return fail(MPPI_EINVAL, "bad selftest arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  unsigned long long* d = nullptr;
+  HIP_TRY(hipMalloc(&d, sizeof(*d)));
+  unsigned long long h = 0;
+  hipError_t e = hipMemsetAsync(d, 0, sizeof(*d), c->stream);
+  if (e == hipSuccess) e = launch_selftest(what, n, seed, d, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(d);
+  if (e != hipSuccess) return fail(MPPI_EHIP, std::string("selftest: ") + hipGetErrorString(e));
+  *mismatches = (int64_t)h;
   return MPPI_OK;
 }
 

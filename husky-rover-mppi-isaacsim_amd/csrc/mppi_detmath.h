@@ -84,10 +84,9 @@ MPPI_HD void dm_sincosf(float x, float* s_out, float* c_out) {
   const float ax = fabsf(x);
   int j = (int)(ax * 1.27323954473516f);
   float y = (float)j;
-  if (j & 1) {
-    j += 1;
-    y = y + 1.0f;
-  }
+  const bool odd = (j & 1) != 0;  // branch-free: selects, no divergent blocks
+  j = odd ? j + 1 : j;
+  y = odd ? y + 1.0f : y;
   j &= 7;
   float r = ax - y * 0.78515625f;
   r = r - y * 2.4187564849853515625e-4f;
@@ -108,19 +107,15 @@ MPPI_HD void dm_sincosf(float x, float* s_out, float* c_out) {
   pc = pc * z;
   pc = pc - 0.5f * z;
   pc = pc + 1.0f;
-  const int q = j >> 1;
-  float s, c;
-  if (q == 0) {
-    s = ps;  c = pc;
-  } else if (q == 1) {
-    s = pc;  c = -ps;
-  } else if (q == 2) {
-    s = -ps; c = -pc;
-  } else {
-    s = -pc; c = ps;
-  }
+  // quadrant q = j/2: (sin, cos) = (ps, pc), (pc, -ps), (-ps, -pc), (-pc, ps)
+  const bool swap = (j & 2) != 0;
+  const float s0 = swap ? pc : ps;
+  const float c0 = swap ? ps : pc;
+  const bool sneg = (j & 4) != 0;
+  const bool cneg = ((j >> 1) ^ (j >> 2)) & 1;
+  const float s = sneg ? -s0 : s0;
   *s_out = (x < 0.0f) ? -s : s;
-  *c_out = c;
+  *c_out = cneg ? -c0 : c0;
 }
 
 // ------------------------------------------------------------------ Philox4x32-10

@@ -39,6 +39,7 @@ struct RolloutArgs {
   // outputs
   float* cost_out;   // [K]
   double* nodes;     // [blocks][2H+2]
+  float* ustore;     // [blocks][2][H][block] sampled controls kept for the weighted sum
   // injected controls (MODE 1), trajectory-major [K*H]
   const float* inj_u1;
   const float* inj_u2;
@@ -69,7 +70,12 @@ struct FinishArgs {
 
 hipError_t launch_rollout(const RolloutArgs& a, int block, int blocks, size_t lds, hipStream_t st,
                           bool use_lds, int proj, int mode, bool dump);
+// warp-specialised rollout: 256 trajectories per 512-thread workgroup
+constexpr int WS_TRAJ = 256;
+hipError_t launch_rollout_ws(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
+                             int mode, bool dump);
 hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool use_lds);
+hipError_t launch_selftest(int what, int64_t n, uint64_t seed, unsigned long long* bad, hipStream_t st);
 hipError_t launch_bilinear(const float* Z, int rows, int grid, float x_min, float y_min, float res,
                            const float* xs, const float* ys, float* hs, int64_t n, hipStream_t st);
 

@@ -7,7 +7,7 @@
 //       noise, wheel filter, 2.5D rollout on the DEM (staged once per workgroup
 //       into LDS), the four critics accumulated online, then the workgroup's
 //       softmax leaf records (min, sum w, sum w*u[t]) -> one float64 record per
-//       workgroup.  Nothing per (k, t) touches HBM.
+//       workgroup.  Per (k, t) only the sampled controls touch memory.
 //   mppi_finish_kernel   (#7-#9)  one workgroup; binary tree over the records,
 //       u_opt = V/S, optimal-sequence filter and the 3D rollout of it.
 //
@@ -21,6 +21,90 @@
 #include "mppi_kernels.h"
 
 namespace mppi {
+
+// =====================================================================  exact f32 division / sqrt
+// Every division and square root of a rollout-step is correctly rounded (IEEE
+// binary32, round to nearest even).  Two implementations, selected by the
+// template flag F:
+//   F = false  the IEEE operators `/` and sqrtf (hipcc's generic expansions);
+//   F = true   fast paths that are bit-identical on a checked operand range:
+//     division: the arithmetic of LLVM's AMDGPU fdiv expansion (v_rcp_f32, one
+//       Newton step on the reciprocal, two fma quotient corrections) without its
+//       v_div_scale / v_div_fixup steps, which are the identity when |a|, |b| lie
+//       in [2^-40, 2^40] (a = +-0 handled by a select); the refined reciprocal is
+//       shared by all quotients with one divisor and needs no VCC;
+//     sqrt: LLVM's expansion (v_sqrt_f32 + one-ulp fma correction) without the
+//       small-input scaling, valid for x = 0 or x in [2^-96, 2^128).
+// A fast-path rollout-step ORs "operand outside its range" into a per-lane
+// flag; a flagged lane recomputes the whole step with F = false, so results
+// never depend on the path.  mppi_selftest() checks the fast paths bitwise.
+// kFastMath selects the fast paths in the rollout-steps.  Measured on MI355X
+// (C3, profiles/r01_*): the range guards cost about what the shorter sequences
+// save (rollout kernel 287 us fast vs 250 us IEEE), so the IEEE path is the default.
+constexpr bool kFastMath = false;
+// The serial chain (chain3d) of the warp-specialised rollout and of the optimal
+// rollout is latency-bound: there the VCC-free fast division (three quotients of
+// a normalisation in parallel instead of serialised through VCC) shortens the
+// dependency chain, and its range guards are off the critical path.
+constexpr bool kChainFast = true;
+
+struct Recip {
+  float b, y;
+};
+__device__ __forceinline__ bool div_ok(float v) {
+  const float a = fabsf(v);
+  return a >= 9.094947017729282e-13f && a <= 1.099511627776e12f;  // 2^-40 .. 2^40
+}
+template <bool F>
+__device__ __forceinline__ Recip rc(float b, bool& bad) {
+  Recip r;
+  r.b = b;
+  r.y = 0.0f;
+  if constexpr (F) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    r.y = __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+    bad |= !div_ok(b);
+  }
+  return r;
+}
+template <bool F>
+__device__ __forceinline__ float dv(float a, const Recip& r, bool& bad) {
+  if constexpr (!F) {
+    return a / r.b;
+  } else {
+    const float q0 = a * r.y;
+    const float e0 = __builtin_fmaf(-r.b, q0, a);
+    const float q1 = __builtin_fmaf(e0, r.y, q0);
+    const float e1 = __builtin_fmaf(-r.b, q1, a);
+    const float q2 = __builtin_fmaf(e1, r.y, q1);
+    const bool zero = (a == 0.0f);
+    bad |= !(zero || div_ok(a));
+    return zero ? q0 : q2;  // q0 = a*y carries the IEEE sign of a zero quotient
+  }
+}
+template <bool F>
+__device__ __forceinline__ float dv1(float a, float b, bool& bad) {
+  return dv<F>(a, rc<F>(b, bad), bad);
+}
+// Measured on MI355X (profiles/ubench/lat.hip): the IEEE sqrt expansion has the
+// shorter dependent latency (144 vs 158 cycles), so sq() uses it on both paths.
+constexpr bool kFastSqrt = false;
+template <bool F>
+__device__ __forceinline__ float sq(float x, bool& bad) {
+  if constexpr (!F || !kFastSqrt) {
+    return sqrtf(x);
+  } else {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __builtin_bit_cast(float, __builtin_bit_cast(int, s) - 1);
+    const float sup = __builtin_bit_cast(float, __builtin_bit_cast(int, s) + 1);
+    const float rdn = __builtin_fmaf(-sdn, s, x);
+    const float rup = __builtin_fmaf(-sup, s, x);
+    float out = (rdn <= 0.0f) ? sdn : s;
+    out = (rup > 0.0f) ? sup : out;
+    bad |= !(x == 0.0f || (x >= 1.2621774483536189e-29f && x <= 3.4e38f));  // 2^-96
+    return out;
+  }
+}
 
 // =====================================================================  grid lookups
 // projection_warp.py:39-40 / :338-339 — C-style truncation; clamping is DEFINED
@@ -36,10 +120,35 @@ struct Dem {
   const float* win;  // LDS window (Wr x W), LDS only
   int rows, grid, wx0, wy0, W, Wr;
   float x_min, y_min, res;
+  Recip rres;  // fast-path reciprocal of res (res is validated on the host)
 
-  __device__ __forceinline__ void cell(float x, float y, int& i, int& j) const {
-    i = trunc_clamped((x - x_min) / res, -1.0f, (float)grid);
-    j = -trunc_clamped((y + y_min) / res, -(float)rows, 1.0f);
+  __device__ __forceinline__ void init(const float* Z_, const float* win_, int rows_, int grid_,
+                                       int wx0_, int wy0_, int W_, int Wr_, float x_min_,
+                                       float y_min_, float res_) {
+    Z = Z_;
+    win = win_;
+    rows = rows_;
+    grid = grid_;
+    wx0 = wx0_;
+    wy0 = wy0_;
+    W = W_;
+    Wr = Wr_;
+    x_min = x_min_;
+    y_min = y_min_;
+    res = res_;
+    bool unused = false;
+    rres = rc<true>(res_, unused);
+  }
+  template <bool F>
+  __device__ __forceinline__ Recip rr() const {
+    Recip r = rres;
+    if constexpr (!F) r.b = res;
+    return r;
+  }
+  template <bool F>
+  __device__ __forceinline__ void cell(float x, float y, int& i, int& j, bool& bad) const {
+    i = trunc_clamped(dv<F>(x - x_min, rr<F>(), bad), -1.0f, (float)grid);
+    j = -trunc_clamped(dv<F>(y + y_min, rr<F>(), bad), -(float)rows, 1.0f);
   }
   __device__ __forceinline__ float at(int row, int col) const {
     row = clampi(row, 0, rows - 1);
@@ -53,182 +162,198 @@ struct Dem {
     }
   }
   // projection_warp.py:8-48
-  __device__ __forceinline__ void corners(float x, float y, float& q00, float& q01, float& q10,
-                                          float& q11) const {
+  template <bool F>
+  __device__ __forceinline__ void corners(float x, float y, float (&q)[4], bool& bad) const {
     int i, j;
-    cell(x, y, i, j);
+    cell<F>(x, y, i, j, bad);
     const int r0 = clampi(j, 0, rows - 1), r1 = clampi(j + 1, 0, rows - 1);
     const int c0 = clampi(i, 0, grid - 1), c1 = clampi(i + 1, 0, grid - 1);
     if constexpr (LDS) {
       const int a0 = clampi(r0 - wy0, 0, Wr - 1) * W, a1 = clampi(r1 - wy0, 0, Wr - 1) * W;
       const int b0 = clampi(c0 - wx0, 0, W - 1), b1 = clampi(c1 - wx0, 0, W - 1);
-      q00 = win[a0 + b0];
-      q01 = win[a0 + b1];
-      q10 = win[a1 + b0];
-      q11 = win[a1 + b1];
+      q[0] = win[a0 + b0];
+      q[1] = win[a0 + b1];
+      q[2] = win[a1 + b0];
+      q[3] = win[a1 + b1];
     } else {
-      q00 = Z[(size_t)r0 * grid + c0];
-      q01 = Z[(size_t)r0 * grid + c1];
-      q10 = Z[(size_t)r1 * grid + c0];
-      q11 = Z[(size_t)r1 * grid + c1];
+      q[0] = Z[(size_t)r0 * grid + c0];
+      q[1] = Z[(size_t)r0 * grid + c1];
+      q[2] = Z[(size_t)r1 * grid + c0];
+      q[3] = Z[(size_t)r1 * grid + c1];
     }
   }
-  __device__ __forceinline__ float point(float x, float y) const {
+  template <bool F>
+  __device__ __forceinline__ float point(float x, float y, bool& bad) const {
     int i, j;
-    cell(x, y, i, j);
+    cell<F>(x, y, i, j, bad);
     return at(j, i);
   }
 };
 
 // projection_warp.py:70-100 (trunc; x-fraction paired with the row neighbour q10)
-__device__ __forceinline__ float bilinear(float x, float y, float q00, float q01, float q10,
-                                          float q11, float res) {
-  const float xn = x / res, yn = y / res;
+template <bool F>
+__device__ __forceinline__ float bilinear(float x, float y, const float (&q)[4], const Recip& rres,
+                                          bool& bad) {
+  const float xn = dv<F>(x, rres, bad), yn = dv<F>(y, rres, bad);
   const float x2 = xn - truncf(xn), y2 = yn - truncf(yn);
-  const float a = ((1.0f - x2) * (1.0f - y2)) * q00;
-  const float b = (x2 * (1.0f - y2)) * q10;
-  const float c = ((1.0f - x2) * y2) * q01;
-  const float d = (x2 * y2) * q11;
+  const float a = ((1.0f - x2) * (1.0f - y2)) * q[0];
+  const float b = (x2 * (1.0f - y2)) * q[2];
+  const float c = ((1.0f - x2) * y2) * q[1];
+  const float d = (x2 * y2) * q[3];
   return ((a + b) + c) + d;
 }
 
-struct Cost {  // critics_warp.py accumulators
-  float pf_sum, sw, sp, ob, last_x, last_y;
-};
+__device__ __forceinline__ float clampf(float x, float lo, float hi) {
+  return fminf(fmaxf(x, lo), hi);
+}
 
 // =====================================================================  one rollout-step
-// State of one trajectory between steps.
-struct Traj {
-  float x, y;         // position[tid]
-  float hx, hy, hz;   // `previous` heading
-  float lwx, lwy, lwz, rwx, rwy, rwz;   // wheel points of the last even step (slope critic)
+struct Traj {                 // state of one trajectory between steps
+  float x, y;                 // position[tid]
+  float hx, hy, hz;           // `previous` heading
 };
 
 struct StepOut {
-  float z;                              // trajectory height
-  float lx, ly, lz, rx, ry, rz;         // wheel points
+  float z;                         // trajectory height
+  float lx, ly, lz, rx, ry, rz;    // wheel points
 };
 
-// 3D step: projection_warp.py:312-350 (loop body of _generate_trajectories_kernel).
-template <bool LDS>
-__device__ __forceinline__ void step3d(const Dem<LDS>& dem, float res_half_neg, float res_sq,
-                                       float dt, float off, float v, float w, Traj& s,
-                                       StepOut& o) {
-  // _update_position :207-223
-  {
-    const float nrm = sqrtf((s.hx * s.hx + s.hy * s.hy) + s.hz * s.hz);
-    const float ux = s.hx / nrm, uy = s.hy / nrm;
+// Serial part of one 3D rollout-step (projection_warp.py:314-326): position
+// update, corner lookup, normal, tangent projection, Rodrigues yaw.  (sn, cs)
+// = dm_sincosf(w*dt).  Leaves the new heading in s and the quad / normal in q, n.
+template <bool F, bool LDS>
+__device__ __forceinline__ void chain3d(const Dem<LDS>& dem, float res_half_neg, float res_sq,
+                                        float dt, float v, float sn, float cs, Traj& s,
+                                        float (&q)[4], float& nx, float& ny, float& nz, bool& bad) {
+  {  // _update_position :207-223
+    const Recip r = rc<F>(sq<F>((s.hx * s.hx + s.hy * s.hy) + s.hz * s.hz, bad), bad);
+    const float ux = dv<F>(s.hx, r, bad), uy = dv<F>(s.hy, r, bad);
     s.x = s.x + (ux * v) * dt;
     s.y = s.y + (uy * v) * dt;
   }
-  float q00, q01, q10, q11;
-  dem.corners(s.x, s.y, q00, q01, q10, q11);
-  o.z = bilinear(s.x, s.y, q00, q01, q10, q11, dem.res);
-  // _normal_on_grid :129-151
-  const float vx = res_half_neg * (((q01 - q00) - q10) + q11);
-  const float vy = res_half_neg * (((q10 - q00) - q01) + q11);
-  const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
-  const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
-  // _get_heading_tangent_vector :168-190
+  dem.template corners<F>(s.x, s.y, q, bad);
+  {  // _normal_on_grid :129-151
+    const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
+    const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
+    const Recip r = rc<F>(sq<F>((vx * vx + vy * vy) + res_sq * res_sq, bad), bad);
+    nx = dv<F>(vx, r, bad);
+    ny = dv<F>(vy, r, bad);
+    nz = dv<F>(res_sq, r, bad);
+  }
   float tx, ty, tz;
-  {
+  {  // _get_heading_tangent_vector :168-190
     const float d = (s.hx * nx + s.hy * ny) + s.hz * nz;
     tx = s.hx - d * nx;
     ty = s.hy - d * ny;
     tz = s.hz - d * nz;
-    const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
-    tx = tx / tn;
-    ty = ty / tn;
-    tz = tz / tn;
+    const Recip r = rc<F>(sq<F>((tx * tx + ty * ty) + tz * tz, bad), bad);
+    tx = dv<F>(tx, r, bad);
+    ty = dv<F>(ty, r, bad);
+    tz = dv<F>(tz, r, bad);
   }
-  // _update_orientation :225-248 (Rodrigues about n)
-  {
-    const float on = sqrtf((tx * tx + ty * ty) + tz * tz);
-    const float ox = tx / on, oy = ty / on, oz = tz / on;
-    float sn, cs;
-    dm_sincosf(w * dt, &sn, &cs);
+  {  // _update_orientation :225-248 (Rodrigues about n)
+    const Recip ro = rc<F>(sq<F>((tx * tx + ty * ty) + tz * tz, bad), bad);
+    const float ox = dv<F>(tx, ro, bad), oy = dv<F>(ty, ro, bad), oz = dv<F>(tz, ro, bad);
     const float crx = ny * oz - nz * oy, cry = nz * ox - nx * oz, crz = nx * oy - ny * ox;
     const float dn = (nx * ox + ny * oy) + nz * oz;
     const float omc = 1.0f - cs;
     const float rx = (ox * cs + crx * sn) + (nx * dn) * omc;
     const float ry = (oy * cs + cry * sn) + (ny * dn) * omc;
     const float rz = (oz * cs + crz * sn) + (nz * dn) * omc;
-    const float rn = sqrtf((rx * rx + ry * ry) + rz * rz);
-    s.hx = rx / rn;
-    s.hy = ry / rn;
-    s.hz = rz / rn;
+    const Recip r = rc<F>(sq<F>((rx * rx + ry * ry) + rz * rz, bad), bad);
+    s.hx = dv<F>(rx, r, bad);
+    s.hy = dv<F>(ry, r, bad);
+    s.hz = dv<F>(rz, r, bad);
   }
-  // wheels :333-348, right = offset * cross(normal, current_hv)
-  const float cx = off * (ny * s.hz - nz * s.hy);
-  const float cy = off * (nz * s.hx - nx * s.hz);
-  o.lx = s.x + cx;
-  o.ly = s.y + cy;
-  o.lz = dem.point(o.lx, o.ly);
-  o.rx = s.x - cx;
-  o.ry = s.y - cy;
-  o.rz = dem.point(o.rx, o.ry);
+}
+
+// Height and wheel contacts of a rollout-step (projection_warp.py:318, :333-348),
+// right = offset * cross(normal, current_hv).
+template <bool F, bool LDS>
+__device__ __forceinline__ void wheels3d(const Dem<LDS>& dem, float off, float x, float y,
+                                         const float (&q)[4], float nx, float ny, float nz,
+                                         float hx, float hy, float hz, StepOut& o, bool& bad) {
+  o.z = bilinear<F>(x, y, q, dem.template rr<F>(), bad);
+  const float cx = off * (ny * hz - nz * hy);
+  const float cy = off * (nz * hx - nx * hz);
+  o.lx = x + cx;
+  o.ly = y + cy;
+  o.lz = dem.template point<F>(o.lx, o.ly, bad);
+  o.rx = x - cx;
+  o.ry = y - cy;
+  o.rz = dem.template point<F>(o.rx, o.ry, bad);
 }
 
 // 2D step: projection_warp.py:373-382 (wheels DEFINED as zero).
-template <bool LDS>
-__device__ __forceinline__ void step2d(const Dem<LDS>& dem, float dt, float v, float w, Traj& s,
-                                       StepOut& o) {
+template <bool F, bool LDS>
+__device__ __forceinline__ void step2d(const Dem<LDS>& dem, float dt, float v, float sn, float cs,
+                                       Traj& s, StepOut& o, bool& bad) {
   {
-    const float nrm = sqrtf((s.hx * s.hx + s.hy * s.hy) + s.hz * s.hz);
-    const float ux = s.hx / nrm, uy = s.hy / nrm;
+    const Recip r = rc<F>(sq<F>((s.hx * s.hx + s.hy * s.hy) + s.hz * s.hz, bad), bad);
+    const float ux = dv<F>(s.hx, r, bad), uy = dv<F>(s.hy, r, bad);
     s.x = s.x + (ux * v) * dt;
     s.y = s.y + (uy * v) * dt;
   }
   {  // _update_orientation_2D :251-275
-    float sn, cs;
-    dm_sincosf(w * dt, &sn, &cs);
     float nx = cs * s.hx - sn * s.hy;
     float ny = sn * s.hx + cs * s.hy;
-    const float nrm = sqrtf(nx * nx + ny * ny);
+    const float nrm = sq<F>(nx * nx + ny * ny, bad);
     if (nrm > 0.0f) {
-      nx = nx / nrm;
-      ny = ny / nrm;
+      const Recip r = rc<F>(nrm, bad);
+      nx = dv<F>(nx, r, bad);
+      ny = dv<F>(ny, r, bad);
     }
     s.hx = nx;
     s.hy = ny;
     s.hz = 0.0f;
   }
-  float q00, q01, q10, q11;
-  dem.corners(s.x, s.y, q00, q01, q10, q11);
-  o.z = bilinear(s.x, s.y, q00, q01, q10, q11, dem.res);
+  float q[4];
+  dem.template corners<F>(s.x, s.y, q, bad);
+  o.z = bilinear<F>(s.x, s.y, q, dem.template rr<F>(), bad);
   o.lx = o.ly = o.lz = o.rx = o.ry = o.rz = 0.0f;
 }
 
 // critics_warp.py:190-218, term for points (t, t+2) of both wheels.
+template <bool F>
 __device__ __forceinline__ float slope_term(float plx, float ply, float plz, float clx, float cly,
                                             float clz, float prx, float pry, float prz, float crx,
-                                            float cry, float crz) {
+                                            float cry, float crz, bool& bad) {
   const float eps = 1e-6f;
   const float dzl = clz - plz;
   const float dxl = clx - plx, dyl = cly - ply;
-  const float dl = sqrtf(dxl * dxl + dyl * dyl);
+  const float dl = sq<F>(dxl * dxl + dyl * dyl, bad);
   const float dzr = crz - prz;
   const float dxr = crx - prx, dyr = cry - pry;
-  const float dr = sqrtf(dxr * dxr + dyr * dyr);
-  const float ratl = fabsf(dzl / (dl + eps));
-  const float ratr = fabsf(dzr / (dr + eps));
+  const float dr = sq<F>(dxr * dxr + dyr * dyr, bad);
+  const float ratl = fabsf(dv1<F>(dzl, dl + eps, bad));
+  const float ratr = fabsf(dv1<F>(dzr, dr + eps, bad));
   const float al = 1.0f + 5.0f * ratl;
   const float ar = 1.0f + 5.0f * ratr;
   const float ls = al * al, rs = ar * ar;
   return (ls > rs) ? ls : rs;
 }
 
-// critics_warp.py:244-253
-__device__ __forceinline__ float costmap_at(const float* cm, int size, float hw, float res_c,
-                                            float x, float y) {
-  const int ix = clampi(trunc_clamped((x + hw) / res_c, -1.0f, (float)size), 0, size - 1);
-  const int iy = clampi(trunc_clamped(((-y) + hw) / res_c, -1.0f, (float)size), 0, size - 1);
-  return cm[ix + size * iy];
+// critics_warp.py:244-248 costmap index (clamped, DEFINED)
+template <bool F>
+__device__ __forceinline__ int costmap_index(int size, float hw, const Recip& rres_c, float x,
+                                             float y, bool& bad) {
+  const int ix = clampi(trunc_clamped(dv<F>(x + hw, rres_c, bad), -1.0f, (float)size), 0, size - 1);
+  const int iy = clampi(trunc_clamped(dv<F>((-y) + hw, rres_c, bad), -1.0f, (float)size), 0, size - 1);
+  return ix + size * iy;
 }
 
-__device__ __forceinline__ float clampf(float x, float lo, float hi) {
-  return fminf(fmaxf(x, lo), hi);
+#ifdef MPPI_STAMPS
+// Diagnostic build only (profiles/ubench/stamps.sh): per-wave cycle stamps.
+__device__ uint64_t g_dbg_stamps[64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2];
+__device__ __forceinline__ uint64_t dbg_stamp() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
 }
+extern "C" int mppi_debug_stamps(uint64_t* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dbg_stamps), n * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 // =====================================================================  reductions
 __device__ __forceinline__ float wave_min(float v) {
@@ -274,6 +399,72 @@ __device__ __forceinline__ double pair_apply(const PairScale& p, double a, doubl
 }
 
 // =====================================================================  rollout kernel
+// Everything one trajectory carries from step to step.
+struct Lane {
+  Traj s;
+  float L, R;                                  // wheel filter state
+  float pf_sum, sw, sp, ob, last_x, last_y;    // critic accumulators
+  float lwx, lwy, lwz, rwx, rwy, rwz;          // wheel points of the last even step
+  float cm_pend;                               // costmap value gathered in the previous step
+};
+
+// Constants of one rollout launch that every step reads.
+template <bool LDS>
+struct StepCtx {
+  const RolloutArgs* a;
+  Dem<LDS> dem;
+  Recip rres_c, rwheel, rT;  // fast-path reciprocals (operands validated on the host)
+  float res_half_neg, res_sq, one_m_fa;
+};
+
+// One rollout-step of one trajectory: filter (sampling_warp.py:120-138), the
+// 3D/2D projection step, and the online critics (critics_warp.py:85-300).
+// Returns the costmap index this step gathers (the value is accumulated next step).
+template <bool F, bool LDS, int PROJ>
+__device__ __forceinline__ int rollout_step(const StepCtx<LDS>& k, int t, float u1, float u2,
+                                            Lane& l, StepOut& o, float& v, float& w, bool& bad) {
+  const RolloutArgs& a = *k.a;
+  Recip rw = k.rwheel, rcm = k.rres_c;
+  if constexpr (!F) {
+    rw.b = a.rwheel;
+    rcm.b = a.res_c;
+  }
+  l.L = l.L * a.fa + (u1 * a.fk) * k.one_m_fa;
+  l.R = l.R * a.fa + (u2 * a.fk) * k.one_m_fa;
+  v = clampf((l.L + l.R) / 2.0f, a.vmin, a.vmax);
+  w = clampf(dv<F>((-l.L) + l.R, rw, bad), a.wmin, a.wmax);
+  float sn, cs;
+  dm_sincosf(w * a.dt, &sn, &cs);
+  if constexpr (PROJ == 3) {
+    float q[4], nx, ny, nz;
+    chain3d<F, LDS>(k.dem, k.res_half_neg, k.res_sq, a.dt, v, sn, cs, l.s, q, nx, ny, nz, bad);
+    wheels3d<F, LDS>(k.dem, a.off, l.s.x, l.s.y, q, nx, ny, nz, l.s.hx, l.s.hy, l.s.hz, o, bad);
+  } else {
+    step2d<F, LDS>(k.dem, a.dt, v, sn, cs, l.s, o, bad);
+  }
+  // _path_follow_critic sum branch (:125-126) over t < H-1; last point (:116)
+  if (t < a.H - 1) l.pf_sum = l.pf_sum + 10.0f * (fabsf(l.s.x - a.gx) + fabsf(l.s.y - a.gy));
+  l.last_x = l.s.x;
+  l.last_y = l.s.y;
+  // _avoid_slope_wheels (:190-216): terms (i, i+2) for even i < H-3
+  if ((t & 1) == 0) {
+    if (t >= 2 && t - 2 < a.H - 3)
+      l.sw = l.sw + slope_term<F>(l.lwx, l.lwy, l.lwz, o.lx, o.ly, o.lz, l.rwx, l.rwy, l.rwz, o.rx,
+                                  o.ry, o.rz, bad);
+    l.lwx = o.lx; l.lwy = o.ly; l.lwz = o.lz;
+    l.rwx = o.rx; l.rwy = o.ry; l.rwz = o.rz;
+  }
+  // _maximise_speed (:296-297)
+  if (a.speed_on) l.sp = l.sp + dv1<F>(a.vmax - v, v + 0.0001f, bad);
+  return costmap_index<F>(a.cm_size, a.hw, rcm, l.s.x, l.s.y, bad);
+}
+
+__device__ __forceinline__ void add_obstacle(const RolloutArgs& a, Lane& l, float cm) {
+  // _avoid_obstacle (critics_warp.py:251-253)
+  if (cm > a.thr) l.ob = l.ob + a.pen;
+  l.ob = l.ob + cm;
+}
+
 template <int BLOCK, bool LDS, int PROJ, int MODE, bool DUMP>
 __global__ __launch_bounds__(BLOCK) void mppi_rollout_kernel(const RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -292,93 +483,80 @@ __global__ __launch_bounds__(BLOCK) void mppi_rollout_kernel(const RolloutArgs a
     }
     __syncthreads();
   }
-  Dem<LDS> dem;
-  dem.Z = a.Z;
-  dem.win = win;
-  dem.rows = a.rows;
-  dem.grid = a.grid;
-  dem.wx0 = a.wx0;
-  dem.wy0 = a.wy0;
-  dem.W = a.W;
-  dem.Wr = a.Wr;
-  dem.x_min = a.x_min;
-  dem.y_min = a.y_min;
-  dem.res = a.res;
+  StepCtx<LDS> k;
+  k.a = &a;
+  k.dem.init(a.Z, win, a.rows, a.grid, a.wx0, a.wy0, a.W, a.Wr, a.x_min, a.y_min, a.res);
+  {
+    bool unused = false;
+    k.rres_c = rc<true>(a.res_c, unused);
+    k.rwheel = rc<true>(a.rwheel, unused);
+    k.rT = rc<true>(a.T, unused);
+  }
+  k.res_half_neg = (-a.res) / 2.0f;
+  k.res_sq = a.res * a.res;
+  k.one_m_fa = 1.0f - a.fa;
 
   const int64_t kl = (int64_t)blockIdx.x * BLOCK + tid;  // shard-local trajectory
   const bool valid = kl < a.K;
   const uint64_t kg = (uint64_t)(a.k_offset + kl);         // global trajectory (Philox subsequence)
   const int H = a.H;
-  const float res_half_neg = (-a.res) / 2.0f;
-  const float res_sq = a.res * a.res;
-  const float one_m_fa = 1.0f - a.fa;
 
-  // ---- initial projection at the robot pose (projection_warp.py:306-310)
-  Traj s;
-  s.x = a.x0;
-  s.y = a.y0;
+  // ---- initial projection at the robot pose (projection_warp.py:306-310), IEEE operators
+  Lane l;
+  l.s.x = a.x0;
+  l.s.y = a.y0;
   {
-    float q00, q01, q10, q11;
-    dem.corners(s.x, s.y, q00, q01, q10, q11);
-    const float vx = res_half_neg * (((q01 - q00) - q10) + q11);
-    const float vy = res_half_neg * (((q10 - q00) - q01) + q11);
-    const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
-    const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
+    bool unused = false;
+    float q[4];
+    k.dem.template corners<false>(l.s.x, l.s.y, q, unused);
+    const float vx = k.res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
+    const float vy = k.res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
+    const float nn = sqrtf((vx * vx + vy * vy) + k.res_sq * k.res_sq);
+    const float nx = vx / nn, ny = vy / nn, nz = k.res_sq / nn;
     if constexpr (PROJ == 3) {
       const float d = (a.h0x * nx + a.h0y * ny) + a.h0z * nz;
-      float tx = a.h0x - d * nx, ty = a.h0y - d * ny, tz = a.h0z - d * nz;
+      const float tx = a.h0x - d * nx, ty = a.h0y - d * ny, tz = a.h0z - d * nz;
       const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
-      s.hx = tx / tn;
-      s.hy = ty / tn;
-      s.hz = tz / tn;
+      l.s.hx = tx / tn;
+      l.s.hy = ty / tn;
+      l.s.hz = tz / tn;
     } else {
-      s.hx = a.h0x;
-      s.hy = a.h0y;
-      s.hz = a.h0z;
+      l.s.hx = a.h0x;
+      l.s.hy = a.h0y;
+      l.s.hz = a.h0z;
     }
   }
-  s.lwx = s.lwy = s.lwz = s.rwx = s.rwy = s.rwz = 0.0f;
+  l.L = a.wl;
+  l.R = a.wr;
+  l.pf_sum = l.sw = l.sp = l.ob = 0.0f;
+  l.last_x = l.s.x;
+  l.last_y = l.s.y;
+  l.lwx = l.lwy = l.lwz = l.rwx = l.rwy = l.rwz = 0.0f;
+  l.cm_pend = 0.0f;
 
-  Cost c;
-  c.pf_sum = c.sw = c.sp = c.ob = 0.0f;
-  c.last_x = s.x;
-  c.last_y = s.y;
-  float L = a.wl, R = a.wr;
+  // sampled controls are kept for the weighted sum: [ch][t][BLOCK] per workgroup (coalesced)
+  float* ust = a.ustore + (size_t)blockIdx.x * (2 * H) * BLOCK + tid;
 
   auto one_step = [&](int t, float u1, float u2) {
-    // _convert_inputs_to_velocities (sampling_warp.py:120-138)
-    L = L * a.fa + (u1 * a.fk) * one_m_fa;
-    R = R * a.fa + (u2 * a.fk) * one_m_fa;
-    const float v = clampf((L + R) / 2.0f, a.vmin, a.vmax);
-    const float w = clampf(((-L) + R) / a.rwheel, a.wmin, a.wmax);
+    ust[(size_t)t * BLOCK] = u1;
+    ust[(size_t)(H + t) * BLOCK] = u2;
+    const Lane saved = l;
     StepOut o;
-    if constexpr (PROJ == 3)
-      step3d<LDS>(dem, res_half_neg, res_sq, a.dt, a.off, v, w, s, o);
-    else
-      step2d<LDS>(dem, a.dt, v, w, s, o);
-    // _path_follow_critic sum branch (:125-126) over t < H-1; last point (:116)
-    if (t < H - 1) c.pf_sum = c.pf_sum + 10.0f * (fabsf(s.x - a.gx) + fabsf(s.y - a.gy));
-    c.last_x = s.x;
-    c.last_y = s.y;
-    // _avoid_slope_wheels (:190-216): terms (i, i+2) for even i < H-3
-    if ((t & 1) == 0) {
-      if (t >= 2 && t - 2 < H - 3)
-        c.sw = c.sw + slope_term(s.lwx, s.lwy, s.lwz, o.lx, o.ly, o.lz, s.rwx, s.rwy, s.rwz, o.rx,
-                                 o.ry, o.rz);
-      s.lwx = o.lx; s.lwy = o.ly; s.lwz = o.lz;
-      s.rwx = o.rx; s.rwy = o.ry; s.rwz = o.rz;
+    float v, w;
+    bool bad = false;
+    int cidx = rollout_step<kFastMath, LDS, PROJ>(k, t, u1, u2, l, o, v, w, bad);
+    if (kFastMath && __builtin_expect(bad, 0)) {  // an operand left the fast-path range: redo with IEEE ops
+      l = saved;
+      cidx = rollout_step<false, LDS, PROJ>(k, t, u1, u2, l, o, v, w, bad);
     }
-    // _maximise_speed (:296-297)
-    if (a.speed_on) c.sp = c.sp + (a.vmax - v) / (v + 0.0001f);
-    // _avoid_obstacle (:244-253)
-    const float cm = costmap_at(a.cm, a.cm_size, a.hw, a.res_c, s.x, s.y);
-    if (cm > a.thr) c.ob = c.ob + a.pen;
-    c.ob = c.ob + cm;
+    // the costmap value gathered in step t is accumulated in step t+1 (latency hiding)
+    if (t > 0) add_obstacle(a, l, l.cm_pend);
+    l.cm_pend = a.cm[cidx];
     if constexpr (DUMP) {
       if (valid) {
         const size_t o3 = ((size_t)kl * H + t) * 3;
-        if (a.d_traj) { a.d_traj[o3] = s.x; a.d_traj[o3 + 1] = s.y; a.d_traj[o3 + 2] = o.z; }
-        if (a.d_hv) { a.d_hv[o3] = s.hx; a.d_hv[o3 + 1] = s.hy; a.d_hv[o3 + 2] = s.hz; }
+        if (a.d_traj) { a.d_traj[o3] = l.s.x; a.d_traj[o3 + 1] = l.s.y; a.d_traj[o3 + 2] = o.z; }
+        if (a.d_hv) { a.d_hv[o3] = l.s.hx; a.d_hv[o3 + 1] = l.s.hy; a.d_hv[o3 + 2] = l.s.hz; }
         if (a.d_lw) { a.d_lw[o3] = o.lx; a.d_lw[o3 + 1] = o.ly; a.d_lw[o3 + 2] = o.lz; }
         if (a.d_rw) { a.d_rw[o3] = o.rx; a.d_rw[o3 + 1] = o.ry; a.d_rw[o3 + 2] = o.rz; }
         const size_t o1 = (size_t)kl * H + t;
@@ -414,247 +592,744 @@ __global__ __launch_bounds__(BLOCK) void mppi_rollout_kernel(const RolloutArgs a
     one_step(t, u1a, u2a);
     if (t + 1 < H) one_step(t + 1, u1b, u2b);
   }
+  add_obstacle(a, l, l.cm_pend);
 
   // ---- _evaluate_trajectories_kernel (critics_warp.py:325-329), costs[] zeroed by reset
   float pf;
   if (a.pf_far) {
-    const float dx = c.last_x - a.igx, dy = c.last_y - a.igy;
+    const float dx = l.last_x - a.igx, dy = l.last_y - a.igy;
     pf = (dx * dx + dy * dy) * a.pf_scale;
   } else {
-    pf = c.pf_sum;
+    pf = l.pf_sum;
   }
   float cost = a.w_path * pf;
-  cost = cost + a.w_slope * c.sw;
-  cost = cost + a.w_speed * c.sp;
-  cost = cost + a.w_obs * c.ob;
+  cost = cost + a.w_slope * l.sw;
+  cost = cost + a.w_speed * l.sp;
+  cost = cost + a.w_obs * l.ob;
   if (valid) a.cost_out[kl] = cost;
 
   // ---- softmax leaf records (DEFINED replacement of critics_warp.py:338-376)
+  // Leaf = 256 trajectories = 4 waves.  m = leaf min, w = dm_expf(-(c-m)/T),
+  // record [m, S, V1[H], V2[H]] with each sum over the leaf taken as
+  //   a_l = (x[l] + x[64+l]) + (x[128+l] + x[192+l])   (float64, l = lane)
+  //   sum = xor-butterfly over the 64 lanes of a_l.
   __syncthreads();  // LDS window no longer needed: reuse it as reduction scratch
+  constexpr int NL = NW / 4;
   const int E = 2 * H + 2;
-  double* red = reinterpret_cast<double*>(smem_raw);     // [NW][2H+1]
-  float* leaf_m = reinterpret_cast<float*>(red + NW * (2 * H + 1));  // [NW/4]
+  float* wbuf = reinterpret_cast<float*>(smem_raw);            // [BLOCK]
+  float* wave_m = wbuf + BLOCK;                                  // [NW]
+  double* red = reinterpret_cast<double*>(smem_raw + ((BLOCK + NW) * 4 + 15) / 16 * 16);  // [NL][E]
   const float cval = valid ? cost : INFINITY;
-  float wm = wave_min(cval);
-  if (lane == 0) leaf_m[wave] = wm;  // temporarily per wave
+  {
+    const float wm = wave_min(cval);
+    if (lane == 0) wave_m[wave] = wm;
+  }
   __syncthreads();
   const int leaf = wave >> 2;
-  const float m_leaf =
-      fminf(fminf(leaf_m[4 * leaf], leaf_m[4 * leaf + 1]), fminf(leaf_m[4 * leaf + 2], leaf_m[4 * leaf + 3]));
-  const bool finite = cval < INFINITY;
-  const float wgt = finite ? dm_expf(-((cval - m_leaf) / a.T)) : 0.0f;
-  const double wd = (double)wgt;
+  const float m_leaf = fminf(fminf(wave_m[4 * leaf], wave_m[4 * leaf + 1]),
+                             fminf(wave_m[4 * leaf + 2], wave_m[4 * leaf + 3]));
   {
-    const double sw = wave_sum(wd);
-    if (lane == 0) red[wave * (2 * H + 1) + 2 * H] = sw;
+    float wgt = 0.0f;
+    if (cval < INFINITY) {
+      bool bad = false;
+      float x = dv<true>(cval - m_leaf, k.rT, bad);
+      if (bad) x = (cval - m_leaf) / a.T;
+      wgt = dm_expf(-x);
+    }
+    wbuf[tid] = wgt;
   }
-  // regenerate u[k,t] (bitwise identical to the rollout) and reduce w*u per t
-  for (int t = 0; t < H; t += 2) {
-    float u1a, u2a, u1b, u2b;
-    if constexpr (MODE == 0) {
-      float e1a, e2a, e1b, e2b;
-      noise_block(a.seed, a.n_base + (uint64_t)(t >> 1), kg, &e1a, &e2a, &e1b, &e2b);
-      sample(t, e1a, e2a, u1a, u2a);
-      sample(t + 1, e1b, e2b, u1b, u2b);
-    } else {
-      const size_t o = (size_t)(valid ? kl : 0) * H + t;
-      u1a = a.inj_u1[o];
-      u2a = a.inj_u2[o];
-      u1b = (t + 1 < H) ? a.inj_u1[o + 1] : 0.0f;
-      u2b = (t + 1 < H) ? a.inj_u2[o + 1] : 0.0f;
-    }
-    const double p1a = wave_sum(wd * (double)u1a);
-    const double p2a = wave_sum(wd * (double)u2a);
-    if (lane == 0) {
-      red[wave * (2 * H + 1) + t] = p1a;
-      red[wave * (2 * H + 1) + H + t] = p2a;
-    }
-    if (t + 1 < H) {
-      const double p1b = wave_sum(wd * (double)u1b);
-      const double p2b = wave_sum(wd * (double)u2b);
-      if (lane == 0) {
-        red[wave * (2 * H + 1) + t + 1] = p1b;
-        red[wave * (2 * H + 1) + H + t + 1] = p2b;
+  __syncthreads();  // wbuf complete; ustore rows written by other waves are ordered by the barrier
+  {
+    const int wl = wave & 3;  // this wave's share of the leaf's rows
+    const float* wl4 = wbuf + 256 * leaf + lane;
+    const double w0 = (double)wl4[0], w1 = (double)wl4[64], w2 = (double)wl4[128], w3 = (double)wl4[192];
+    const float* ub = a.ustore + (size_t)blockIdx.x * (2 * H) * BLOCK + 256 * leaf + lane;
+    for (int j = 1 + wl; j < E; j += 4) {
+      double x0 = w0, x1 = w1, x2 = w2, x3 = w3;   // j == 1: S = sum w
+      if (j >= 2) {
+        const float* u = ub + (size_t)(j - 2) * BLOCK;
+        x0 = w0 * (double)u[0];
+        x1 = w1 * (double)u[64];
+        x2 = w2 * (double)u[128];
+        x3 = w3 * (double)u[192];
       }
+      const double sum = wave_sum((x0 + x1) + (x2 + x3));
+      if (lane == 0) red[leaf * E + j] = sum;
     }
   }
+  if (tid < NL) red[tid * E] = 0.0;
   __syncthreads();
-  // leaf records: ((W0 + W1) + (W2 + W3)); then the block's subtree over its leaves
-  constexpr int NL = NW / 4;
+  // the block's subtree over its NL leaves (oracle/mppi_ref.py tree_reduce order)
   for (int j = tid; j < E; j += BLOCK) {
     double val[NL];
     float lm[NL];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) {
-      lm[l] = fminf(fminf(leaf_m[4 * l], leaf_m[4 * l + 1]), fminf(leaf_m[4 * l + 2], leaf_m[4 * l + 3]));
-      if (j == 0) {
-        val[l] = (double)lm[l];
-      } else {
-        const int jj = (j == 1) ? 2 * H : j - 2;  // record [m, S, V1, V2] <- red [V1, V2, S]
-        const double* rr = red + (4 * l) * (2 * H + 1) + jj;
-        const int st = 2 * H + 1;
-        val[l] = (rr[0] + rr[st]) + (rr[2 * st] + rr[3 * st]);
-      }
+    for (int q = 0; q < NL; ++q) {
+      lm[q] = fminf(fminf(wave_m[4 * q], wave_m[4 * q + 1]), fminf(wave_m[4 * q + 2], wave_m[4 * q + 3]));
+      val[q] = (j == 0) ? (double)lm[q] : red[q * E + j];
     }
 #pragma unroll
     for (int width = NL; width > 1; width >>= 1) {
 #pragma unroll
-      for (int l = 0; l < width / 2; ++l) {
-        const PairScale ps = pair_scale(lm[2 * l], lm[2 * l + 1], a.T);
-        val[l] = pair_apply(ps, val[2 * l], val[2 * l + 1], j);
-        lm[l] = ps.m;  // fminf(m, +inf) = m covers the empty-child modes
+      for (int q = 0; q < width / 2; ++q) {
+        const PairScale ps = pair_scale(lm[2 * q], lm[2 * q + 1], a.T);
+        val[q] = pair_apply(ps, val[2 * q], val[2 * q + 1], j);
+        lm[q] = ps.m;  // fminf(m, +inf) = m covers the empty-child modes
       }
     }
     a.nodes[(size_t)blockIdx.x * E + j] = val[0];
   }
 }
 
+// =====================================================================  leaf records (shared)
+// Softmax leaf records (DEFINED replacement of critics_warp.py:338-376) for the
+// TB trajectories of a workgroup, whose costs are in cost_lds[TB] and sampled
+// controls in ustore rows [2H][TB].  Leaf = 256 trajectories.
+//   m = leaf min, w = dm_expf(-(c - m)/T),
+//   record [m, S, V1[H], V2[H]], each sum over the leaf taken as
+//   a_l = (x[l] + x[64+l]) + (x[128+l] + x[192+l])  (float64, l = lane),
+//   then the xor-butterfly over the 64 lanes of a_l;
+// then the workgroup's subtree over its TB/256 leaves (tree_reduce order).
+// Called by all NT threads; `scratch` is LDS of at least
+// TB*4 + TB/64*4 (rounded to 16) + TB/256*(2H+2)*8 bytes.
+template <int TB, int NT>
+__device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
+                                             unsigned char* scratch, const float* ub_block) {
+  constexpr int NL = TB / 256;
+  constexpr int NWL = TB / 64;   // waves' worth of trajectories
+  constexpr int NWAVES = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H, E = 2 * H + 2;
+  float* wbuf = reinterpret_cast<float*>(scratch);                           // [TB]
+  float* wave_m = wbuf + TB;                                                 // [NWL]
+  double* red = reinterpret_cast<double*>(scratch + ((TB + NWL) * 4 + 15) / 16 * 16);  // [NL][E]
+  if (wave < NWL) {
+    const float wm = wave_min(cost_lds[tid]);
+    if (lane == 0) wave_m[wave] = wm;
+  }
+  __syncthreads();
+  for (int j = tid; j < TB; j += NT) {
+    const int leaf = j >> 8;
+    const float m = fminf(fminf(wave_m[4 * leaf], wave_m[4 * leaf + 1]),
+                          fminf(wave_m[4 * leaf + 2], wave_m[4 * leaf + 3]));
+    const float c = cost_lds[j];
+    wbuf[j] = (c < INFINITY) ? dm_expf(-((c - m) / a.T)) : 0.0f;
+  }
+  __syncthreads();
+  // rows (leaf, j), j in [1, E): lane l of the wave sums trajectories l, 64+l, 128+l, 192+l
+  for (int r = wave; r < NL * (E - 1); r += NWAVES) {
+    const int leaf = r / (E - 1), j = 1 + r - leaf * (E - 1);
+    const float* wl4 = wbuf + 256 * leaf + lane;
+    const double w0 = (double)wl4[0], w1 = (double)wl4[64], w2 = (double)wl4[128], w3 = (double)wl4[192];
+    double x0 = w0, x1 = w1, x2 = w2, x3 = w3;  // j == 1: S = sum w
+    if (j >= 2) {
+      const float* u = ub_block + (size_t)(j - 2) * TB + 256 * leaf + lane;
+      x0 = w0 * (double)u[0];
+      x1 = w1 * (double)u[64];
+      x2 = w2 * (double)u[128];
+      x3 = w3 * (double)u[192];
+    }
+    const double sum = wave_sum((x0 + x1) + (x2 + x3));
+    if (lane == 0) red[leaf * E + j] = sum;
+  }
+  __syncthreads();
+  for (int j = tid; j < E; j += NT) {
+    double val[NL];
+    float lm[NL];
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+      lm[q] = fminf(fminf(wave_m[4 * q], wave_m[4 * q + 1]), fminf(wave_m[4 * q + 2], wave_m[4 * q + 3]));
+      val[q] = (j == 0) ? (double)lm[q] : red[q * E + j];
+    }
+#pragma unroll
+    for (int width = NL; width > 1; width >>= 1) {
+#pragma unroll
+      for (int q = 0; q < width / 2; ++q) {
+        const PairScale ps = pair_scale(lm[2 * q], lm[2 * q + 1], a.T);
+        val[q] = pair_apply(ps, val[2 * q], val[2 * q + 1], j);
+        lm[q] = ps.m;
+      }
+    }
+    a.nodes[(size_t)blockIdx.x * E + j] = val[0];
+  }
+}
+
+// =====================================================================  warp-specialised rollout kernel
+// A workgroup of 2*TB threads serves TB trajectories.  Waves [0, TB/64) are
+// CHAIN waves: lane l of chain wave w runs the serial projection
+// (projection_warp.py:314-326) of trajectory 64w + l.  Waves [TB/64, TB/32)
+// are SIDE waves for the same trajectories: Philox noise, sampling, wheel
+// filter and sin/cos ahead of the chain (sampling_warp.py:54-138), wheel
+// contacts and the four critics behind it (projection_warp.py:333-348,
+// critics_warp.py:85-300).  Each SIMD then runs one chain and one side wave,
+// which doubles its issue rate over one wave per SIMD.  Per-step values go
+// through double-buffered LDS rings, one workgroup barrier per phase p:
+//   side : produce step p  (v, sin, cos)       -> in [p & 1]
+//   chain: consume in[(p-1) & 1], run step p-1 -> out[(p-1) & 1] (x, y, right.x, right.y)
+//   side : consume out[(p-2) & 1]: wheels + critics of step p-2
+template <int TB, int PROJ, int MODE, bool DUMP>
+__global__ __launch_bounds__(2 * TB) void mppi_rollout_ws_kernel(const RolloutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  constexpr int NT = 2 * TB;
+  constexpr int NWC = TB / 64;
+  float* ring_in = reinterpret_cast<float*>(smem_raw);   // [2][3][TB]: v, sin, cos
+  float* ring_out = ring_in + 6 * TB;                    // [2][4][TB]: x, y, cx, cy
+  float* cost_lds = ring_out + 8 * TB;                   // [TB]
+  unsigned char* scratch = reinterpret_cast<unsigned char*>(cost_lds + TB);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool side = wave >= NWC;
+  const int tj = side ? tid - TB : tid;  // trajectory within the workgroup
+#ifdef MPPI_STAMPS
+  const uint64_t k_t0 = dbg_stamp(), k_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  const int64_t kl = (int64_t)blockIdx.x * TB + tj;
+  const bool valid = kl < a.K;
+  const uint64_t kg = (uint64_t)(a.k_offset + kl);
+  const int H = a.H;
+  Dem<false> dem;
+  dem.init(a.Z, nullptr, a.rows, a.grid, 0, 0, 1, 1, a.x_min, a.y_min, a.res);
+  const float res_half_neg = (-a.res) / 2.0f;
+  const float res_sq = a.res * a.res;
+  bool nobad = false;
+
+  // ---------------- per-role state
+  Traj s;                       // chain
+  float L = a.wl, R = a.wr;     // side: filter
+  float e1b = 0.f, e2b = 0.f;   // side: noise of the odd step of the current Philox block
+  float vq0 = 0.f, vq1 = 0.f, wq0 = 0.f, wq1 = 0.f;  // side: v, w of steps p-2, p-1
+  float pf_sum = 0.f, sw = 0.f, sp = 0.f, ob = 0.f, last_x = a.x0, last_y = a.y0;
+  float lwx = 0.f, lwy = 0.f, lwz = 0.f, rwx = 0.f, rwy = 0.f, rwz = 0.f;
+  float cm_pend = 0.f;
+  float* ust = a.ustore + (size_t)blockIdx.x * (2 * H) * TB + tj;
+
+  if (!side) {  // initial projection at the robot pose (projection_warp.py:306-310)
+    s.x = a.x0;
+    s.y = a.y0;
+    float q[4];
+    dem.template corners<false>(s.x, s.y, q, nobad);
+    const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
+    const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
+    const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
+    const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
+    if constexpr (PROJ == 3) {
+      const float d = (a.h0x * nx + a.h0y * ny) + a.h0z * nz;
+      const float tx = a.h0x - d * nx, ty = a.h0y - d * ny, tz = a.h0z - d * nz;
+      const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
+      s.hx = tx / tn;
+      s.hy = ty / tn;
+      s.hz = tz / tn;
+    } else {
+      s.hx = a.h0x;
+      s.hy = a.h0y;
+      s.hz = a.h0z;
+    }
+  }
+
+  // ---- side: wheels + critics of step sc (branch-free: conditions become selects)
+  auto consume = [&](int sc, bool even) __attribute__((always_inline)) {
+    const float* ro = ring_out + (sc & 1) * 4 * TB + tj;
+    const float x = ro[0], y = ro[TB], cx = ro[2 * TB], cy = ro[3 * TB];
+    float lx = 0.f, ly = 0.f, lz = 0.f, rx = 0.f, ry = 0.f, rz = 0.f;
+    if constexpr (PROJ == 3) {
+      lx = x + cx;
+      ly = y + cy;
+      lz = dem.template point<false>(lx, ly, nobad);
+      rx = x - cx;
+      ry = y - cy;
+      rz = dem.template point<false>(rx, ry, nobad);
+    }
+    Recip rcm;
+    rcm.b = a.res_c;
+    const float cm_now = a.cm[costmap_index<false>(a.cm_size, a.hw, rcm, x, y, nobad)];
+    const float pft = pf_sum + 10.0f * (fabsf(x - a.gx) + fabsf(y - a.gy));
+    pf_sum = (sc < H - 1) ? pft : pf_sum;   // _path_follow_critic sum over t < H-1
+    last_x = x;
+    last_y = y;
+    if (even) {  // _avoid_slope_wheels terms (i, i+2), even i < H-3
+      const float term = slope_term<false>(lwx, lwy, lwz, lx, ly, lz, rwx, rwy, rwz, rx, ry, rz, nobad);
+      sw = (sc >= 2 && sc - 2 < H - 3) ? sw + term : sw;
+      lwx = lx; lwy = ly; lwz = lz;
+      rwx = rx; rwy = ry; rwz = rz;
+    }
+    const float spt = sp + (a.vmax - vq0) / (vq0 + 0.0001f);  // _maximise_speed
+    sp = a.speed_on ? spt : sp;
+    // _avoid_obstacle: the costmap value gathered in the previous consume
+    const float ob1 = (cm_pend > a.thr) ? ob + a.pen : ob;
+    ob = (sc > 0) ? ob1 + cm_pend : ob;
+    cm_pend = cm_now;
+    if constexpr (DUMP) {
+      if (valid) {
+        const size_t o3 = ((size_t)kl * H + sc) * 3;
+        if (a.d_lw) { a.d_lw[o3] = lx; a.d_lw[o3 + 1] = ly; a.d_lw[o3 + 2] = lz; }
+        if (a.d_rw) { a.d_rw[o3] = rx; a.d_rw[o3 + 1] = ry; a.d_rw[o3 + 2] = rz; }
+        const size_t o1 = (size_t)kl * H + sc;
+        if (a.d_v) a.d_v[o1] = vq0;
+        if (a.d_w) a.d_w[o1] = wq0;
+      }
+    }
+  };
+  // ---- side: noise, sampling, filter, sin/cos of step p
+  auto produce = [&](int p, bool even, float& vp, float& wp) __attribute__((always_inline)) {
+    float u1, u2;
+    if constexpr (MODE == 0) {
+      float e1, e2;
+      if (even) {
+        noise_block(a.seed, a.n_base + (uint64_t)(p >> 1), kg, &e1, &e2, &e1b, &e2b);
+      } else {
+        e1 = e1b;
+        e2 = e2b;
+      }
+      const int ti = min(p + 1, H - 1);
+      u1 = clampf(a.u_nom1[ti] + a.s1 * e1, a.min_u1, a.max_u1);
+      u2 = clampf(a.u_nom2[ti] + a.s2 * e2, a.min_u2, a.max_u2);
+    } else {
+      const size_t o = (size_t)(valid ? kl : 0) * H + p;
+      u1 = a.inj_u1[o];
+      u2 = a.inj_u2[o];
+    }
+    ust[(size_t)p * TB] = u1;
+    ust[(size_t)(H + p) * TB] = u2;
+    L = L * a.fa + (u1 * a.fk) * (1.0f - a.fa);
+    R = R * a.fa + (u2 * a.fk) * (1.0f - a.fa);
+    vp = clampf((L + R) / 2.0f, a.vmin, a.vmax);
+    wp = clampf(((-L) + R) / a.rwheel, a.wmin, a.wmax);
+    float* ri = ring_in + (p & 1) * 3 * TB + tj;
+    ri[0] = vp;
+    ri[TB] = wp;
+    if constexpr (DUMP) {
+      if (valid) {
+        const size_t o1 = (size_t)kl * H + p;
+        if (a.d_u1) a.d_u1[o1] = u1;
+        if (a.d_u2) a.d_u2[o1] = u2;
+      }
+    }
+  };
+  // ---- chain: step sc (sin/cos of w*dt evaluated here: it overlaps the position update)
+  auto chain_step = [&](int sc) __attribute__((always_inline)) {
+    const float* ri = ring_in + (sc & 1) * 3 * TB + tj;
+    const float v = ri[0], wv = ri[TB];
+    float sn, cs;
+    dm_sincosf(wv * a.dt, &sn, &cs);
+    float cx = 0.f, cy = 0.f, z = 0.f;
+    float q[4];
+    if constexpr (PROJ == 3) {
+      float nx, ny, nz;
+      bool bad = false;
+      const Traj saved = s;
+      chain3d<kChainFast, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+      if (kChainFast && __builtin_expect(bad, 0)) {  // operand outside the fast range: IEEE redo
+        s = saved;
+        chain3d<false, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+      }
+      cx = a.off * (ny * s.hz - nz * s.hy);
+      cy = a.off * (nz * s.hx - nx * s.hz);
+      if constexpr (DUMP) z = bilinear<false>(s.x, s.y, q, dem.template rr<false>(), nobad);
+    } else {
+      StepOut o;
+      step2d<false, false>(dem, a.dt, v, sn, cs, s, o, nobad);
+      z = o.z;
+    }
+    float* ro = ring_out + (sc & 1) * 4 * TB + tj;
+    ro[0] = s.x;
+    ro[TB] = s.y;
+    ro[2 * TB] = cx;
+    ro[3 * TB] = cy;
+    if constexpr (DUMP) {
+      if (valid) {
+        const size_t o3 = ((size_t)kl * H + sc) * 3;
+        if (a.d_traj) { a.d_traj[o3] = s.x; a.d_traj[o3 + 1] = s.y; a.d_traj[o3 + 2] = z; }
+        if (a.d_hv) { a.d_hv[o3] = s.hx; a.d_hv[o3 + 1] = s.hy; a.d_hv[o3 + 2] = s.hz; }
+      }
+    }
+  };
+#ifdef MPPI_STAMPS
+  uint64_t st_work = 0, st_wait = 0;
+#endif
+  // one phase: flags are compile-time constants at the peeled call sites below
+  auto phase = [&](int p, bool prod, bool cons, bool chain, bool even) __attribute__((always_inline)) {
+#ifdef MPPI_STAMPS
+    const uint64_t t0 = dbg_stamp();
+#endif
+    if (side) {
+      if (cons) consume(p - 2, even);
+      float vp = 0.f, wp = 0.f;
+      if (prod) produce(p, even, vp, wp);
+      vq0 = vq1;
+      vq1 = vp;
+      wq0 = wq1;
+      wq1 = wp;
+    } else if (chain) {
+      chain_step(p - 1);
+    }
+#ifdef MPPI_STAMPS
+    const uint64_t t1 = dbg_stamp();
+#endif
+    __syncthreads();
+#ifdef MPPI_STAMPS
+    const uint64_t t2 = dbg_stamp();
+    st_work += t1 - t0;
+    st_wait += t2 - t1;
+#endif
+  };
+
+  if (H >= 4) {
+    phase(0, true, false, false, true);
+    phase(1, true, false, true, false);
+    int p = 2;
+    for (; p + 1 < H; p += 2) {
+      phase(p, true, true, true, true);
+      phase(p + 1, true, true, true, false);
+    }
+    if (p < H) {  // odd H: one more producing (even) phase
+      phase(p, true, true, true, true);
+      ++p;
+    }
+    if ((H & 1) == 0) {
+      phase(H, false, true, true, true);
+      phase(H + 1, false, true, false, false);
+    } else {
+      phase(H, false, true, true, false);
+      phase(H + 1, false, true, false, true);
+    }
+  } else {
+    for (int p = 0; p < H + 2; ++p) phase(p, p < H, p >= 2, p >= 1 && p <= H, (p & 1) == 0);
+  }
+#ifdef MPPI_STAMPS
+  if ((tid & 63) == 0 && blockIdx.x < 64) {
+    g_dbg_stamps[(blockIdx.x * (NT / 64) + wave) * 2] = st_work;
+    g_dbg_stamps[(blockIdx.x * (NT / 64) + wave) * 2 + 1] = st_wait;
+  }
+#endif
+  if (side) {
+    if (cm_pend > a.thr) ob = ob + a.pen;  // last step's obstacle term
+    ob = ob + cm_pend;
+    // _evaluate_trajectories_kernel (critics_warp.py:325-329)
+    float pf;
+    if (a.pf_far) {
+      const float dx = last_x - a.igx, dy = last_y - a.igy;
+      pf = (dx * dx + dy * dy) * a.pf_scale;
+    } else {
+      pf = pf_sum;
+    }
+    float cost = a.w_path * pf;
+    cost = cost + a.w_slope * sw;
+    cost = cost + a.w_speed * sp;
+    cost = cost + a.w_obs * ob;
+    if (valid) a.cost_out[kl] = cost;
+    cost_lds[tj] = valid ? cost : INFINITY;
+  }
+  __syncthreads();
+#ifdef MPPI_STAMPS
+  const uint64_t k_t1 = dbg_stamp();
+#endif
+  leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
+#ifdef MPPI_STAMPS
+  const uint64_t k_t2 = dbg_stamp(), k_r2 = __builtin_amdgcn_s_memrealtime();
+  if ((tid & 63) == 0 && blockIdx.x < 64) {
+    uint64_t* g = g_dbg_stamps + 64 * 16 * 2 + (blockIdx.x * (NT / 64) + wave) * 4;
+    g[0] = k_t1 - k_t0;   // start .. end of phase loop + cost
+    g[1] = k_t2 - k_t1;   // leaf records
+    g[2] = k_r2 - k_r0;   // wall (100 MHz ticks)
+    g[3] = k_t2 - k_t0;   // total shader cycles
+  }
+  if (tid == 0 && blockIdx.x < 1024) {
+    uint64_t* g = g_dbg_stamps + 64 * 16 * 6 + blockIdx.x * 2;
+    g[0] = k_r0;
+    g[1] = k_r2;
+  }
+#endif
+}
+
 // =====================================================================  finish kernel
-// Tree over n records (padded to a power of two with empty records), then
-// (MODE_RECORD) write the root, or (MODE_FINISH) u_opt = V/S, optimal filter
-// (MPPI_isaac.py:672-692) and the 3D rollout of the optimal sequence (:696-720).
+// One workgroup.  (1) Binary tree over n records (padded to a power of two with
+// empty records): passes combining aligned groups of 8 (three tree levels) while
+// more than 32 nodes remain, then the last levels in LDS.  (2) MODE 0 writes the
+// root (rank record); MODE 1 computes u_opt = V/S, the optimal filter
+// (MPPI_isaac.py:672-692) and the 3D rollout of the optimal sequence (:696-720):
+// only the serial chain (chain3d) runs on one lane, sin/cos, heights and wheel
+// contacts are computed by all lanes around it.
+constexpr int FIN_THREADS = 1024;
+constexpr int FIN_LDS_NODES = 32;
+constexpr int FIN_GROUP_CHUNK = 128;   // groups per scale-table fill (7 PairScale each)
+constexpr int FIN_MAX_ITEMS = 8;       // (FIN_LDS_NODES/2) * (2H+2) <= 8192  <=>  H <= 255
+
+// scales of the 7 pairs of a group of 8 (levels 0,1,2) from the members' m
+__device__ __forceinline__ void group8_scales(const float (&m)[8], float T, PairScale (&ps)[7]) {
+  float m1[4], m2[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    ps[i] = pair_scale(m[2 * i], m[2 * i + 1], T);
+    m1[i] = ps[i].m;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    ps[4 + i] = pair_scale(m1[2 * i], m1[2 * i + 1], T);
+    m2[i] = ps[4 + i].m;
+  }
+  ps[6] = pair_scale(m2[0], m2[1], T);
+}
+
+__device__ __forceinline__ double group8_apply(const PairScale* ps, const double (&v)[8], int j) {
+  double a[4], b[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a[i] = pair_apply(ps[i], v[2 * i], v[2 * i + 1], j);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) b[i] = pair_apply(ps[4 + i], a[2 * i], a[2 * i + 1], j);
+  return pair_apply(ps[6], b[0], b[1], j);
+}
+
 template <bool LDS>
-__global__ __launch_bounds__(1024) void mppi_finish_kernel(const FinishArgs f) {
+__global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishArgs f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int tid = threadIdx.x;
   const int H = f.H;
   const int E = 2 * H + 2;
-  PairScale* scales = reinterpret_cast<PairScale*>(smem_raw);  // [1024]
-
+  // ---------------- (1) tree
+  // LDS during the tree: [FIN_LDS_NODES][E] doubles, then PairScale table
+  double* lnode = reinterpret_cast<double*>(smem_raw);
+  PairScale* lps = reinterpret_cast<PairScale*>(smem_raw + (size_t)FIN_LDS_NODES * E * sizeof(double));
   const double* cur = f.recs;
   int n = f.n_recs;
   double* bufs[2] = {f.scratch0, f.scratch1};
   int flip = 0;
-  while (n > 1) {
-    const int pairs = (n + 1) >> 1;
+  while (n > FIN_LDS_NODES) {  // global -> global, groups of 8
+    const int groups = (n + 7) >> 3;
     double* out = bufs[flip];
-    for (int p0 = 0; p0 < pairs; p0 += 1024) {
-      const int np = min(1024, pairs - p0);
-      if (tid < np) {
-        const int p = p0 + tid;
-        const float ma = (float)cur[(size_t)(2 * p) * E];
-        const float mb = (2 * p + 1 < n) ? (float)cur[(size_t)(2 * p + 1) * E] : INFINITY;
-        scales[tid] = pair_scale(ma, mb, f.T);
+    for (int g0 = 0; g0 < groups; g0 += FIN_GROUP_CHUNK) {
+      const int ng = min(FIN_GROUP_CHUNK, groups - g0);
+      if (tid < ng) {
+        const int g = g0 + tid;
+        float m[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m[i] = (8 * g + i < n) ? (float)cur[(size_t)(8 * g + i) * E] : INFINITY;
+        PairScale ps[7];
+        group8_scales(m, f.T, ps);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) lps[tid * 7 + i] = ps[i];
       }
       __syncthreads();
-      for (int it = tid; it < np * E; it += 1024) {
-        const int pl = it / E, j = it - pl * E;
-        const int p = p0 + pl;
-        const double va = cur[(size_t)(2 * p) * E + j];
-        const double vb = (2 * p + 1 < n) ? cur[(size_t)(2 * p + 1) * E + j] : 0.0;
-        out[(size_t)p * E + j] = pair_apply(scales[pl], va, vb, j);
+      for (int it = tid; it < ng * E; it += FIN_THREADS) {
+        const int gl = it / E, j = it - gl * E;
+        const int g = g0 + gl;
+        double v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (8 * g + i < n) ? cur[(size_t)(8 * g + i) * E + j] : 0.0;
+        out[(size_t)g * E + j] = group8_apply(lps + gl * 7, v, j);
       }
       __syncthreads();
     }
     cur = out;
-    n = pairs;
+    n = groups;
     flip ^= 1;
   }
-  if (f.mode == 0) {  // rank record
-    for (int j = tid; j < E; j += 1024) f.record_out[j] = (n == 1) ? cur[j] : (j == 0 ? INFINITY : 0.0);
+  for (int it = tid; it < n * E; it += FIN_THREADS) lnode[it] = cur[it];
+  __syncthreads();
+  while (n > 1) {  // LDS levels
+    const int pairs = (n + 1) >> 1;
+    if (tid < pairs) {
+      const float ma = (float)lnode[(size_t)(2 * tid) * E];
+      const float mb = (2 * tid + 1 < n) ? (float)lnode[(size_t)(2 * tid + 1) * E] : INFINITY;
+      lps[tid] = pair_scale(ma, mb, f.T);
+    }
+    __syncthreads();
+    double res[FIN_MAX_ITEMS];
+#pragma unroll
+    for (int q = 0; q < FIN_MAX_ITEMS; ++q) {
+      const int it = tid + q * FIN_THREADS;
+      if (it < pairs * E) {
+        const int p = it / E, j = it - p * E;
+        const double va = lnode[(size_t)(2 * p) * E + j];
+        const double vb = (2 * p + 1 < n) ? lnode[(size_t)(2 * p + 1) * E + j] : 0.0;
+        res[q] = pair_apply(lps[p], va, vb, j);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < FIN_MAX_ITEMS; ++q) {
+      const int it = tid + q * FIN_THREADS;
+      if (it < pairs * E) lnode[it] = res[q];
+    }
+    __syncthreads();
+    n = pairs;
+  }
+  // root = lnode[0..E) (n == 1) or empty (n == 0)
+  if (f.mode == 0) {
+    for (int j = tid; j < E; j += FIN_THREADS)
+      f.record_out[j] = (n == 1) ? lnode[j] : (j == 0 ? (double)INFINITY : 0.0);
     return;
   }
-  // ---- u_opt = V / S (DEFINED; zero if no finite cost)
-  float* uo = reinterpret_cast<float*>(smem_raw);  // [2H] (scales no longer needed)
-  __syncthreads();
-  const double S = (n == 1) ? cur[1] : 0.0;
-  for (int j = tid; j < 2 * H; j += 1024) {
-    const float u = (S > 0.0) ? (float)(cur[2 + j] / S) : 0.0f;
-    uo[j] = u;
-    f.u_nom_next[j] = u;
-    f.out[j] = u;
+  // ---------------- (2) optimal sequence
+  // LDS: uo[2H] v[H] w[H] sn[H] cs[H] chain[12H] | window (at f.win_offset)
+  const double S = (n == 1) ? lnode[1] : 0.0;
+  // u_opt = V / S (DEFINED; zero when no trajectory has a finite cost)
+  const float ures = (tid < 2 * H && S > 0.0) ? (float)(lnode[2 + tid] / S) : 0.0f;
+  __syncthreads();  // lnode is dead from here on
+  float* uo = reinterpret_cast<float*>(smem_raw);
+  float* vb = uo + 2 * H;
+  float* wb = vb + H;
+  float* snb = wb + H;
+  float* csb = snb + H;
+  float* chain = csb + H;  // [H][12]: x, y, q00, q01, q10, q11, nx, ny, nz, hx, hy, hz
+  if (tid < 2 * H) {
+    uo[tid] = ures;
+    f.u_nom_next[tid] = ures;
+    f.out[tid] = ures;
   }
   float* win = reinterpret_cast<float*>(smem_raw + f.win_offset);
   if constexpr (LDS) {
     const int lane = tid & 63, wave = tid >> 6;
-    for (int r = wave; r < f.Wr; r += 16) {
+    for (int r = wave; r < f.Wr; r += FIN_THREADS / 64) {
       const float* src = f.Z + (size_t)(f.wy0 + r) * f.grid + f.wx0;
       float* dst = win + r * f.W;
       for (int c2 = lane; c2 < f.W; c2 += 64) dst[c2] = src[c2];
     }
   }
   __syncthreads();
-  if (tid != 0) return;
+  if (tid == 0) {  // optimal-sequence wheel filter (sampling_warp.py:120-138, k=3.0, a=0.92)
+    float L = f.wl, R = f.wr;
+    const float one_m_a = 1.0f - f.oa;
+    for (int t = 0; t < H; ++t) {
+      L = L * f.oa + (uo[t] * f.ok) * one_m_a;
+      R = R * f.oa + (uo[H + t] * f.ok) * one_m_a;
+      vb[t] = clampf((L + R) / 2.0f, f.vmin, f.vmax);
+      wb[t] = clampf(((-L) + R) / f.rwheel, f.wmin, f.wmax);
+    }
+  }
+  __syncthreads();
+  for (int t = tid; t < H; t += FIN_THREADS) {
+    float sn, cs;
+    dm_sincosf(wb[t] * f.dt, &sn, &cs);
+    snb[t] = sn;
+    csb[t] = cs;
+    f.out[2 * H + t] = vb[t];
+    f.out[3 * H + t] = wb[t];
+  }
+  __syncthreads();
   Dem<LDS> dem;
-  dem.Z = f.Z;
-  dem.win = win;
-  dem.rows = f.rows;
-  dem.grid = f.grid;
-  dem.wx0 = f.wx0;
-  dem.wy0 = f.wy0;
-  dem.W = f.W;
-  dem.Wr = f.Wr;
-  dem.x_min = f.x_min;
-  dem.y_min = f.y_min;
-  dem.res = f.res;
+  dem.init(f.Z, win, f.rows, f.grid, f.wx0, f.wy0, f.W, f.Wr, f.x_min, f.y_min, f.res);
   const float res_half_neg = (-f.res) / 2.0f;
   const float res_sq = f.res * f.res;
-  float* o_v = f.out + 2 * H;
-  float* o_w = f.out + 3 * H;
-  float* o_traj = f.out + 4 * H;
-  float* o_hv = f.out + 7 * H;
-  float* o_lw = f.out + 10 * H;
-  float* o_rw = f.out + 13 * H;
-  Traj s;
-  s.x = f.x0;
-  s.y = f.y0;
-  {
-    float q00, q01, q10, q11;
-    dem.corners(s.x, s.y, q00, q01, q10, q11);
-    const float vx = res_half_neg * (((q01 - q00) - q10) + q11);
-    const float vy = res_half_neg * (((q10 - q00) - q01) + q11);
-    const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
-    const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
-    const float d = (f.h0x * nx + f.h0y * ny) + f.h0z * nz;
-    float tx = f.h0x - d * nx, ty = f.h0y - d * ny, tz = f.h0z - d * nz;
-    const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
-    s.hx = tx / tn;
-    s.hy = ty / tn;
-    s.hz = tz / tn;
+  if (tid == 0) {  // the serial chain (projection_warp.py:306-326)
+    Traj s;
+    s.x = f.x0;
+    s.y = f.y0;
+    {
+      bool unused = false;
+      float q[4];
+      dem.template corners<false>(s.x, s.y, q, unused);
+      const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
+      const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
+      const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
+      const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
+      const float d = (f.h0x * nx + f.h0y * ny) + f.h0z * nz;
+      const float tx = f.h0x - d * nx, ty = f.h0y - d * ny, tz = f.h0z - d * nz;
+      const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
+      s.hx = tx / tn;
+      s.hy = ty / tn;
+      s.hz = tz / tn;
+    }
+    float vn = vb[0], sn_n = snb[0], cs_n = csb[0];
+    for (int t = 0; t < H; ++t) {
+      const float v = vn, sn = sn_n, cs = cs_n;
+      const int tn = min(t + 1, H - 1);  // prefetch the next step's inputs from LDS
+      vn = vb[tn];
+      sn_n = snb[tn];
+      cs_n = csb[tn];
+      const Traj saved = s;
+      float q[4], nx, ny, nz;
+      bool bad = false;
+      chain3d<kChainFast, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+      if (kChainFast && __builtin_expect(bad, 0)) {
+        s = saved;
+        chain3d<false, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+      }
+      float* ch = chain + 12 * t;
+      ch[0] = s.x; ch[1] = s.y;
+      ch[2] = q[0]; ch[3] = q[1]; ch[4] = q[2]; ch[5] = q[3];
+      ch[6] = nx; ch[7] = ny; ch[8] = nz;
+      ch[9] = s.hx; ch[10] = s.hy; ch[11] = s.hz;
+    }
   }
-  float L = f.wl, R = f.wr;
-  const float one_m_a = 1.0f - f.oa;
-  for (int t = 0; t < H; ++t) {
-    L = L * f.oa + (uo[t] * f.ok) * one_m_a;
-    R = R * f.oa + (uo[H + t] * f.ok) * one_m_a;
-    const float v = clampf((L + R) / 2.0f, f.vmin, f.vmax);
-    const float w = clampf(((-L) + R) / f.rwheel, f.wmin, f.wmax);
-    o_v[t] = v;
-    o_w[t] = w;
+  __syncthreads();
+  for (int t = tid; t < H; t += FIN_THREADS) {  // heights + wheel contacts, all lanes
+    const float* ch = chain + 12 * t;
+    const float q[4] = {ch[2], ch[3], ch[4], ch[5]};
     StepOut o;
-    step3d<LDS>(dem, res_half_neg, res_sq, f.dt, f.off, v, w, s, o);
-    o_traj[3 * t] = s.x; o_traj[3 * t + 1] = s.y; o_traj[3 * t + 2] = o.z;
-    o_hv[3 * t] = s.hx; o_hv[3 * t + 1] = s.hy; o_hv[3 * t + 2] = s.hz;
-    o_lw[3 * t] = o.lx; o_lw[3 * t + 1] = o.ly; o_lw[3 * t + 2] = o.lz;
-    o_rw[3 * t] = o.rx; o_rw[3 * t + 1] = o.ry; o_rw[3 * t + 2] = o.rz;
+    bool bad = false;
+    wheels3d<kFastMath, LDS>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
+    if (kFastMath && bad)
+      wheels3d<false, LDS>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
+    float* o_traj = f.out + 4 * H + 3 * t;
+    float* o_hv = f.out + 7 * H + 3 * t;
+    float* o_lw = f.out + 10 * H + 3 * t;
+    float* o_rw = f.out + 13 * H + 3 * t;
+    o_traj[0] = ch[0]; o_traj[1] = ch[1]; o_traj[2] = o.z;
+    o_hv[0] = ch[9]; o_hv[1] = ch[10]; o_hv[2] = ch[11];
+    o_lw[0] = o.lx; o_lw[1] = o.ly; o_lw[2] = o.lz;
+    o_rw[0] = o.rx; o_rw[1] = o.ry; o_rw[2] = o.rz;
   }
 }
 
 // =====================================================================  standalone bilinear
 // Scattered-query corner lookup + bilinear (projection_warp.py:8-100) over the
-// full DEM in HBM: one lane per query, float4 query loads.
+// full DEM in HBM: one lane per query.
 __global__ __launch_bounds__(256) void mppi_bilinear_kernel(const float* __restrict__ Z, int rows,
                                                             int grid, float x_min, float y_min,
                                                             float res, const float* __restrict__ xs,
                                                             const float* __restrict__ ys,
                                                             float* __restrict__ hs, int64_t n) {
   Dem<false> dem;
-  dem.Z = Z;
-  dem.win = nullptr;
-  dem.rows = rows;
-  dem.grid = grid;
-  dem.wx0 = dem.wy0 = 0;
-  dem.W = dem.Wr = 0;
-  dem.x_min = x_min;
-  dem.y_min = y_min;
-  dem.res = res;
+  dem.init(Z, nullptr, rows, grid, 0, 0, 1, 1, x_min, y_min, res);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const float x = xs[i], y = ys[i];
-    float q00, q01, q10, q11;
-    dem.corners(x, y, q00, q01, q10, q11);
-    hs[i] = bilinear(x, y, q00, q01, q10, q11, res);
+    float q[4];
+    bool bad = false;
+    dem.template corners<true>(x, y, q, bad);
+    float h = bilinear<true>(x, y, q, dem.template rr<true>(), bad);
+    if (bad) {
+      dem.template corners<false>(x, y, q, bad);
+      h = bilinear<false>(x, y, q, dem.template rr<false>(), bad);
+    }
+    hs[i] = h;
   }
+}
+
+// =====================================================================  self-test
+// Bitwise check of the fast division / sqrt paths against the IEEE operators
+// on random operands spanning the fast-path range and beyond; an operand
+// flagged out of range counts as checked (the engine would recompute it).
+__global__ __launch_bounds__(256) void mppi_selftest_kernel(int what, int64_t n, uint64_t seed,
+                                                            unsigned long long* bad_count) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long local = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const U4 r = philox4x32_10(U4{(uint32_t)i, (uint32_t)(i >> 32), 0x5e1fu, 0x7e57u}, (uint32_t)seed,
+                               (uint32_t)(seed >> 32));
+    // random sign/mantissa; exponent uniform over [-50, 50] (beyond the fast-path bounds)
+    auto mk = [](uint32_t bits, uint32_t eb) {
+      const int e = (int)(eb % 101u) - 50 + 127;
+      return bits_f((bits & 0x807FFFFFu) | ((uint32_t)e << 23));
+    };
+    float a = mk(r.x, r.z), b = mk(r.y, r.w);
+    if ((i & 1023) == 7) a = 0.0f;
+    if ((i & 1023) == 9) a = -0.0f;
+    if ((i & 4095) == 11) a = bits_f(r.x & 0x807FFFFFu);  // subnormal
+    bool flagged = false;
+    if (what == 0) {
+      const float want = a / b;
+      const float got = dv1<true>(a, b, flagged);
+      if (!flagged && f_bits(want) != f_bits(got)) ++local;
+    } else {
+      const float x = fabsf(a);
+      const float want = sqrtf(x);
+      const float got = sq<true>(x, flagged);
+      if (!flagged && f_bits(want) != f_bits(got)) ++local;
+    }
+  }
+  if (local) atomicAdd(bad_count, local);
 }
 
 // =====================================================================  launchers
@@ -697,11 +1372,39 @@ hipError_t launch_rollout(const RolloutArgs& a, int block, int blocks, size_t ld
   }
 }
 
+template <int TB, int PROJ>
+static hipError_t launch_ws_m(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int mode,
+                              bool dump) {
+  if (mode == 0) {
+    if (dump)
+      hipLaunchKernelGGL((mppi_rollout_ws_kernel<TB, PROJ, 0, true>), dim3(blocks), dim3(2 * TB), lds, st, a);
+    else
+      hipLaunchKernelGGL((mppi_rollout_ws_kernel<TB, PROJ, 0, false>), dim3(blocks), dim3(2 * TB), lds, st, a);
+  } else {
+    if (dump)
+      hipLaunchKernelGGL((mppi_rollout_ws_kernel<TB, PROJ, 1, true>), dim3(blocks), dim3(2 * TB), lds, st, a);
+    else
+      hipLaunchKernelGGL((mppi_rollout_ws_kernel<TB, PROJ, 1, false>), dim3(blocks), dim3(2 * TB), lds, st, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_rollout_ws(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
+                             int mode, bool dump) {
+  if (proj == 3) return launch_ws_m<256, 3>(a, blocks, lds, st, mode, dump);
+  return launch_ws_m<256, 2>(a, blocks, lds, st, mode, dump);
+}
+
 hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool use_lds) {
   if (use_lds)
-    hipLaunchKernelGGL(mppi_finish_kernel<true>, dim3(1), dim3(1024), lds, st, f);
+    hipLaunchKernelGGL(mppi_finish_kernel<true>, dim3(1), dim3(FIN_THREADS), lds, st, f);
   else
-    hipLaunchKernelGGL(mppi_finish_kernel<false>, dim3(1), dim3(1024), lds, st, f);
+    hipLaunchKernelGGL(mppi_finish_kernel<false>, dim3(1), dim3(FIN_THREADS), lds, st, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_selftest(int what, int64_t n, uint64_t seed, unsigned long long* bad, hipStream_t st) {
+  hipLaunchKernelGGL(mppi_selftest_kernel, dim3(2048), dim3(256), 0, st, what, n, seed, bad);
   return hipGetLastError();
 }
 

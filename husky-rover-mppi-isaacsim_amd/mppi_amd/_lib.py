@@ -87,6 +87,7 @@ _PROTOS = {
     "mppi_set_dem_path": (C.c_int, [C.c_void_p, C.c_int32]),
     "mppi_get_launch_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]),
     "mppi_bilinear_query": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
+    "mppi_selftest": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.POINTER(C.c_int64)]),
 }
 
 _lib = None
@@ -241,7 +242,7 @@ class Engine:
         return u1, u2
 
     def set_dem_path(self, mode):
-        self._c(self.lib.mppi_set_dem_path(self.ctx, {"auto": 0, "lds": 1, "global": 2}.get(mode, mode)),
+        self._c(self.lib.mppi_set_dem_path(self.ctx, {"auto": 0, "lds": 1, "global": 2, "ws": 3}.get(mode, mode)),
                 "mppi_set_dem_path")
 
     # ------------------------------------------------------------ steps
@@ -310,6 +311,11 @@ class Engine:
         self._c(self.lib.mppi_get_launch_info(self.ctx, info, 6), "mppi_get_launch_info")
         keys = ("dem_in_lds", "block", "blocks", "window_cols", "window_rows", "lds_bytes")
         return dict(zip(keys, [int(v) for v in info]))
+
+    def selftest(self, what, n=1 << 24, seed=1):
+        bad = C.c_int64()
+        self._c(self.lib.mppi_selftest(self.ctx, int(what), int(n), int(seed), C.byref(bad)), "mppi_selftest")
+        return bad.value
 
     def bilinear_query(self, x_ptr, y_ptr, h_ptr, n):
         self._c(self.lib.mppi_bilinear_query(self.ctx, C.c_void_p(int(x_ptr)), C.c_void_p(int(y_ptr)),

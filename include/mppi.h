@@ -163,8 +163,11 @@ int mppi_dump_rollouts(mppi_ctx* ctx, float* traj, float* heading, float* left_w
 int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
 int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_t* launches);
 
-/* DEM access path of the rollout kernel: 0 = auto (LDS window when it fits),
- * 1 = LDS window (error if it does not fit), 2 = global memory (L2/MALL). */
+/* Rollout kernel variant: 0 = default (= 3); 1 = one wave per trajectory group
+ * with the DEM window staged in LDS (error if it does not fit); 2 = one wave per
+ * trajectory group, DEM read through L1/L2; 3 = warp-specialised (a chain wave
+ * and a side wave per 64 trajectories, DEM through L1/L2).  All variants give
+ * bitwise identical results. */
 int mppi_set_dem_path(mppi_ctx* ctx, int32_t mode);
 
 /* Layout/launch facts for the last step (for tests and the bench):
@@ -177,6 +180,12 @@ int mppi_get_launch_info(mppi_ctx* ctx, int64_t* info, int32_t n);
  * as projection_warp.py:8-100, on the context's DEM. */
 int mppi_bilinear_query(mppi_ctx* ctx, const float* x_dev, const float* y_dev, float* h_dev,
                         int64_t n);
+
+/* Device self-test of the engine's exact-arithmetic fast paths: what = 0 checks
+ * the shared-reciprocal division against IEEE a/b, what = 1 the sqrt path
+ * against IEEE sqrtf, on n random operands; *mismatches receives the count of
+ * results that differ in any bit (0 expected). */
+int mppi_selftest(mppi_ctx* ctx, int32_t what, int64_t n, uint64_t seed, int64_t* mismatches);
 
 #ifdef __cplusplus
 }

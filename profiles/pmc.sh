@@ -1,0 +1,18 @@
+#!/bin/bash
+# PMC passes (one counter group per rocprofv3 run, kernel-trace only, no sys/runtime trace).
+# Usage (on the GPU box): bash profiles/pmc.sh <tag> [bench args...]
+set -o pipefail
+TAG=${1:-pmc}; shift
+OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+i=0
+for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" \
+           "SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE" "TCC_HIT_sum TCC_MISS_sum"; do
+  timeout -k 10 240 rocprofv3 --pmc $grp --kernel-trace -d $OUT/p$i -o p --output-format csv -- \
+      python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 3 --cpu-baseline-seconds 0 "$@" > /dev/null 2> $OUT/p$i.err || echo "pass $i ($grp) failed rc=$?" >> $OUT/status.txt
+  i=$((i+1))
+done
+cd $GRAFT_REPO_ROOT
+python3 profiles/pmc_summary.py $OUT > $OUT/summary.json && cat $OUT/summary.json

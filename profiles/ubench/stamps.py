@@ -1,0 +1,72 @@
+"""Diagnostic: per-wave work / barrier-wait cycles of the warp-specialised rollout kernel.
+
+Builds a separate library with -DMPPI_STAMPS (never the product .so), runs C3
+steps and prints average cycles per phase for chain and side waves.
+Usage (GPU box): python profiles/ubench/stamps.py [K]
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+PKG = os.path.join(ROOT, "husky-rover-mppi-isaacsim_amd")
+sys.path[:0] = [ROOT, PKG]
+SO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmppi_hip_stamps.so")
+
+
+def build():
+    csrc = os.path.join(PKG, "csrc")
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+           "-fPIC", "-shared", "-DMPPI_STAMPS", f"-I{ROOT}/include", f"-I{csrc}", "-x", "hip",
+           os.path.join(csrc, "mppi_kernels.hip"), os.path.join(csrc, "mppi_capi.cpp"), "-o", SO]
+    subprocess.run(cmd, check=True)
+
+
+def main():
+    K = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    if not os.path.exists(SO):
+        build()
+    from mppi_amd import _lib, scene
+    lib = _lib.load_library(SO)
+    lib.mppi_debug_stamps.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+    _lib._lib = lib  # Engine uses the stamps build
+    Z, hw, cm = scene.scene_c3()
+    H = 100
+    eng = _lib.Engine(_lib.make_params(K, H), 0)
+    eng.set_dem_path("ws")
+    eng.set_dem(Z, hw)
+    eng.set_costmap(cm, hw)
+    eng.set_state(_lib.make_state(-60.0, -5.0, goal_x=65.0, goal_y=10.0))
+    for i in range(5):
+        eng.step("3d", i)
+    n = 64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2
+    buf = (C.c_uint64 * n)()
+    assert lib.mppi_debug_stamps(buf, n) == 0
+    allv = np.array(buf, dtype=np.float64)
+    nb_all = (K + 255) // 256
+    se = allv[64 * 16 * 6: 64 * 16 * 6 + 2 * nb_all].reshape(nb_all, 2)
+    t0 = se[:, 0].min()
+    st, en = (se[:, 0] - t0) / 100.0, (se[:, 1] - t0) / 100.0
+    print(f"  block start (us): min {st.min():.1f} median {np.median(st):.1f} max {st.max():.1f}; "
+          f"end: min {en.min():.1f} median {np.median(en):.1f} max {en.max():.1f}")
+    print("  start histogram (10 us bins):", np.histogram(st, bins=np.arange(0, st.max() + 10, 10))[0].tolist())
+    a = allv[:64 * 16 * 2].reshape(64, 16, 2)
+    b = allv[64 * 16 * 2: 64 * 16 * 6].reshape(64, 16, 4)[: min(64, (K + 255) // 256), :8]
+    print(f"  loop+cost {b[..., 0].mean():10.0f} cyc   leaf records {b[..., 1].mean():8.0f} cyc   "
+          f"total {b[..., 3].mean():10.0f} cyc = {b[..., 2].mean() / 100:8.1f} us wall "
+          f"-> clock {b[..., 3].mean() / (b[..., 2].mean() * 10):.2f} GHz")
+    nb = min(64, (K + 255) // 256)
+    a = a[:nb, :8]
+    phases = H + 2
+    chain = a[:, :4].reshape(-1, 2) / phases
+    side = a[:, 4:].reshape(-1, 2) / phases
+    print(f"K={K}: cycles per phase (mean over {nb} blocks)")
+    print(f"  chain waves: work {chain[:, 0].mean():8.1f}  wait {chain[:, 1].mean():8.1f}")
+    print(f"  side  waves: work {side[:, 0].mean():8.1f}  wait {side[:, 1].mean():8.1f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -80,6 +80,19 @@ def test_global_dem_path_matches_lds_path():
     _assert_step(ref, out_g, eng_g)
 
 
+@pytest.mark.parametrize("path", ["ws", "global", "lds"])
+@pytest.mark.parametrize("K,H,proj", [(256, 20, "3d"), (1000, 33, "3d"), (4096, 50, "3d"), (700, 24, "2d")])
+def test_kernel_variants_parity(path, K, H, proj):
+    st = hp.oracle_state(wl=0.2, wr=0.1)
+    ref, out, eng = _run_both(K, H, 8, st, proj=proj, step=2, dem_path=path)
+    _assert_step(ref, out, eng)
+    d = eng.dump()
+    part = ref["parts"][0]
+    for name, key in (("u1", "u1"), ("u2", "u2"), ("v", "v"), ("w", "w"), ("traj", "traj"), ("hv", "hv"),
+                      ("lw", "lw"), ("rw", "rw")):
+        assert np.array_equal(d[name], part[key]), hp.mismatch_report(f"{path}:{name}", d[name], part[key])
+
+
 def test_proj_2d_parity():
     st = hp.oracle_state()
     ref, out, eng = _run_both(512, 30, 4, st, proj="2d")
