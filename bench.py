@@ -103,28 +103,23 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     from mppi_amd import _lib, scene
+    from mppi_amd.distributed import ShardedMPPI
     Z, hw, cm = scene.scene_c3()
     H = args.horizon
     Kl = args.k_per_gpu
-    params = _lib.make_params(Kl, H, k_offset=rank * Kl)
-    eng = _lib.Engine(params, local_rank)
+    if Kl % 256:
+        raise SystemExit("--k-per-gpu must be a multiple of 256 (reduction leaf)")
+    # rank r owns trajectories [r*Kl, (r+1)*Kl) of the global K = Kl*world (shard_bounds)
+    sharded = ShardedMPPI(Kl * world, H, local_rank) if world > 1 else None
+    eng = sharded.engine if sharded is not None else _lib.Engine(_lib.make_params(Kl, H), local_rank)
     eng.set_dem_path(args.dem_path)
     eng.set_dem(Z, hw)
     eng.set_costmap(cm, hw)
     eng.set_state(_lib.make_state(START[0], START[1], (1.0, 0.0, 0.0), goal_x=GOAL[0], goal_y=GOAL[1]))
 
-    if world > 1:
-        stream = torch.cuda.Stream()        # non-default stream shared by the engine and RCCL
-        torch.cuda.set_stream(stream)
-        eng.set_stream(stream.cuda_stream)
-        E = eng.record_len()
-        rec = torch.empty(E, dtype=torch.float64, device="cuda")
-        gathered = torch.empty(world * E, dtype=torch.float64, device="cuda")
-
+    if sharded is not None:
         def one_step(i):
-            eng.step_partial(rec.data_ptr(), args.proj, i)
-            dist.all_gather_into_tensor(gathered, rec)
-            eng.step_finish(gathered.data_ptr(), world, copy=False)
+            sharded.step(args.proj, i, copy=False)
     else:
         def one_step(i):
             eng.step(args.proj, i, copy=False)
@@ -197,7 +192,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "mppi_rollout_kernel",
+                "kernel": "mppi_rollout_ws_kernel" if args.dem_path in ("auto", "ws") else "mppi_rollout_kernel",
                 "kernel_avg_ms": round(k_avg_ms, 5),
                 "algorithmic_bytes_per_launch": alg_bytes,
             },
