@@ -102,6 +102,14 @@ def load_library(path: str = LIB_PATH):
         raise RuntimeError(
             f"HIP engine library not found at {path}; build it with "
             "`make -C husky-rover-mppi-isaacsim_amd/csrc` (no CPU fallback exists)")
+    # PyTorch-ROCm bundles its own libamdhip64.so.7.  Load it first so that the
+    # engine's NEEDED libamdhip64.so.7 resolves to the same runtime: a second
+    # HIP/HSA runtime in the process would make torch.cuda fail to initialise
+    # ("No HIP GPUs are available") once the engine has claimed the device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in _PROTOS.items():
         fn = getattr(lib, name)

@@ -74,7 +74,9 @@ def test_controller_step_alias_and_rebinding():
     K, H = 256, 16
     Z, hw, cm = hp.c3_scene()
     cfg = _config(K, H)
-    ctl = MPPI_Controller(Surface.from_arrays(Z, cm, hw), Robot(-60.0, -5.0, [1, 0, 0], cfg), cfg, 65.0, 10.0, 0.0)
+    robot = Robot(-60.0, -5.0, [1, 0, 0], cfg)
+    robot.left_wheel_speed = robot.right_wheel_speed = 1.5     # moving: rollouts cross DEM cells
+    ctl = MPPI_Controller(Surface.from_arrays(Z, cm, hw), robot, cfg, 65.0, 10.0, 0.0)
     ctl.warp_setup()
     a0 = ctl.step("3d")
     assert isinstance(a0, tuple) and len(a0) == 2 and a0 == ctl.get_action()
@@ -86,8 +88,15 @@ def test_controller_step_alias_and_rebinding():
     ctl.step_index = 0
     a1 = ctl.step("3d")
     assert a1 == a0
-    # flattened warp-style upload of a different DEM changes the answer
-    ctl.Z_wp = (Z * 2.0).ravel()
+    # flattened warp-style upload of a different DEM: the engine now follows the new terrain
+    Z2 = (Z * 3.0).astype(np.float32)
+    ctl.Z_wp = Z2.ravel()
     ctl.reset("sim")
     ctl.step_index = 0
-    assert ctl.step("3d") != a0
+    a2 = ctl.step("3d")
+    st = R.State(x=-60.0, y=-5.0, left_wheel_speed=1.5, right_wheel_speed=1.5, goal_x=65.0, goal_y=10.0)
+    ref = R.mppi_step(R.Params(K=K, H=H, seed=42), R.Scene(Z2, hw, cm), st, np.zeros(H, np.float32),
+                      np.zeros(H, np.float32), 0)
+    np.testing.assert_array_equal(ctl.optimal_u1_wp.numpy(), ref["u1_opt"])
+    np.testing.assert_array_equal(ctl.costs_wp.numpy(), ref["cost"])
+    assert a2 == (float(ref["v_opt"][0]), float(ref["w_opt"][0]))
