@@ -79,8 +79,10 @@ struct mppi_ctx {
   double* record = nullptr;  // single-rank root record (unused output)
   float* ustore = nullptr;   // sampled controls of the current step [blocks][2][H][block]
   size_t ustore_cap = 0;
-  float* out_dev = nullptr;
-  float* out_host = nullptr;  // pinned
+  float* stage = nullptr;     // pinned [16H]: the finish kernel stores the outputs here directly
+  unsigned* done = nullptr;   // pinned completion word (FinishArgs::done)
+  unsigned seq = 0;
+  float* out_host = nullptr;  // [16H] last complete outputs (host memory)
   float* inj1 = nullptr;
   float* inj2 = nullptr;
   int dem_path = 0;
@@ -90,12 +92,22 @@ struct mppi_ctx {
   uint64_t last_step = 0;
   mppi_state last_state{};
   int last_nominal = 0;
+  // deferred optimal rollout (mppi_set_async_tail): side stream + buffers
+  bool async_tail = false;
+  hipStream_t tail_stream = nullptr;
+  hipEvent_t ev_fin_done = nullptr;
+  hipEvent_t ev_tail[2] = {nullptr, nullptr};  // per parity: tail done
+  bool tail_pending = false;       // the latest tail's outputs are not merged into out_host yet
+  bool tail_inflight[2] = {false, false};  // the tail of that parity may still run
+  int tail_par = 0;                // parity of the latest tail
+  float* tail_in[2] = {nullptr, nullptr};    // device [3H] per parity
+  float* tail_host[2] = {nullptr, nullptr};  // pinned [12H] per parity (written by the kernel)
   // timing
   bool timing = false;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  bool ev_roll_pending = false, ev_fin_pending = false;
-  double t_roll = 0, t_fin = 0;
-  int64_t launches = 0;
+  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  bool ev_roll_pending = false, ev_fin_pending = false, ev_tail_pending = false;
+  double t_roll = 0, t_fin = 0, t_tail = 0;
+  int64_t launches = 0, tail_launches = 0;
   Plan last_plan;
 };
 
@@ -278,7 +290,7 @@ void fill_finish(const mppi_ctx* c, const Plan& pl, const mppi_state& st, Finish
   f.scratch0 = c->scratch0;
   f.scratch1 = c->scratch1;
   f.u_nom_next = c->u_nom[c->cur ^ 1];
-  f.out = c->out_dev;
+  f.out = c->stage;
   f.Z = c->Z;
   f.rows = c->rows;
   f.grid = c->cols;
@@ -316,6 +328,52 @@ void collect_timing(mppi_ctx* c) {
   }
   if (c->ev_fin_pending && hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess) c->t_fin += ms;
   c->ev_roll_pending = c->ev_fin_pending = false;
+}
+
+// Tail timing events live on the side stream: fold them in once the tail is done.
+void collect_tail_timing(mppi_ctx* c) {
+  if (!c->ev_tail_pending) return;
+  float ms = 0.f;
+  if (hipEventSynchronize(c->ev[5]) == hipSuccess && hipEventElapsedTime(&ms, c->ev[4], c->ev[5]) == hipSuccess) {
+    c->t_tail += ms;
+    c->tail_launches += 1;
+  }
+  c->ev_tail_pending = false;
+}
+
+// Wait until no deferred optimal rollout can still read tail_in or the DEM, and
+// merge the latest one's outputs into out_host[4H, 16H).
+int sync_tail(mppi_ctx* c) {
+  if (!c->tail_inflight[0] && !c->tail_inflight[1] && !c->tail_pending) return MPPI_OK;
+  HIP_TRY(hipStreamSynchronize(c->tail_stream));
+  collect_tail_timing(c);
+  c->tail_inflight[0] = c->tail_inflight[1] = false;
+  if (c->tail_pending) {
+    const int H = H_of(c);
+    std::memcpy(c->out_host + 4 * H, c->tail_host[c->tail_par], (size_t)12 * H * sizeof(float));
+    c->tail_pending = false;
+  }
+  return MPPI_OK;
+}
+
+// Spin until the finish kernel has published c->seq (all outputs in pinned host
+// memory); a fault surfaces through hipStreamQuery.
+int wait_done(mppi_ctx* c) {
+  if (c->timing) {  // timing events need the stream to retire
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  for (uint64_t i = 0;; ++i) {
+    if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == c->seq) return MPPI_OK;
+    if ((i & 255) == 255) {
+      const hipError_t e = hipStreamQuery(c->stream);
+      if (e == hipSuccess) {
+        if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == c->seq) return MPPI_OK;
+        return fail(MPPI_EHIP, "finish kernel retired without publishing its outputs");
+      }
+      if (e != hipErrorNotReady) return fail(MPPI_EHIP, std::string("step failed: ") + hipGetErrorString(e));
+    }
+    __builtin_ia32_pause();
+  }
 }
 
 // Enqueue the rollout kernel for the current state / nominal sequence.
@@ -361,10 +419,28 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
                    int mode, double* record_out, bool timed) {
   FinishArgs f;
   fill_finish(c, pl, st, f);
+  if (mode == 1 && c->async_tail) mode = 2;
   f.recs = recs;
   f.n_recs = n;
   f.mode = mode;
   f.record_out = record_out;
+  if (mode >= 1) {
+    f.done = c->done;
+    f.seq = ++c->seq;
+  }
+  const int par = c->tail_par ^ 1;
+  if (mode == 2) {
+    f.tail_in = c->tail_in[par];
+    f.tail_out = c->tail_host[par];
+    // the tail of two steps ago used these buffers; in steady state it finished long ago
+    // (it is shorter than a rollout kernel), so the cross-stream wait is rarely enqueued
+    if (c->tail_inflight[par]) {
+      const hipError_t q = hipEventQuery(c->ev_tail[par]);
+      if (q == hipErrorNotReady) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_tail[par], 0));
+      else if (q != hipSuccess) return fail(MPPI_EHIP, std::string("tail: ") + hipGetErrorString(q));
+      else c->tail_inflight[par] = false;
+    }
+  }
   if (n > 1) {
     int rc = ensure_nodes(c, n);
     if (rc) return rc;
@@ -378,27 +454,64 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     c->ev_fin_pending = true;
   }
+  if (mode == 2) {  // the optimal rollout runs on the side stream, overlapping what follows
+    HIP_TRY(hipEventRecord(c->ev_fin_done, c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->tail_stream, c->ev_fin_done, 0));
+    if (c->timing) {
+      collect_tail_timing(c);
+      HIP_TRY(hipEventRecord(c->ev[4], c->tail_stream));
+    }
+    HIP_TRY(launch_tail(f, c->tail_stream));
+    if (c->timing) {
+      HIP_TRY(hipEventRecord(c->ev[5], c->tail_stream));
+      c->ev_tail_pending = true;
+    }
+    HIP_TRY(hipEventRecord(c->ev_tail[par], c->tail_stream));
+    c->tail_inflight[par] = true;
+    c->tail_par = par;
+    c->tail_pending = true;
+  }
   return MPPI_OK;
+}
+
+void fill_outputs(const float* o, int H, mppi_outputs* out) {
+  if (out->u1_opt) std::memcpy(out->u1_opt, o, H * sizeof(float));
+  if (out->u2_opt) std::memcpy(out->u2_opt, o + H, H * sizeof(float));
+  if (out->lin_vel) std::memcpy(out->lin_vel, o + 2 * H, H * sizeof(float));
+  if (out->ang_vel) std::memcpy(out->ang_vel, o + 3 * H, H * sizeof(float));
+  if (out->traj_sim) std::memcpy(out->traj_sim, o + 4 * H, 3 * H * sizeof(float));
+  if (out->heading_sim) std::memcpy(out->heading_sim, o + 7 * H, 3 * H * sizeof(float));
+  if (out->left_wheel_sim) std::memcpy(out->left_wheel_sim, o + 10 * H, 3 * H * sizeof(float));
+  if (out->right_wheel_sim) std::memcpy(out->right_wheel_sim, o + 13 * H, 3 * H * sizeof(float));
 }
 
 int copy_outputs(mppi_ctx* c, mppi_outputs* out) {
   const int H = H_of(c);
-  HIP_TRY(hipMemcpyAsync(c->out_host, c->out_dev, (size_t)16 * H * sizeof(float),
-                         hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  int rc = wait_done(c);
+  if (rc) return rc;
+  if (c->async_tail) {
+    // controls + the first optimal-rollout row now; rows 1.. arrive with the tail
+    const float* stage = c->stage;
+    collect_timing(c);
+    c->cur ^= 1;
+    std::memcpy(c->out_host, stage, (size_t)4 * H * sizeof(float));
+    if (out) {
+      const float* o = stage;
+      if (out->u1_opt) std::memcpy(out->u1_opt, o, H * sizeof(float));
+      if (out->u2_opt) std::memcpy(out->u2_opt, o + H, H * sizeof(float));
+      if (out->lin_vel) std::memcpy(out->lin_vel, o + 2 * H, H * sizeof(float));
+      if (out->ang_vel) std::memcpy(out->ang_vel, o + 3 * H, H * sizeof(float));
+      if (out->traj_sim) std::memcpy(out->traj_sim, o + 4 * H, 3 * sizeof(float));
+      if (out->heading_sim) std::memcpy(out->heading_sim, o + 4 * H + 3, 3 * sizeof(float));
+      if (out->left_wheel_sim) std::memcpy(out->left_wheel_sim, o + 4 * H + 6, 3 * sizeof(float));
+      if (out->right_wheel_sim) std::memcpy(out->right_wheel_sim, o + 4 * H + 9, 3 * sizeof(float));
+    }
+    return MPPI_OK;
+  }
+  std::memcpy(c->out_host, c->stage, (size_t)16 * H * sizeof(float));
   collect_timing(c);
   c->cur ^= 1;  // the finish kernel wrote the new nominal sequence into u_nom[cur^1]
-  if (out) {
-    const float* o = c->out_host;
-    if (out->u1_opt) std::memcpy(out->u1_opt, o, H * sizeof(float));
-    if (out->u2_opt) std::memcpy(out->u2_opt, o + H, H * sizeof(float));
-    if (out->lin_vel) std::memcpy(out->lin_vel, o + 2 * H, H * sizeof(float));
-    if (out->ang_vel) std::memcpy(out->ang_vel, o + 3 * H, H * sizeof(float));
-    if (out->traj_sim) std::memcpy(out->traj_sim, o + 4 * H, 3 * H * sizeof(float));
-    if (out->heading_sim) std::memcpy(out->heading_sim, o + 7 * H, 3 * H * sizeof(float));
-    if (out->left_wheel_sim) std::memcpy(out->left_wheel_sim, o + 10 * H, 3 * H * sizeof(float));
-    if (out->right_wheel_sim) std::memcpy(out->right_wheel_sim, o + 13 * H, 3 * H * sizeof(float));
-  }
+  if (out) fill_outputs(c->out_host, H, out);
   return MPPI_OK;
 }
 
@@ -466,9 +579,13 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   if (hipMalloc(&c->u_nom[0], 2 * H * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->u_nom[1], 2 * H * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->cost, std::max<int64_t>(p.num_trajectories, 1) * sizeof(float)) != hipSuccess ||
-      hipMalloc(&c->out_dev, 16 * H * sizeof(float)) != hipSuccess ||
+      hipHostMalloc(&c->stage, 16 * H * sizeof(float), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&c->done, 64, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
-      hipHostMalloc(&c->out_host, 16 * H * sizeof(float), hipHostMallocDefault) != hipSuccess)
+      hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
+      hipMalloc(&c->tail_in[1], 3 * H * sizeof(float)) != hipSuccess ||
+      hipHostMalloc(&c->tail_host[0], 12 * H * sizeof(float), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&c->tail_host[1], 12 * H * sizeof(float), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "device allocation failed"));
   if (hipMemset(c->u_nom[0], 0, 2 * H * sizeof(float)) != hipSuccess ||
       hipMemset(c->u_nom[1], 0, 2 * H * sizeof(float)) != hipSuccess ||
@@ -476,6 +593,14 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(MPPI_EHIP, "hipEventCreate failed"));
+  if (hipEventCreateWithFlags(&c->ev_fin_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_tail[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_tail[1], hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->tail_stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(MPPI_EHIP, "side stream / event creation failed"));
+  c->out_host = new float[16 * H]();
+  std::memset(c->stage, 0, 16 * H * sizeof(float));
+  *c->done = 0;
   if (hipDeviceSynchronize() != hipSuccess) return cleanup(fail(MPPI_EHIP, "device sync failed"));
   *out = c;
   return MPPI_OK;
@@ -485,6 +610,7 @@ void mppi_destroy(mppi_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->tail_stream) hipStreamSynchronize(c->tail_stream);
   if (c->Z_owned && c->Z) hipFree(c->Z);
   if (c->cm) hipFree(c->cm);
   for (float* u : c->u_nom)
@@ -495,8 +621,16 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->scratch1) hipFree(c->scratch1);
   if (c->record) hipFree(c->record);
   if (c->ustore) hipFree(c->ustore);
-  if (c->out_dev) hipFree(c->out_dev);
-  if (c->out_host) hipHostFree(c->out_host);
+  if (c->stage) hipHostFree(c->stage);
+  if (c->done) hipHostFree(c->done);
+  delete[] c->out_host;
+  for (int i = 0; i < 2; ++i) {
+    if (c->tail_in[i]) hipFree(c->tail_in[i]);
+    if (c->tail_host[i]) hipHostFree(c->tail_host[i]);
+    if (c->ev_tail[i]) hipEventDestroy(c->ev_tail[i]);
+  }
+  if (c->ev_fin_done) hipEventDestroy(c->ev_fin_done);
+  if (c->tail_stream) hipStreamDestroy(c->tail_stream);
   if (c->inj1) hipFree(c->inj1);
   if (c->inj2) hipFree(c->inj2);
   for (auto& e : c->ev)
@@ -509,6 +643,8 @@ int mppi_set_stream(mppi_ctx* c, void* s) {
   if (!c) return fail(MPPI_EINVAL, "null context");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  int rc = sync_tail(c);
+  if (rc) return rc;
   if (c->own_stream && c->stream) HIP_TRY(hipStreamDestroy(c->stream));
   if (s) {
     c->stream = (hipStream_t)s;
@@ -532,6 +668,8 @@ int mppi_set_dem(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float 
   int rc = check_grid(rows, cols, resolution);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
+  rc = sync_tail(c);  // a deferred optimal rollout may still read the DEM
+  if (rc) return rc;
   const size_t bytes = (size_t)rows * cols * sizeof(float);
   if (!c->Z_owned || bytes > c->Z_cap) {
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -558,6 +696,8 @@ int mppi_set_dem_device(mppi_ctx* c, const float* z, int32_t rows, int32_t cols,
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  rc = sync_tail(c);
+  if (rc) return rc;
   if (c->Z_owned && c->Z) HIP_TRY(hipFree(c->Z));
   c->Z = const_cast<float*>(z);
   c->Z_owned = false;
@@ -711,9 +851,39 @@ int mppi_dump_rollouts(mppi_ctx* c, float* traj, float* hv, float* lw, float* rw
 
 int mppi_set_timing(mppi_ctx* c, int32_t enable) {
   if (!c) return fail(MPPI_EINVAL, "null context");
+  int rc = sync_tail(c);
+  if (rc) return rc;
   c->timing = enable != 0;
-  c->t_roll = c->t_fin = 0.0;
-  c->launches = 0;
+  c->t_roll = c->t_fin = c->t_tail = 0.0;
+  c->launches = c->tail_launches = 0;
+  c->ev_roll_pending = c->ev_fin_pending = c->ev_tail_pending = false;
+  return MPPI_OK;
+}
+
+int mppi_get_tail_timing(mppi_ctx* c, double* tail_ms, int64_t* n) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  int rc = sync_tail(c);
+  if (rc) return rc;
+  if (tail_ms) *tail_ms = c->t_tail;
+  if (n) *n = c->tail_launches;
+  return MPPI_OK;
+}
+
+int mppi_set_async_tail(mppi_ctx* c, int32_t enable) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = sync_tail(c);
+  if (rc) return rc;
+  c->async_tail = enable != 0;
+  return MPPI_OK;
+}
+
+int mppi_get_outputs(mppi_ctx* c, mppi_outputs* out) {
+  if (!c || !out) return fail(MPPI_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = sync_tail(c);
+  if (rc) return rc;
+  fill_outputs(c->out_host, H_of(c), out);
   return MPPI_OK;
 }
 

@@ -49,7 +49,8 @@ struct RolloutArgs {
 
 struct FinishArgs {
   int H;
-  int mode;  // 0: write root record, 1: finish (u_opt + optimal rollout)
+  int mode;  // 0: write root record, 1: finish (u_opt + optimal rollout),
+             // 2: finish with the optimal rollout deferred to mppi_tail_kernel (step 0 only here)
   const double* recs;
   int n_recs;
   double* scratch0;
@@ -66,6 +67,13 @@ struct FinishArgs {
   int win_offset;  // LDS byte offset of the window
   float x0, y0, h0x, h0y, h0z, wl, wr;
   float ok, oa, rwheel, vmin, vmax, wmin, wmax, dt, off;
+  // deferred optimal rollout (mode 2 / mppi_tail_kernel)
+  float* tail_in;   // [3H] v, sin(w dt), cos(w dt) of the optimal sequence
+  float* tail_out;  // [12H] traj, hv, lw, rw (pinned host memory)
+  // completion: after every output store, lane 0 stores `seq` to *done (pinned host
+  // memory, system scope, release) so the host can spin on it instead of a stream sync
+  unsigned* done;
+  unsigned seq;
 };
 
 hipError_t launch_rollout(const RolloutArgs& a, int block, int blocks, size_t lds, hipStream_t st,
@@ -75,6 +83,9 @@ constexpr int WS_TRAJ = 256;
 hipError_t launch_rollout_ws(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
                              int mode, bool dump);
 hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool use_lds);
+// optimal rollout of the sequence a mode-2 finish left in f.tail_in (one workgroup)
+constexpr int TAIL_THREADS = 256;
+hipError_t launch_tail(const FinishArgs& f, hipStream_t st);
 hipError_t launch_selftest(int what, int64_t n, uint64_t seed, unsigned long long* bad, hipStream_t st);
 hipError_t launch_bilinear(const float* Z, int rows, int grid, float x_min, float y_min, float res,
                            const float* xs, const float* ys, float* hs, int64_t n, hipStream_t st);

@@ -1080,6 +1080,85 @@ __device__ __forceinline__ double group8_apply(const PairScale* ps, const double
   return pair_apply(ps[6], b[0], b[1], j);
 }
 
+// The 3D rollout of the optimal sequence for `nsteps` steps from the robot pose
+// (projection_warp.py:306-348 on one trajectory): the serial chain on lane 0
+// (12 floats per step into LDS `chain`), then heights and wheel contacts on all
+// lanes.  Writes traj[3n] | hv[3n] | lw[3n] | rw[3n] at `out`.
+template <bool LDS>
+__device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem<LDS>& dem, const float* vb,
+                                                const float* snb, const float* csb, float* chain,
+                                                int nsteps, float* out, int tid, int nthreads) {
+  const float res_half_neg = (-f.res) / 2.0f;
+  const float res_sq = f.res * f.res;
+  if (tid == 0) {  // the serial chain (projection_warp.py:306-326)
+    Traj s;
+    s.x = f.x0;
+    s.y = f.y0;
+    {
+      bool unused = false;
+      float q[4];
+      dem.template corners<false>(s.x, s.y, q, unused);
+      const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
+      const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
+      const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
+      const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
+      const float d = (f.h0x * nx + f.h0y * ny) + f.h0z * nz;
+      const float tx = f.h0x - d * nx, ty = f.h0y - d * ny, tz = f.h0z - d * nz;
+      const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
+      s.hx = tx / tn;
+      s.hy = ty / tn;
+      s.hz = tz / tn;
+    }
+    float vn = vb[0], sn_n = snb[0], cs_n = csb[0];
+    for (int t = 0; t < nsteps; ++t) {
+      const float v = vn, sn = sn_n, cs = cs_n;
+      const int tn = min(t + 1, nsteps - 1);  // prefetch the next step's inputs from LDS
+      vn = vb[tn];
+      sn_n = snb[tn];
+      cs_n = csb[tn];
+      const Traj saved = s;
+      float q[4], nx, ny, nz;
+      bool bad = false;
+      chain3d<kChainFast, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+      if (kChainFast && __builtin_expect(bad, 0)) {
+        s = saved;
+        chain3d<false, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+      }
+      float* ch = chain + 12 * t;
+      ch[0] = s.x; ch[1] = s.y;
+      ch[2] = q[0]; ch[3] = q[1]; ch[4] = q[2]; ch[5] = q[3];
+      ch[6] = nx; ch[7] = ny; ch[8] = nz;
+      ch[9] = s.hx; ch[10] = s.hy; ch[11] = s.hz;
+    }
+  }
+  __syncthreads();
+  for (int t = tid; t < nsteps; t += nthreads) {  // heights + wheel contacts, all lanes
+    const float* ch = chain + 12 * t;
+    const float q[4] = {ch[2], ch[3], ch[4], ch[5]};
+    StepOut o;
+    bool bad = false;
+    wheels3d<kFastMath, LDS>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
+    if (kFastMath && bad)
+      wheels3d<false, LDS>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
+    float* o_traj = out + 3 * t;
+    float* o_hv = out + 3 * nsteps + 3 * t;
+    float* o_lw = out + 6 * nsteps + 3 * t;
+    float* o_rw = out + 9 * nsteps + 3 * t;
+    o_traj[0] = ch[0]; o_traj[1] = ch[1]; o_traj[2] = o.z;
+    o_hv[0] = ch[9]; o_hv[1] = ch[10]; o_hv[2] = ch[11];
+    o_lw[0] = o.lx; o_lw[1] = o.ly; o_lw[2] = o.lz;
+    o_rw[0] = o.rx; o_rw[1] = o.ry; o_rw[2] = o.rz;
+  }
+}
+
+// Make every lane's output stores visible system-wide, then publish f.seq.
+__device__ __forceinline__ void signal_done(const FinishArgs& f) {
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0 && f.done)
+    __hip_atomic_store(f.done, f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <bool LDS>
 __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishArgs f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -1186,16 +1265,25 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
       for (int c2 = lane; c2 < f.W; c2 += 64) dst[c2] = src[c2];
     }
   }
+  // optimal-sequence wheel filter (sampling_warp.py:120-138, k=3.0, a=0.92): the
+  // inputs (u*k)*(1-a) in parallel, only the recurrence L = L*a + in on lane 0
+  const float one_m_a = 1.0f - f.oa;
+  if (tid < 2 * H) uo[tid] = (uo[tid] * f.ok) * one_m_a;
   __syncthreads();
-  if (tid == 0) {  // optimal-sequence wheel filter (sampling_warp.py:120-138, k=3.0, a=0.92)
+  if (tid == 0) {
     float L = f.wl, R = f.wr;
-    const float one_m_a = 1.0f - f.oa;
     for (int t = 0; t < H; ++t) {
-      L = L * f.oa + (uo[t] * f.ok) * one_m_a;
-      R = R * f.oa + (uo[H + t] * f.ok) * one_m_a;
-      vb[t] = clampf((L + R) / 2.0f, f.vmin, f.vmax);
-      wb[t] = clampf(((-L) + R) / f.rwheel, f.wmin, f.wmax);
+      L = L * f.oa + uo[t];
+      R = R * f.oa + uo[H + t];
+      vb[t] = L;
+      wb[t] = R;
     }
+  }
+  __syncthreads();
+  for (int t = tid; t < H; t += FIN_THREADS) {
+    const float L = vb[t], R = wb[t];
+    vb[t] = clampf((L + R) / 2.0f, f.vmin, f.vmax);
+    wb[t] = clampf(((-L) + R) / f.rwheel, f.wmin, f.wmax);
   }
   __syncthreads();
   for (int t = tid; t < H; t += FIN_THREADS) {
@@ -1205,71 +1293,37 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
     csb[t] = cs;
     f.out[2 * H + t] = vb[t];
     f.out[3 * H + t] = wb[t];
+    if (f.mode == 2) {  // inputs of the deferred optimal rollout (mppi_tail_kernel)
+      f.tail_in[t] = vb[t];
+      f.tail_in[H + t] = sn;
+      f.tail_in[2 * H + t] = cs;
+    }
   }
   __syncthreads();
   Dem<LDS> dem;
   dem.init(f.Z, win, f.rows, f.grid, f.wx0, f.wy0, f.W, f.Wr, f.x_min, f.y_min, f.res);
-  const float res_half_neg = (-f.res) / 2.0f;
-  const float res_sq = f.res * f.res;
-  if (tid == 0) {  // the serial chain (projection_warp.py:306-326)
-    Traj s;
-    s.x = f.x0;
-    s.y = f.y0;
-    {
-      bool unused = false;
-      float q[4];
-      dem.template corners<false>(s.x, s.y, q, unused);
-      const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
-      const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
-      const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
-      const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
-      const float d = (f.h0x * nx + f.h0y * ny) + f.h0z * nz;
-      const float tx = f.h0x - d * nx, ty = f.h0y - d * ny, tz = f.h0z - d * nz;
-      const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
-      s.hx = tx / tn;
-      s.hy = ty / tn;
-      s.hz = tz / tn;
-    }
-    float vn = vb[0], sn_n = snb[0], cs_n = csb[0];
-    for (int t = 0; t < H; ++t) {
-      const float v = vn, sn = sn_n, cs = cs_n;
-      const int tn = min(t + 1, H - 1);  // prefetch the next step's inputs from LDS
-      vn = vb[tn];
-      sn_n = snb[tn];
-      cs_n = csb[tn];
-      const Traj saved = s;
-      float q[4], nx, ny, nz;
-      bool bad = false;
-      chain3d<kChainFast, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-      if (kChainFast && __builtin_expect(bad, 0)) {
-        s = saved;
-        chain3d<false, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-      }
-      float* ch = chain + 12 * t;
-      ch[0] = s.x; ch[1] = s.y;
-      ch[2] = q[0]; ch[3] = q[1]; ch[4] = q[2]; ch[5] = q[3];
-      ch[6] = nx; ch[7] = ny; ch[8] = nz;
-      ch[9] = s.hx; ch[10] = s.hy; ch[11] = s.hz;
-    }
-  }
+  // mode 1: the whole optimal rollout; mode 2: its first step only (the pose the
+  // closed loop needs now), the rest runs in mppi_tail_kernel on a side stream
+  optimal_rollout<LDS>(f, dem, vb, snb, csb, chain, f.mode == 2 ? 1 : H, f.out + 4 * H, tid, FIN_THREADS);
+  signal_done(f);
+}
+
+// Deferred optimal rollout (MPPI_isaac.py:696-720) of the sequence a mode-2
+// finish left in f.tail_in; launched on a side stream so that it overlaps the
+// next step's rollout kernel.  Bitwise identical to the mode-1 finish.
+__global__ __launch_bounds__(TAIL_THREADS) void mppi_tail_kernel(const FinishArgs f) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int tid = threadIdx.x;
+  const int H = f.H;
+  float* vb = reinterpret_cast<float*>(smem_raw);
+  float* snb = vb + H;
+  float* csb = snb + H;
+  float* chain = csb + H;
+  for (int i = tid; i < 3 * H; i += TAIL_THREADS) vb[i] = f.tail_in[i];
   __syncthreads();
-  for (int t = tid; t < H; t += FIN_THREADS) {  // heights + wheel contacts, all lanes
-    const float* ch = chain + 12 * t;
-    const float q[4] = {ch[2], ch[3], ch[4], ch[5]};
-    StepOut o;
-    bool bad = false;
-    wheels3d<kFastMath, LDS>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
-    if (kFastMath && bad)
-      wheels3d<false, LDS>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
-    float* o_traj = f.out + 4 * H + 3 * t;
-    float* o_hv = f.out + 7 * H + 3 * t;
-    float* o_lw = f.out + 10 * H + 3 * t;
-    float* o_rw = f.out + 13 * H + 3 * t;
-    o_traj[0] = ch[0]; o_traj[1] = ch[1]; o_traj[2] = o.z;
-    o_hv[0] = ch[9]; o_hv[1] = ch[10]; o_hv[2] = ch[11];
-    o_lw[0] = o.lx; o_lw[1] = o.ly; o_lw[2] = o.lz;
-    o_rw[0] = o.rx; o_rw[1] = o.ry; o_rw[2] = o.rz;
-  }
+  Dem<false> dem;
+  dem.init(f.Z, nullptr, f.rows, f.grid, 0, 0, 1, 1, f.x_min, f.y_min, f.res);
+  optimal_rollout<false>(f, dem, vb, snb, csb, chain, H, f.tail_out, tid, TAIL_THREADS);
 }
 
 // =====================================================================  standalone bilinear
@@ -1400,6 +1454,12 @@ hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool u
     hipLaunchKernelGGL(mppi_finish_kernel<true>, dim3(1), dim3(FIN_THREADS), lds, st, f);
   else
     hipLaunchKernelGGL(mppi_finish_kernel<false>, dim3(1), dim3(FIN_THREADS), lds, st, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_tail(const FinishArgs& f, hipStream_t st) {
+  const size_t lds = (size_t)15 * f.H * sizeof(float);
+  hipLaunchKernelGGL(mppi_tail_kernel, dim3(1), dim3(TAIL_THREADS), lds, st, f);
   return hipGetLastError();
 }
 

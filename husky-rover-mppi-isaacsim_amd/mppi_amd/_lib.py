@@ -76,6 +76,8 @@ _PROTOS = {
     "mppi_get_nominal": (C.c_int, [C.c_void_p, _FP, _FP]),
     "mppi_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.POINTER(MppiOutputs)]),
     "mppi_step_injected": (C.c_int, [C.c_void_p, C.c_int32, _FP, _FP, C.POINTER(MppiOutputs)]),
+    "mppi_set_async_tail": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mppi_get_outputs": (C.c_int, [C.c_void_p, C.POINTER(MppiOutputs)]),
     "mppi_record_len": (C.c_int64, [C.c_void_p]),
     "mppi_step_partial": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.c_void_p]),
     "mppi_step_finish": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(MppiOutputs)]),
@@ -84,6 +86,7 @@ _PROTOS = {
     "mppi_set_timing": (C.c_int, [C.c_void_p, C.c_int32]),
     "mppi_get_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_int64)]),
+    "mppi_get_tail_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "mppi_set_dem_path": (C.c_int, [C.c_void_p, C.c_int32]),
     "mppi_get_launch_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]),
     "mppi_bilinear_query": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
@@ -189,6 +192,7 @@ class Engine:
         self._buf = {n: np.zeros(3 * H if n.endswith("_sim") else H, np.float32) for n in self.OUT_NAMES}
         self._out = MppiOutputs(*[_fp(self._buf[n]) for n in self.OUT_NAMES])
         self._keep = []
+        self.async_tail = False
 
     # ------------------------------------------------------------ lifetime
     def close(self):
@@ -275,6 +279,17 @@ class Engine:
                 "mppi_step_injected")
         return self._outputs()
 
+    def set_async_tail(self, on=True):
+        """Deferred optimal rollout: step() returns the controls + row 0 of the *_sim arrays;
+        outputs() waits for the rest (bitwise identical)."""
+        self._c(self.lib.mppi_set_async_tail(self.ctx, 1 if on else 0), "mppi_set_async_tail")
+        self.async_tail = bool(on)
+
+    def outputs(self):
+        """All outputs of the last step (waits for a deferred optimal rollout)."""
+        self._c(self.lib.mppi_get_outputs(self.ctx, C.byref(self._out)), "mppi_get_outputs")
+        return self._outputs()
+
     def record_len(self):
         return int(self.lib.mppi_record_len(self.ctx))
 
@@ -313,6 +328,12 @@ class Engine:
         n = C.c_int64()
         self._c(self.lib.mppi_get_timing(self.ctx, C.byref(r), C.byref(f), C.byref(n)), "mppi_get_timing")
         return r.value, f.value, n.value
+
+    def tail_timing(self):
+        t = C.c_double()
+        n = C.c_int64()
+        self._c(self.lib.mppi_get_tail_timing(self.ctx, C.byref(t), C.byref(n)), "mppi_get_tail_timing")
+        return t.value, n.value
 
     def launch_info(self):
         info = (C.c_int64 * 6)()

@@ -205,6 +205,9 @@ class MPPI_Controller:
         self.device = int(eng.get("device", 0))
         self.kernel = eng.get("kernel", "default")
         self.max_loops = int(eng.get("max_loops", 3500))
+        # deferred optimal rollout: MPPI_step returns with the controls and row 0 of the
+        # *_sim arrays; the other rows are fetched on first access (bitwise identical)
+        self.async_tail = bool(eng.get("async_tail", True))
         self.step_index = 0          # Philox step counter (replaces rng.integers at :517)
         self.engine = None
         self._out = None
@@ -225,6 +228,8 @@ class MPPI_Controller:
             self.engine.close()
         self.engine = _lib.Engine(self._params(), self.device)
         self.engine.set_dem_path({"default": "auto"}.get(self.kernel, self.kernel))
+        self.engine.set_async_tail(self.async_tail)
+        self._tail_fresh = True
         self._upload_dem(self.surface.Z)
         self._upload_costmap(self.surface.costmap)
         H, K = self.number_of_iterations, self.number_of_trajectories
@@ -242,10 +247,10 @@ class MPPI_Controller:
                                          lambda v: self._set_nominal(None, v), "optimal_u2_wp")
         self.optimal_lin_vel_wp = EngineArray(lambda: self._out["lin_vel"], name="optimal_lin_vel_wp")
         self.optimal_ang_vel_wp = EngineArray(lambda: self._out["ang_vel"], name="optimal_ang_vel_wp")
-        self.trajectories_sim = EngineArray(lambda: self._out["traj_sim"], name="trajectories_sim")
-        self.heading_vectors_sim = EngineArray(lambda: self._out["heading_sim"], name="heading_vectors_sim")
-        self.left_wheel_pos_sim = EngineArray(lambda: self._out["left_wheel_sim"], name="left_wheel_pos_sim")
-        self.right_wheel_pos_sim = EngineArray(lambda: self._out["right_wheel_sim"], name="right_wheel_pos_sim")
+        self.trajectories_sim = EngineArray(lambda: self._sim("traj_sim"), name="trajectories_sim")
+        self.heading_vectors_sim = EngineArray(lambda: self._sim("heading_sim"), name="heading_vectors_sim")
+        self.left_wheel_pos_sim = EngineArray(lambda: self._sim("left_wheel_sim"), name="left_wheel_pos_sim")
+        self.right_wheel_pos_sim = EngineArray(lambda: self._sim("right_wheel_sim"), name="right_wheel_pos_sim")
         self.costs_wp = EngineArray(self._costs, name="costs_wp")
         self.weights_wp = EngineArray(self._weights, name="weights_wp")
         self.costmap_wp = EngineArray(lambda: np.asarray(self.surface.costmap, np.float32).ravel(),
@@ -313,6 +318,13 @@ class MPPI_Controller:
         c1, c2 = self.engine.get_nominal()
         self.engine.set_nominal(c1 if u1 is None else u1, c2 if u2 is None else u2)
 
+    def _sim(self, key):
+        """Optimal-rollout arrays; waits for the deferred rollout on first access after a step."""
+        if not self._tail_fresh:
+            self._out = self.engine.outputs()
+            self._tail_fresh = True
+        return self._out[key]
+
     def _costs(self):
         return self.engine.costs()
 
@@ -353,6 +365,7 @@ class MPPI_Controller:
             raise RuntimeError("call warp_setup() first")
         self.engine.set_state(self._state())
         self._out = self.engine.step(proj, self.step_index)
+        self._tail_fresh = not self.async_tail
         self._dump = None
         self.step_index += 1
 
@@ -374,8 +387,9 @@ class MPPI_Controller:
                and self.loop < self.max_loops):
             self.reset("controller")
             self.MPPI_step(proj=proj)
-            traj = self.trajectories_sim.numpy()
-            hv = self.heading_vectors_sim.numpy()
+            # row 0 of the optimal rollout is returned with the step itself
+            traj = self._out["traj_sim"]
+            hv = self._out["heading_sim"]
             self.robot.update_position(traj[0][0], traj[0][1], traj[0][2], hv[0])
             lin_vel = self.optimal_lin_vel_wp.numpy()[0]
             ang_vel = self.optimal_ang_vel_wp.numpy()[0]

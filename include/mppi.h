@@ -139,6 +139,19 @@ int mppi_step(mppi_ctx* ctx, int32_t proj, uint64_t step, mppi_outputs* out);
 int mppi_step_injected(mppi_ctx* ctx, int32_t proj, const float* u1_host, const float* u2_host,
                        mppi_outputs* out);
 
+/* Deferred optimal rollout.  With enable != 0, mppi_step / mppi_step_finish /
+ * mppi_step_injected return as soon as the control outputs are in host memory:
+ * u1_opt, u2_opt, lin_vel, ang_vel in full and ROW 0 of traj_sim, heading_sim,
+ * left_wheel_sim, right_wheel_sim (the pose MPPI_Controller.run consumes,
+ * MPPI_isaac.py:769-773).  The rest of the optimal rollout
+ * (MPPI_isaac.py:696-720) runs on a side stream, overlapping whatever the
+ * caller enqueues next (typically the next step's rollout), and its rows are
+ * copied to pinned host memory; mppi_get_outputs waits for it.  Values are
+ * bitwise identical to the synchronous mode (enable = 0, the default). */
+int mppi_set_async_tail(mppi_ctx* ctx, int32_t enable);
+/* All outputs of the last step (waits for a deferred optimal rollout). */
+int mppi_get_outputs(mppi_ctx* ctx, mppi_outputs* out);
+
 /* ---- K-sharded multi-GPU step (no reference equivalent) ----
  * Record = [m, S, V1[H], V2[H]] float64 (mppi_record_len() doubles).
  * mppi_step_partial enqueues this rank's rollout and writes its record to
@@ -162,6 +175,8 @@ int mppi_dump_rollouts(mppi_ctx* ctx, float* traj, float* heading, float* left_w
  * kernel, measured on the context stream around each launch. */
 int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
 int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_t* launches);
+/* HIP-event time of the deferred optimal-rollout kernels (side stream). */
+int mppi_get_tail_timing(mppi_ctx* ctx, double* tail_ms, int64_t* launches);
 
 /* Rollout kernel variant: 0 = default (= 3); 1 = one wave per trajectory group
  * with the DEM window staged in LDS (error if it does not fit); 2 = one wave per

@@ -86,3 +86,35 @@ def test_partial_finish_shards_on_one_gpu(K, H, world):
             assert np.array_equal(outs[0][a], one[a]), a
     for e in engines:
         e.close()
+
+
+@pytest.mark.parametrize("proj", ["3d", "2d"])
+def test_async_tail_bitwise_equal_to_sync(proj):
+    """Deferred optimal rollout: controls + row 0 at return, all rows after outputs(); identical to sync mode."""
+    K, H = 2048, 40
+    Z, hw, cm = hp.c3_scene()
+    st = hp.oracle_state(wl=0.3, wr=0.5)
+    sync = hp.engine_for(K, H, Z, hw, cm, st, seed=9)
+    asyn = hp.engine_for(K, H, Z, hw, cm, st, seed=9)
+    asyn.set_async_tail(True)
+    for i in range(4):          # nominal chain across steps, tails overlapping the next rollout
+        a = asyn.step(proj, i)
+        b = sync.step(proj, i)
+        for k in ("u1_opt", "u2_opt", "lin_vel", "ang_vel"):
+            assert np.array_equal(a[k], b[k]), (i, k)
+        for k in ("traj_sim", "heading_sim", "left_wheel_sim", "right_wheel_sim"):
+            assert np.array_equal(a[k][0], b[k][0]), (i, k, "row 0")
+        if i % 2 == 1:
+            full = asyn.outputs()
+            for k in b:
+                assert np.array_equal(full[k], b[k]), (i, k)
+    # a DEM change waits for the in-flight tail; the next step sees the new terrain
+    asyn.set_dem(Z * 2.0, hw)
+    sync.set_dem(Z * 2.0, hw)
+    a = asyn.step(proj, 7)
+    b = sync.step(proj, 7)
+    full = asyn.outputs()
+    for k in b:
+        assert np.array_equal(full[k], b[k]), k
+    t_ms, n = asyn.tail_timing()
+    assert n == 0 or t_ms > 0
