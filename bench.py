@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--k-per-gpu", type=int, default=65536)
     ap.add_argument("--horizon", type=int, default=100)
     ap.add_argument("--proj", default="3d")
-    ap.add_argument("--dem-path", default="auto", choices=["auto", "lds", "global", "ws"])
+    ap.add_argument("--dem-path", default="auto", choices=["auto", "lds", "global", "ws", "pair"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="bounded oracle sample on the host (rank 0, N=1); 0 disables")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 
 #include "mppi.h"
 #include "mppi_kernels.h"
@@ -38,6 +39,7 @@ constexpr size_t kLdsBytes = 160 * 1024;
 struct Plan {
   bool lds = false;       // rollout kernel DEM path
   bool ws = false;        // warp-specialised rollout kernel (chain + side waves)
+  bool pair = false;      // ... synchronised per chain/side pair (default)
   int traj_per_block = 256;
   bool fin_lds = false;   // finish kernel DEM path
   int block = 256, blocks = 0;
@@ -64,6 +66,10 @@ struct mppi_ctx {
   size_t cm_cap = 0;
   int cm_size = 0;
   float cm_hw = 0, cm_res = 0;
+  // verified division-by-constant reciprocals (0 = use the IEEE division)
+  float rinv_res = 0, rinv_res_c = 0;
+  unsigned* cdiv_bad = nullptr;  // device counter for launch_cdiv_verify
+  std::unordered_map<uint32_t, float> cdiv_cache;  // divisor bits -> verified y (0: none)
   // state
   mppi_state st{};
   bool have_state = false;
@@ -114,6 +120,38 @@ struct mppi_ctx {
 namespace {
 
 int H_of(const mppi_ctx* c) { return c->p.num_iterations; }
+
+// Reciprocal y for cdiv_f(a, b, y) that reproduces the IEEE quotient for every
+// significand (checked exhaustively on the device, 2^23 cases); 0 if none of
+// RN(1/b) and its two neighbours qualifies.  Cached per divisor.
+int verified_reciprocal(mppi_ctx* c, float b, float* y_out) {
+  uint32_t key;
+  std::memcpy(&key, &b, 4);
+  auto it = c->cdiv_cache.find(key);
+  if (it != c->cdiv_cache.end()) {
+    *y_out = it->second;
+    return MPPI_OK;
+  }
+  float y = 0.0f;
+  if (std::isfinite(b) && b != 0.0f) {
+    const float y0 = (float)(1.0 / (double)b);
+    const float cand[3] = {y0, std::nextafter(y0, 0.0f), std::nextafter(y0, 2.0f * y0)};
+    for (float yc : cand) {
+      unsigned bad = 1;
+      HIP_TRY(hipMemsetAsync(c->cdiv_bad, 0, sizeof(unsigned), c->stream));
+      HIP_TRY(launch_cdiv_verify(b, yc, c->cdiv_bad, c->stream));
+      HIP_TRY(hipMemcpyAsync(&bad, c->cdiv_bad, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (bad == 0) {
+        y = yc;
+        break;
+      }
+    }
+  }
+  c->cdiv_cache[key] = y;
+  *y_out = y;
+  return MPPI_OK;
+}
 int E_of(const mppi_ctx* c) { return 2 * c->p.num_iterations + 2; }
 
 int check_ready(mppi_ctx* c) {
@@ -170,17 +208,22 @@ Plan make_plan(const mppi_ctx* c) {
   const size_t scratch = ((size_t)(pl.block + NW) * sizeof(float) + 15) / 16 * 16 +
                          (size_t)(NW / 4) * (2 * H + 2) * sizeof(double);
   pl.lds_bytes = std::max(pl.lds ? win : (size_t)0, scratch);
-  if (c->dem_path == 3 || c->dem_path == 0) {
-    // default: warp-specialised kernel (rings [2][7][TB] + cost[TB] + scratch in LDS, DEM via
-    // L1/L2): measured fastest at C3 (profiles/r01_notes.md)
+  if (c->dem_path == 3 || c->dem_path == 0 || c->dem_path == 4) {
+    // warp-specialised kernels (chain + side waves, DEM via L1/L2).  Default: the
+    // pair-synchronised one (rings [D][6][TB] + cost[TB] + flags + scratch in LDS);
+    // 3: one workgroup barrier per step (rings [2][7][TB]).  profiles/r01_notes.md
     const int TB = WS_TRAJ;
     pl.ws = true;
+    pl.pair = c->dem_path != 3;
     pl.lds = false;
     pl.traj_per_block = TB;
     pl.block = 2 * TB;
     pl.blocks = (int)((K + TB - 1) / TB);
-    pl.lds_bytes = (size_t)15 * TB * sizeof(float) + ((size_t)(TB + TB / 64) * 4 + 15) / 16 * 16 +
-                   (size_t)(TB / 256) * (2 * H + 2) * sizeof(double);
+    const size_t scratch_ws = ((size_t)(TB + TB / 64) * 4 + 15) / 16 * 16 +
+                              (size_t)(TB / 256) * (2 * H + 2) * sizeof(double);
+    pl.lds_bytes = pl.pair ? (size_t)(6 * PAIR_RING + 1) * TB * sizeof(float) + 4 * (TB / 64) * sizeof(int) +
+                                 scratch_ws
+                           : (size_t)15 * TB * sizeof(float) + scratch_ws;
   }
   // finish kernel: tree phase [32][2H+2] doubles + 128*7 PairScale (16 B); tail phase
   // uo[2H] v[H] w[H] sin[H] cos[H] chain[12H] floats, then the DEM window
@@ -230,6 +273,10 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   a.cm_size = c->cm_size;
   a.hw = c->cm_hw;
   a.res_c = c->cm_res;
+  a.rinv_res = c->rinv_res;
+  a.cdiv_res = c->rinv_res != 0.0f;
+  a.rinv_res_c = c->rinv_res_c;
+  a.cdiv_res_c = c->rinv_res_c != 0.0f;
   a.x0 = st.x;
   a.y0 = st.y;
   a.h0x = st.heading[0];
@@ -297,6 +344,8 @@ void fill_finish(const mppi_ctx* c, const Plan& pl, const mppi_state& st, Finish
   f.x_min = c->x_min;
   f.y_min = c->y_min;
   f.res = c->res;
+  f.rinv_res = c->rinv_res;
+  f.cdiv_res = c->rinv_res != 0.0f;
   f.wx0 = pl.wx0;
   f.wy0 = pl.wy0;
   f.W = pl.W;
@@ -403,7 +452,9 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   }
   if (pl.blocks == 0) return MPPI_OK;
   if (c->timing && !dump_args) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-  if (pl.ws)
+  if (pl.pair)
+    HIP_TRY(launch_rollout_pair(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr));
+  else if (pl.ws)
     HIP_TRY(launch_rollout_ws(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr));
   else
     HIP_TRY(launch_rollout(a, pl.block, pl.blocks, pl.lds_bytes, c->stream, pl.lds, proj, mode,
@@ -581,6 +632,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipMalloc(&c->cost, std::max<int64_t>(p.num_trajectories, 1) * sizeof(float)) != hipSuccess ||
       hipHostMalloc(&c->stage, 16 * H * sizeof(float), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&c->done, 64, hipHostMallocDefault) != hipSuccess ||
+      hipMalloc(&c->cdiv_bad, sizeof(unsigned)) != hipSuccess ||
       hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->tail_in[1], 3 * H * sizeof(float)) != hipSuccess ||
@@ -623,6 +675,7 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->ustore) hipFree(c->ustore);
   if (c->stage) hipHostFree(c->stage);
   if (c->done) hipHostFree(c->done);
+  if (c->cdiv_bad) hipFree(c->cdiv_bad);
   delete[] c->out_host;
   for (int i = 0; i < 2; ++i) {
     if (c->tail_in[i]) hipFree(c->tail_in[i]);
@@ -686,7 +739,7 @@ int mppi_set_dem(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float 
   c->x_min = x_min;
   c->y_min = y_min;
   c->res = resolution;
-  return MPPI_OK;
+  return verified_reciprocal(c, resolution, &c->rinv_res);
 }
 
 int mppi_set_dem_device(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float x_min,
@@ -707,7 +760,7 @@ int mppi_set_dem_device(mppi_ctx* c, const float* z, int32_t rows, int32_t cols,
   c->x_min = x_min;
   c->y_min = y_min;
   c->res = resolution;
-  return MPPI_OK;
+  return verified_reciprocal(c, resolution, &c->rinv_res);
 }
 
 int mppi_set_costmap(mppi_ctx* c, const float* cm, int32_t size, float half_width, float resolution) {
@@ -728,7 +781,7 @@ int mppi_set_costmap(mppi_ctx* c, const float* cm, int32_t size, float half_widt
   c->cm_size = size;
   c->cm_hw = half_width;
   c->cm_res = resolution;
-  return MPPI_OK;
+  return verified_reciprocal(c, resolution, &c->rinv_res_c);
 }
 
 int mppi_set_state(mppi_ctx* c, const mppi_state* s) {
@@ -897,7 +950,7 @@ int mppi_get_timing(mppi_ctx* c, double* roll, double* fin, int64_t* n) {
 
 int mppi_set_dem_path(mppi_ctx* c, int32_t mode) {
   if (!c) return fail(MPPI_EINVAL, "null context");
-  if (mode < 0 || mode > 3) return fail(MPPI_EINVAL, "dem path must be 0, 1, 2 or 3");
+  if (mode < 0 || mode > 4) return fail(MPPI_EINVAL, "dem path must be 0, 1, 2, 3 or 4");
   c->dem_path = mode;
   return MPPI_OK;
 }
@@ -905,7 +958,7 @@ int mppi_set_dem_path(mppi_ctx* c, int32_t mode) {
 int mppi_get_launch_info(mppi_ctx* c, int64_t* info, int32_t n) {
   if (!c || !info) return fail(MPPI_EINVAL, "null argument");
   const Plan& pl = c->last_plan;
-  const int64_t v[6] = {pl.ws ? 3 : (pl.lds ? 1 : 0), pl.block, pl.blocks, pl.W, pl.Wr,
+  const int64_t v[6] = {pl.pair ? 4 : (pl.ws ? 3 : (pl.lds ? 1 : 0)), pl.block, pl.blocks, pl.W, pl.Wr,
                         (int64_t)pl.lds_bytes};
   for (int i = 0; i < n && i < 6; ++i) info[i] = v[i];
   return MPPI_OK;

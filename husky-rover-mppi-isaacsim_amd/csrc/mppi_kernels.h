@@ -21,6 +21,9 @@ struct RolloutArgs {
   const float* cm;
   int cm_size;
   float hw, res_c;
+  // verified division-by-constant for grid indices (cdiv_f): reciprocal + enable flag
+  float rinv_res, rinv_res_c;
+  int cdiv_res, cdiv_res_c;
   // robot / goal state (MPPI_isaac.py:489-497, :611-613)
   float x0, y0, h0x, h0y, h0z, wl, wr, gx, gy, s1, s2;
   // sampling
@@ -63,6 +66,8 @@ struct FinishArgs {
   const float* Z;
   int rows, grid;
   float x_min, y_min, res;
+  float rinv_res;
+  int cdiv_res;
   int wx0, wy0, W, Wr;
   int win_offset;  // LDS byte offset of the window
   float x0, y0, h0x, h0y, h0z, wl, wr;
@@ -82,11 +87,17 @@ hipError_t launch_rollout(const RolloutArgs& a, int block, int blocks, size_t ld
 constexpr int WS_TRAJ = 256;
 hipError_t launch_rollout_ws(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
                              int mode, bool dump);
+// pair-synchronised variant (LDS progress counters per chain/side pair instead of barriers)
+constexpr int PAIR_RING = 8;  // = PAIR_D in mppi_kernels.hip
+hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
+                               int mode, bool dump);
 hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool use_lds);
 // optimal rollout of the sequence a mode-2 finish left in f.tail_in (one workgroup)
 constexpr int TAIL_THREADS = 256;
 hipError_t launch_tail(const FinishArgs& f, hipStream_t st);
 hipError_t launch_selftest(int what, int64_t n, uint64_t seed, unsigned long long* bad, hipStream_t st);
+// counts the significands a in [1, 2) for which cdiv_f(a, b, y) != a / b (IEEE)
+hipError_t launch_cdiv_verify(float b, float y, unsigned* bad, hipStream_t st);
 hipError_t launch_bilinear(const float* Z, int rows, int grid, float x_min, float y_min, float res,
                            const float* xs, const float* ys, float* hs, int64_t n, hipStream_t st);
 

@@ -106,6 +106,18 @@ __device__ __forceinline__ float sq(float x, bool& bad) {
   }
 }
 
+// Division by a launch constant b for quotients that are only truncated to a grid
+// index: y = 1/b rounded, q = q0 + (a - q0*b)*y (Markstein's correction).  The
+// host accepts y only after launch_cdiv_verify found the result equal to the IEEE
+// quotient for every significand a in [1, 2); by scaling that covers every a
+// whose quotient has magnitude in [2^-100, 2^126], and a smaller quotient
+// truncates to 0 on both paths.  3 VALU ops instead of the ~10-op IEEE expansion.
+__device__ __forceinline__ float cdiv_f(float a, float b, float y) {
+  const float q0 = a * y;
+  const float r = __builtin_fmaf(-q0, b, a);
+  return __builtin_fmaf(r, y, q0);
+}
+
 // =====================================================================  grid lookups
 // projection_warp.py:39-40 / :338-339 — C-style truncation; clamping is DEFINED
 // here (the reference reads out of bounds).
@@ -121,10 +133,14 @@ struct Dem {
   int rows, grid, wx0, wy0, W, Wr;
   float x_min, y_min, res;
   Recip rres;  // fast-path reciprocal of res (res is validated on the host)
+  float rinv;  // verified reciprocal for cdiv_f (cdiv != 0)
+  int cdiv;
 
   __device__ __forceinline__ void init(const float* Z_, const float* win_, int rows_, int grid_,
                                        int wx0_, int wy0_, int W_, int Wr_, float x_min_,
-                                       float y_min_, float res_) {
+                                       float y_min_, float res_, float rinv_ = 0.0f, int cdiv_ = 0) {
+    rinv = rinv_;
+    cdiv = cdiv_;
     Z = Z_;
     win = win_;
     rows = rows_;
@@ -147,8 +163,16 @@ struct Dem {
   }
   template <bool F>
   __device__ __forceinline__ void cell(float x, float y, int& i, int& j, bool& bad) const {
-    i = trunc_clamped(dv<F>(x - x_min, rr<F>(), bad), -1.0f, (float)grid);
-    j = -trunc_clamped(dv<F>(y + y_min, rr<F>(), bad), -(float)rows, 1.0f);
+    float fi, fj;
+    if (cdiv) {  // uniform branch
+      fi = cdiv_f(x - x_min, res, rinv);
+      fj = cdiv_f(y + y_min, res, rinv);
+    } else {
+      fi = dv<F>(x - x_min, rr<F>(), bad);
+      fj = dv<F>(y + y_min, rr<F>(), bad);
+    }
+    i = trunc_clamped(fi, -1.0f, (float)grid);
+    j = -trunc_clamped(fj, -(float)rows, 1.0f);
   }
   __device__ __forceinline__ float at(int row, int col) const {
     row = clampi(row, 0, rows - 1);
@@ -336,15 +360,28 @@ __device__ __forceinline__ float slope_term(float plx, float ply, float plz, flo
 // critics_warp.py:244-248 costmap index (clamped, DEFINED)
 template <bool F>
 __device__ __forceinline__ int costmap_index(int size, float hw, const Recip& rres_c, float x,
-                                             float y, bool& bad) {
-  const int ix = clampi(trunc_clamped(dv<F>(x + hw, rres_c, bad), -1.0f, (float)size), 0, size - 1);
-  const int iy = clampi(trunc_clamped(dv<F>((-y) + hw, rres_c, bad), -1.0f, (float)size), 0, size - 1);
+                                             float y, bool& bad, float rinv = 0.0f, int cdiv = 0) {
+  float fx, fy;
+  if (cdiv) {  // uniform branch
+    fx = cdiv_f(x + hw, rres_c.b, rinv);
+    fy = cdiv_f((-y) + hw, rres_c.b, rinv);
+  } else {
+    fx = dv<F>(x + hw, rres_c, bad);
+    fy = dv<F>((-y) + hw, rres_c, bad);
+  }
+  const int ix = clampi(trunc_clamped(fx, -1.0f, (float)size), 0, size - 1);
+  const int iy = clampi(trunc_clamped(fy, -1.0f, (float)size), 0, size - 1);
   return ix + size * iy;
 }
 
 #ifdef MPPI_STAMPS
 // Diagnostic build only (profiles/ubench/stamps.sh): per-wave cycle stamps.
-__device__ uint64_t g_dbg_stamps[64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2];
+__device__ uint64_t g_dbg_stamps[64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8];
+#define LEAF_STAMP(k)                                                                   \
+  do {                                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x < 64)                                            \
+      g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + blockIdx.x * 8 + (k)] = dbg_stamp();        \
+  } while (0)
 __device__ __forceinline__ uint64_t dbg_stamp() {
   uint64_t t;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -456,7 +493,7 @@ __device__ __forceinline__ int rollout_step(const StepCtx<LDS>& k, int t, float 
   }
   // _maximise_speed (:296-297)
   if (a.speed_on) l.sp = l.sp + dv1<F>(a.vmax - v, v + 0.0001f, bad);
-  return costmap_index<F>(a.cm_size, a.hw, rcm, l.s.x, l.s.y, bad);
+  return costmap_index<F>(a.cm_size, a.hw, rcm, l.s.x, l.s.y, bad, a.rinv_res_c, a.cdiv_res_c);
 }
 
 __device__ __forceinline__ void add_obstacle(const RolloutArgs& a, Lane& l, float cm) {
@@ -485,7 +522,8 @@ __global__ __launch_bounds__(BLOCK) void mppi_rollout_kernel(const RolloutArgs a
   }
   StepCtx<LDS> k;
   k.a = &a;
-  k.dem.init(a.Z, win, a.rows, a.grid, a.wx0, a.wy0, a.W, a.Wr, a.x_min, a.y_min, a.res);
+  k.dem.init(a.Z, win, a.rows, a.grid, a.wx0, a.wy0, a.W, a.Wr, a.x_min, a.y_min, a.res, a.rinv_res,
+             a.cdiv_res);
   {
     bool unused = false;
     k.rres_c = rc<true>(a.res_c, unused);
@@ -704,6 +742,9 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
   float* wbuf = reinterpret_cast<float*>(scratch);                           // [TB]
   float* wave_m = wbuf + TB;                                                 // [NWL]
   double* red = reinterpret_cast<double*>(scratch + ((TB + NWL) * 4 + 15) / 16 * 16);  // [NL][E]
+#ifdef MPPI_STAMPS
+  LEAF_STAMP(0);
+#endif
   if (wave < NWL) {
     const float wm = wave_min(cost_lds[tid]);
     if (lane == 0) wave_m[wave] = wm;
@@ -717,22 +758,52 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
     wbuf[j] = (c < INFINITY) ? dm_expf(-((c - m) / a.T)) : 0.0f;
   }
   __syncthreads();
-  // rows (leaf, j), j in [1, E): lane l of the wave sums trajectories l, 64+l, 128+l, 192+l
-  for (int r = wave; r < NL * (E - 1); r += NWAVES) {
-    const int leaf = r / (E - 1), j = 1 + r - leaf * (E - 1);
-    const float* wl4 = wbuf + 256 * leaf + lane;
-    const double w0 = (double)wl4[0], w1 = (double)wl4[64], w2 = (double)wl4[128], w3 = (double)wl4[192];
-    double x0 = w0, x1 = w1, x2 = w2, x3 = w3;  // j == 1: S = sum w
-    if (j >= 2) {
-      const float* u = ub_block + (size_t)(j - 2) * TB + 256 * leaf + lane;
-      x0 = w0 * (double)u[0];
-      x1 = w1 * (double)u[64];
-      x2 = w2 * (double)u[128];
-      x3 = w3 * (double)u[192];
+#ifdef MPPI_STAMPS
+  LEAF_STAMP(1);
+#endif
+  // rows (leaf, j), j in [1, E): lane l of the wave sums trajectories l, 64+l, 128+l, 192+l.
+  // LEAF_UNROLL rows per wave are loaded before any is reduced, so the sampled-control
+  // loads overlap instead of serialising row by row.  (The re-read of the sampled
+  // controls runs at ~4.5 TB/s aggregate: this phase is HBM-bound, profiles/r01_notes.md.)
+  constexpr int LEAF_UNROLL = 5;
+  const int NR = NL * (E - 1);
+  for (int r0 = wave; r0 < NR; r0 += NWAVES * LEAF_UNROLL) {
+    float uv[LEAF_UNROLL][4];
+#pragma unroll
+    for (int q = 0; q < LEAF_UNROLL; ++q) {
+      const int r = r0 + q * NWAVES;
+      const int leaf = r / (E - 1), j = 1 + r - leaf * (E - 1);
+      uv[q][0] = uv[q][1] = uv[q][2] = uv[q][3] = 1.0f;  // j == 1: S = sum w
+      if (r < NR && j >= 2) {
+        const float* u = ub_block + (size_t)(j - 2) * TB + 256 * leaf + lane;
+        uv[q][0] = u[0];
+        uv[q][1] = u[64];
+        uv[q][2] = u[128];
+        uv[q][3] = u[192];
+      }
     }
-    const double sum = wave_sum((x0 + x1) + (x2 + x3));
-    if (lane == 0) red[leaf * E + j] = sum;
+#pragma unroll
+    for (int q = 0; q < LEAF_UNROLL; ++q) {
+      const int r = r0 + q * NWAVES;
+      if (r < NR) {
+        const int leaf = r / (E - 1), j = 1 + r - leaf * (E - 1);
+        const float* wl4 = wbuf + 256 * leaf + lane;
+        const double w0 = (double)wl4[0], w1 = (double)wl4[64], w2 = (double)wl4[128], w3 = (double)wl4[192];
+        double x0 = w0, x1 = w1, x2 = w2, x3 = w3;
+        if (j >= 2) {
+          x0 = w0 * (double)uv[q][0];
+          x1 = w1 * (double)uv[q][1];
+          x2 = w2 * (double)uv[q][2];
+          x3 = w3 * (double)uv[q][3];
+        }
+        const double sum = wave_sum((x0 + x1) + (x2 + x3));
+        if (lane == 0) red[leaf * E + j] = sum;
+      }
+    }
   }
+#ifdef MPPI_STAMPS
+  LEAF_STAMP(4);
+#endif
   __syncthreads();
   for (int j = tid; j < E; j += NT) {
     double val[NL];
@@ -789,7 +860,7 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_ws_kernel(const RolloutAr
   const uint64_t kg = (uint64_t)(a.k_offset + kl);
   const int H = a.H;
   Dem<false> dem;
-  dem.init(a.Z, nullptr, a.rows, a.grid, 0, 0, 1, 1, a.x_min, a.y_min, a.res);
+  dem.init(a.Z, nullptr, a.rows, a.grid, 0, 0, 1, 1, a.x_min, a.y_min, a.res, a.rinv_res, a.cdiv_res);
   const float res_half_neg = (-a.res) / 2.0f;
   const float res_sq = a.res * a.res;
   bool nobad = false;
@@ -842,7 +913,7 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_ws_kernel(const RolloutAr
     }
     Recip rcm;
     rcm.b = a.res_c;
-    const float cm_now = a.cm[costmap_index<false>(a.cm_size, a.hw, rcm, x, y, nobad)];
+    const float cm_now = a.cm[costmap_index<false>(a.cm_size, a.hw, rcm, x, y, nobad, a.rinv_res_c, a.cdiv_res_c)];
     const float pft = pf_sum + 10.0f * (fabsf(x - a.gx) + fabsf(y - a.gy));
     pf_sum = (sc < H - 1) ? pft : pf_sum;   // _path_follow_critic sum over t < H-1
     last_x = x;
@@ -1033,6 +1104,279 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_ws_kernel(const RolloutAr
     g[1] = k_t2 - k_t1;   // leaf records
     g[2] = k_r2 - k_r0;   // wall (100 MHz ticks)
     g[3] = k_t2 - k_t0;   // total shader cycles
+  }
+  if (tid == 0 && blockIdx.x < 1024) {
+    uint64_t* g = g_dbg_stamps + 64 * 16 * 6 + blockIdx.x * 2;
+    g[0] = k_r0;
+    g[1] = k_r2;
+  }
+#endif
+}
+
+// =====================================================================  pair-synchronised rollout kernel
+// Same roles as mppi_rollout_ws_kernel (chain wave c and side wave c serve the
+// trajectories 64c..64c+63), but each chain/side PAIR synchronises only with
+// itself, through three LDS progress counters, instead of all eight waves
+// meeting at a workgroup barrier every step.  Deeper rings (PAIR_D steps) let
+// a pair absorb step-to-step jitter (DEM gather latency) instead of paying the
+// slowest of eight waves every step:
+//   chain step s : needs produced > s and consumed > s - D        -> chained = s + 1
+//   side  iter p : produce p   (needs chained > p - D)           -> produced = p + 1
+//                  consume p-L (needs chained > p - L)           -> consumed = p - L + 1
+// with L = PAIR_LAG; deadlock-free for 0 < L < D (the chain's waits are always
+// satisfied by side iterations that do not wait on it).  Bitwise identical results.
+constexpr int PAIR_D = 8;
+constexpr int PAIR_LAG = 4;
+static_assert(PAIR_LAG > 0 && PAIR_LAG < PAIR_D, "ring depth must exceed the consume lag");
+
+__device__ __forceinline__ int lds_load_acquire(const int* f) {
+  return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store_release(int* f, int v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int TB, int PROJ, int MODE, bool DUMP>
+__global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const RolloutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  constexpr int NT = 2 * TB;
+  constexpr int NWC = TB / 64;
+  constexpr int D = PAIR_D;
+  float* ring_in = reinterpret_cast<float*>(smem_raw);   // [D][2][TB]: v, w
+  float* ring_out = ring_in + D * 2 * TB;                // [D][4][TB]: x, y, cx, cy
+  float* cost_lds = ring_out + D * 4 * TB;               // [TB]
+  int* flags = reinterpret_cast<int*>(cost_lds + TB);    // [4][NWC]: produced, chained, consumed, -
+  unsigned char* scratch = reinterpret_cast<unsigned char*>(flags + 4 * NWC);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool side = wave >= NWC;
+  const int tj = side ? tid - TB : tid;  // trajectory within the workgroup
+  const int pair = side ? wave - NWC : wave;
+  int* f_prod = flags + pair;
+  int* f_chain = flags + NWC + pair;
+  int* f_cons = flags + 2 * NWC + pair;
+#ifdef MPPI_STAMPS
+  const uint64_t k_t0 = dbg_stamp(), k_r0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t st_wait = 0;
+#endif
+  const int64_t kl = (int64_t)blockIdx.x * TB + tj;
+  const bool valid = kl < a.K;
+  const uint64_t kg = (uint64_t)(a.k_offset + kl);
+  const int H = a.H;
+  Dem<false> dem;
+  dem.init(a.Z, nullptr, a.rows, a.grid, 0, 0, 1, 1, a.x_min, a.y_min, a.res, a.rinv_res, a.cdiv_res);
+  const float res_half_neg = (-a.res) / 2.0f;
+  const float res_sq = a.res * a.res;
+  bool nobad = false;
+  if (tid < 4 * NWC) flags[tid] = 0;
+
+  // ---------------- per-role state
+  Traj s;                       // chain
+  float L = a.wl, R = a.wr;     // side: filter
+  float e1b = 0.f, e2b = 0.f;   // side: noise of the odd step of the current Philox block
+  float pf_sum = 0.f, sw = 0.f, sp = 0.f, ob = 0.f, last_x = a.x0, last_y = a.y0;
+  float lwx = 0.f, lwy = 0.f, lwz = 0.f, rwx = 0.f, rwy = 0.f, rwz = 0.f;
+  float cm_pend = 0.f;
+  float* ust = a.ustore + (size_t)blockIdx.x * (2 * H) * TB + tj;
+
+  if (!side) {  // initial projection at the robot pose (projection_warp.py:306-310)
+    s.x = a.x0;
+    s.y = a.y0;
+    float q[4];
+    dem.template corners<false>(s.x, s.y, q, nobad);
+    const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
+    const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
+    const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
+    const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
+    if constexpr (PROJ == 3) {
+      const float d = (a.h0x * nx + a.h0y * ny) + a.h0z * nz;
+      const float tx = a.h0x - d * nx, ty = a.h0y - d * ny, tz = a.h0z - d * nz;
+      const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
+      s.hx = tx / tn;
+      s.hy = ty / tn;
+      s.hz = tz / tn;
+    } else {
+      s.hx = a.h0x;
+      s.hy = a.h0y;
+      s.hz = a.h0z;
+    }
+  }
+  __syncthreads();  // flags initialised
+
+  auto wait_ge = [&](const int* f, int target) __attribute__((always_inline)) {
+#ifdef MPPI_STAMPS
+    const uint64_t t0 = dbg_stamp();
+#endif
+    while (lds_load_acquire(f) < target) __builtin_amdgcn_s_sleep(1);
+#ifdef MPPI_STAMPS
+    st_wait += dbg_stamp() - t0;
+#endif
+  };
+
+  if (!side) {
+    // ---------------- chain wave: the serial projection, one step per iteration
+    for (int sc = 0; sc < H; ++sc) {
+      wait_ge(f_prod, sc + 1);
+      wait_ge(f_cons, sc - D + 1);
+      const float* ri = ring_in + (sc % D) * 2 * TB + tj;
+      const float v = ri[0], wv = ri[TB];
+      float sn, cs;
+      dm_sincosf(wv * a.dt, &sn, &cs);
+      float cx = 0.f, cy = 0.f, z = 0.f;
+      float q[4];
+      if constexpr (PROJ == 3) {
+        float nx, ny, nz;
+        bool bad = false;
+        const Traj saved = s;
+        chain3d<kChainFast, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+        if (kChainFast && __builtin_expect(bad, 0)) {  // operand outside the fast range: IEEE redo
+          s = saved;
+          chain3d<false, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+        }
+        cx = a.off * (ny * s.hz - nz * s.hy);
+        cy = a.off * (nz * s.hx - nx * s.hz);
+        if constexpr (DUMP) z = bilinear<false>(s.x, s.y, q, dem.template rr<false>(), nobad);
+      } else {
+        StepOut o;
+        step2d<false, false>(dem, a.dt, v, sn, cs, s, o, nobad);
+        z = o.z;
+      }
+      float* ro = ring_out + (sc % D) * 4 * TB + tj;
+      ro[0] = s.x;
+      ro[TB] = s.y;
+      ro[2 * TB] = cx;
+      ro[3 * TB] = cy;
+      if constexpr (DUMP) {
+        if (valid) {
+          const size_t o3 = ((size_t)kl * H + sc) * 3;
+          if (a.d_traj) { a.d_traj[o3] = s.x; a.d_traj[o3 + 1] = s.y; a.d_traj[o3 + 2] = z; }
+          if (a.d_hv) { a.d_hv[o3] = s.hx; a.d_hv[o3 + 1] = s.hy; a.d_hv[o3 + 2] = s.hz; }
+        }
+      }
+      lds_store_release(f_chain, sc + 1);
+    }
+  } else {
+    // ---------------- side wave: produce step p, consume step p - PAIR_LAG
+    for (int p = 0; p < H + PAIR_LAG; ++p) {
+      if (p < H) {  // noise, sampling, filter (sampling_warp.py:54-138)
+        wait_ge(f_chain, p - D + 1);
+        float u1, u2;
+        if constexpr (MODE == 0) {
+          float e1, e2;
+          if ((p & 1) == 0) {
+            noise_block(a.seed, a.n_base + (uint64_t)(p >> 1), kg, &e1, &e2, &e1b, &e2b);
+          } else {
+            e1 = e1b;
+            e2 = e2b;
+          }
+          const int ti = min(p + 1, H - 1);
+          u1 = clampf(a.u_nom1[ti] + a.s1 * e1, a.min_u1, a.max_u1);
+          u2 = clampf(a.u_nom2[ti] + a.s2 * e2, a.min_u2, a.max_u2);
+        } else {
+          const size_t o = (size_t)(valid ? kl : 0) * H + p;
+          u1 = a.inj_u1[o];
+          u2 = a.inj_u2[o];
+        }
+        ust[(size_t)p * TB] = u1;
+        ust[(size_t)(H + p) * TB] = u2;
+        L = L * a.fa + (u1 * a.fk) * (1.0f - a.fa);
+        R = R * a.fa + (u2 * a.fk) * (1.0f - a.fa);
+        const float vp = clampf((L + R) / 2.0f, a.vmin, a.vmax);
+        const float wp = clampf(((-L) + R) / a.rwheel, a.wmin, a.wmax);
+        float* ri = ring_in + (p % D) * 2 * TB + tj;
+        ri[0] = vp;
+        ri[TB] = wp;
+        if constexpr (DUMP) {
+          if (valid) {
+            const size_t o1 = (size_t)kl * H + p;
+            if (a.d_u1) a.d_u1[o1] = u1;
+            if (a.d_u2) a.d_u2[o1] = u2;
+          }
+        }
+        lds_store_release(f_prod, p + 1);
+      }
+      const int sc = p - PAIR_LAG;
+      if (sc >= 0) {  // wheel contacts + critics of step sc (projection_warp.py:333-348, critics_warp.py)
+        wait_ge(f_chain, sc + 1);
+        const float* ro = ring_out + (sc % D) * 4 * TB + tj;
+        const float x = ro[0], y = ro[TB], cx = ro[2 * TB], cy = ro[3 * TB];
+        const float vq = ring_in[(sc % D) * 2 * TB + tj];  // v of step sc (slot not reused yet)
+        float lx = 0.f, ly = 0.f, lz = 0.f, rx = 0.f, ry = 0.f, rz = 0.f;
+        if constexpr (PROJ == 3) {
+          lx = x + cx;
+          ly = y + cy;
+          lz = dem.template point<false>(lx, ly, nobad);
+          rx = x - cx;
+          ry = y - cy;
+          rz = dem.template point<false>(rx, ry, nobad);
+        }
+        Recip rcm;
+        rcm.b = a.res_c;
+        const float cm_now =
+            a.cm[costmap_index<false>(a.cm_size, a.hw, rcm, x, y, nobad, a.rinv_res_c, a.cdiv_res_c)];
+        const float pft = pf_sum + 10.0f * (fabsf(x - a.gx) + fabsf(y - a.gy));
+        pf_sum = (sc < H - 1) ? pft : pf_sum;   // _path_follow_critic sum over t < H-1
+        last_x = x;
+        last_y = y;
+        if ((sc & 1) == 0) {  // _avoid_slope_wheels terms (i, i+2), even i < H-3
+          const float term = slope_term<false>(lwx, lwy, lwz, lx, ly, lz, rwx, rwy, rwz, rx, ry, rz, nobad);
+          sw = (sc >= 2 && sc - 2 < H - 3) ? sw + term : sw;
+          lwx = lx; lwy = ly; lwz = lz;
+          rwx = rx; rwy = ry; rwz = rz;
+        }
+        const float spt = sp + (a.vmax - vq) / (vq + 0.0001f);  // _maximise_speed
+        sp = a.speed_on ? spt : sp;
+        // _avoid_obstacle: the costmap value gathered in the previous consume
+        const float ob1 = (cm_pend > a.thr) ? ob + a.pen : ob;
+        ob = (sc > 0) ? ob1 + cm_pend : ob;
+        cm_pend = cm_now;
+        if constexpr (DUMP) {
+          if (valid) {
+            const size_t o3 = ((size_t)kl * H + sc) * 3;
+            if (a.d_lw) { a.d_lw[o3] = lx; a.d_lw[o3 + 1] = ly; a.d_lw[o3 + 2] = lz; }
+            if (a.d_rw) { a.d_rw[o3] = rx; a.d_rw[o3 + 1] = ry; a.d_rw[o3 + 2] = rz; }
+            const size_t o1 = (size_t)kl * H + sc;
+            if (a.d_v) a.d_v[o1] = vq;
+            if (a.d_w) a.d_w[o1] = ring_in[(sc % D) * 2 * TB + TB + tj];
+          }
+        }
+        lds_store_release(f_cons, sc + 1);
+      }
+    }
+    if (cm_pend > a.thr) ob = ob + a.pen;  // last step's obstacle term
+    ob = ob + cm_pend;
+    // _evaluate_trajectories_kernel (critics_warp.py:325-329)
+    float pf;
+    if (a.pf_far) {
+      const float dx = last_x - a.igx, dy = last_y - a.igy;
+      pf = (dx * dx + dy * dy) * a.pf_scale;
+    } else {
+      pf = pf_sum;
+    }
+    float cost = a.w_path * pf;
+    cost = cost + a.w_slope * sw;
+    cost = cost + a.w_speed * sp;
+    cost = cost + a.w_obs * ob;
+    if (valid) a.cost_out[kl] = cost;
+    cost_lds[tj] = valid ? cost : INFINITY;
+  }
+#ifdef MPPI_STAMPS
+  const uint64_t k_t1 = dbg_stamp();
+  if ((tid & 63) == 0 && blockIdx.x < 64) {
+    g_dbg_stamps[(blockIdx.x * (NT / 64) + wave) * 2] = (k_t1 - k_t0) - st_wait;
+    g_dbg_stamps[(blockIdx.x * (NT / 64) + wave) * 2 + 1] = st_wait;
+  }
+#endif
+  __syncthreads();
+  leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
+#ifdef MPPI_STAMPS
+  const uint64_t k_t2 = dbg_stamp(), k_r2 = __builtin_amdgcn_s_memrealtime();
+  if ((tid & 63) == 0 && blockIdx.x < 64) {
+    uint64_t* g = g_dbg_stamps + 64 * 16 * 2 + (blockIdx.x * (NT / 64) + wave) * 4;
+    g[0] = k_t1 - k_t0;
+    g[1] = k_t2 - k_t1;
+    g[2] = k_r2 - k_r0;
+    g[3] = k_t2 - k_t0;
   }
   if (tid == 0 && blockIdx.x < 1024) {
     uint64_t* g = g_dbg_stamps + 64 * 16 * 6 + blockIdx.x * 2;
@@ -1301,7 +1645,7 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
   }
   __syncthreads();
   Dem<LDS> dem;
-  dem.init(f.Z, win, f.rows, f.grid, f.wx0, f.wy0, f.W, f.Wr, f.x_min, f.y_min, f.res);
+  dem.init(f.Z, win, f.rows, f.grid, f.wx0, f.wy0, f.W, f.Wr, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
   // mode 1: the whole optimal rollout; mode 2: its first step only (the pose the
   // closed loop needs now), the rest runs in mppi_tail_kernel on a side stream
   optimal_rollout<LDS>(f, dem, vb, snb, csb, chain, f.mode == 2 ? 1 : H, f.out + 4 * H, tid, FIN_THREADS);
@@ -1322,7 +1666,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void mppi_tail_kernel(const FinishArg
   for (int i = tid; i < 3 * H; i += TAIL_THREADS) vb[i] = f.tail_in[i];
   __syncthreads();
   Dem<false> dem;
-  dem.init(f.Z, nullptr, f.rows, f.grid, 0, 0, 1, 1, f.x_min, f.y_min, f.res);
+  dem.init(f.Z, nullptr, f.rows, f.grid, 0, 0, 1, 1, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
   optimal_rollout<false>(f, dem, vb, snb, csb, chain, H, f.tail_out, tid, TAIL_THREADS);
 }
 
@@ -1443,6 +1787,29 @@ static hipError_t launch_ws_m(const RolloutArgs& a, int blocks, size_t lds, hipS
   return hipGetLastError();
 }
 
+template <int TB, int PROJ>
+static hipError_t launch_pair_m(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int mode,
+                                bool dump) {
+  if (mode == 0) {
+    if (dump)
+      hipLaunchKernelGGL((mppi_rollout_pair_kernel<TB, PROJ, 0, true>), dim3(blocks), dim3(2 * TB), lds, st, a);
+    else
+      hipLaunchKernelGGL((mppi_rollout_pair_kernel<TB, PROJ, 0, false>), dim3(blocks), dim3(2 * TB), lds, st, a);
+  } else {
+    if (dump)
+      hipLaunchKernelGGL((mppi_rollout_pair_kernel<TB, PROJ, 1, true>), dim3(blocks), dim3(2 * TB), lds, st, a);
+    else
+      hipLaunchKernelGGL((mppi_rollout_pair_kernel<TB, PROJ, 1, false>), dim3(blocks), dim3(2 * TB), lds, st, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
+                               int mode, bool dump) {
+  if (proj == 3) return launch_pair_m<256, 3>(a, blocks, lds, st, mode, dump);
+  return launch_pair_m<256, 2>(a, blocks, lds, st, mode, dump);
+}
+
 hipError_t launch_rollout_ws(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
                              int mode, bool dump) {
   if (proj == 3) return launch_ws_m<256, 3>(a, blocks, lds, st, mode, dump);
@@ -1460,6 +1827,19 @@ hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool u
 hipError_t launch_tail(const FinishArgs& f, hipStream_t st) {
   const size_t lds = (size_t)15 * f.H * sizeof(float);
   hipLaunchKernelGGL(mppi_tail_kernel, dim3(1), dim3(TAIL_THREADS), lds, st, f);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void mppi_cdiv_verify_kernel(float b, float y, unsigned* bad) {
+  const unsigned i = blockIdx.x * 256u + threadIdx.x;  // significand bits, 2^23 threads
+  const float a = __builtin_bit_cast(float, 0x3f800000u | i);
+  const float q = cdiv_f(a, b, y);
+  const float ref = a / b;
+  if (__builtin_bit_cast(unsigned, q) != __builtin_bit_cast(unsigned, ref)) atomicAdd(bad, 1u);
+}
+
+hipError_t launch_cdiv_verify(float b, float y, unsigned* bad, hipStream_t st) {
+  hipLaunchKernelGGL(mppi_cdiv_verify_kernel, dim3(1u << 15), dim3(256), 0, st, b, y, bad);
   return hipGetLastError();
 }
 

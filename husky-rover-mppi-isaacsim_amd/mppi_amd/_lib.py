@@ -254,7 +254,7 @@ class Engine:
         return u1, u2
 
     def set_dem_path(self, mode):
-        self._c(self.lib.mppi_set_dem_path(self.ctx, {"auto": 0, "lds": 1, "global": 2, "ws": 3}.get(mode, mode)),
+        self._c(self.lib.mppi_set_dem_path(self.ctx, {"auto": 0, "lds": 1, "global": 2, "ws": 3, "pair": 4}.get(mode, mode)),
                 "mppi_set_dem_path")
 
     # ------------------------------------------------------------ steps

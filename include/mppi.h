@@ -178,11 +178,12 @@ int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_
 /* HIP-event time of the deferred optimal-rollout kernels (side stream). */
 int mppi_get_tail_timing(mppi_ctx* ctx, double* tail_ms, int64_t* launches);
 
-/* Rollout kernel variant: 0 = default (= 3); 1 = one wave per trajectory group
+/* Rollout kernel variant: 0 = default (= 4); 1 = one wave per trajectory group
  * with the DEM window staged in LDS (error if it does not fit); 2 = one wave per
  * trajectory group, DEM read through L1/L2; 3 = warp-specialised (a chain wave
- * and a side wave per 64 trajectories, DEM through L1/L2).  All variants give
- * bitwise identical results. */
+ * and a side wave per 64 trajectories, DEM through L1/L2, one workgroup barrier
+ * per step); 4 = warp-specialised, each chain/side pair synchronised through LDS
+ * progress counters.  All variants give bitwise identical results. */
 int mppi_set_dem_path(mppi_ctx* ctx, int32_t mode);
 
 /* Layout/launch facts for the last step (for tests and the bench):

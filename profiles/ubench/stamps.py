@@ -27,6 +27,7 @@ def build():
 
 def main():
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    path = sys.argv[2] if len(sys.argv) > 2 else "pair"
     if not os.path.exists(SO):
         build()
     from mppi_amd import _lib, scene
@@ -36,13 +37,13 @@ def main():
     Z, hw, cm = scene.scene_c3()
     H = 100
     eng = _lib.Engine(_lib.make_params(K, H), 0)
-    eng.set_dem_path("ws")
+    eng.set_dem_path(path)
     eng.set_dem(Z, hw)
     eng.set_costmap(cm, hw)
     eng.set_state(_lib.make_state(-60.0, -5.0, goal_x=65.0, goal_y=10.0))
     for i in range(5):
         eng.step("3d", i)
-    n = 64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2
+    n = 64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8
     buf = (C.c_uint64 * n)()
     assert lib.mppi_debug_stamps(buf, n) == 0
     allv = np.array(buf, dtype=np.float64)
@@ -53,8 +54,9 @@ def main():
     print(f"  block start (us): min {st.min():.1f} median {np.median(st):.1f} max {st.max():.1f}; "
           f"end: min {en.min():.1f} median {np.median(en):.1f} max {en.max():.1f}")
     print("  start histogram (10 us bins):", np.histogram(st, bins=np.arange(0, st.max() + 10, 10))[0].tolist())
-    a = allv[:64 * 16 * 2].reshape(64, 16, 2)
-    b = allv[64 * 16 * 2: 64 * 16 * 6].reshape(64, 16, 4)[: min(64, (K + 255) // 256), :8]
+    # per-wave slots: (block * 8 + wave) * 2 and 2048 + (block * 8 + wave) * 4 (8 waves per block)
+    a = allv[:64 * 8 * 2].reshape(64, 8, 2)
+    b = allv[64 * 16 * 2: 64 * 16 * 2 + 64 * 8 * 4].reshape(64, 8, 4)[: min(64, (K + 255) // 256)]
     print(f"  loop+cost {b[..., 0].mean():10.0f} cyc   leaf records {b[..., 1].mean():8.0f} cyc   "
           f"total {b[..., 3].mean():10.0f} cyc = {b[..., 2].mean() / 100:8.1f} us wall "
           f"-> clock {b[..., 3].mean() / (b[..., 2].mean() * 10):.2f} GHz")
@@ -63,7 +65,9 @@ def main():
     phases = H + 2
     chain = a[:, :4].reshape(-1, 2) / phases
     side = a[:, 4:].reshape(-1, 2) / phases
-    print(f"K={K}: cycles per phase (mean over {nb} blocks)")
+    lf = allv[64 * 16 * 6 + 1024 * 2:].reshape(64, 8)[:nb]
+    print(f"  leaf records: min+exp {(lf[:, 1] - lf[:, 0]).mean():.0f}  rows {(lf[:, 4] - lf[:, 1]).mean():.0f} cyc")
+    print(f"K={K} kernel={path}: cycles per step (mean over {nb} blocks)")
     print(f"  chain waves: work {chain[:, 0].mean():8.1f}  wait {chain[:, 1].mean():8.1f}")
     print(f"  side  waves: work {side[:, 0].mean():8.1f}  wait {side[:, 1].mean():8.1f}")
 

@@ -80,7 +80,7 @@ def test_global_dem_path_matches_lds_path():
     _assert_step(ref, out_g, eng_g)
 
 
-@pytest.mark.parametrize("path", ["ws", "global", "lds"])
+@pytest.mark.parametrize("path", ["pair", "ws", "global", "lds"])
 @pytest.mark.parametrize("K,H,proj", [(256, 20, "3d"), (1000, 33, "3d"), (4096, 50, "3d"), (700, 24, "2d")])
 def test_kernel_variants_parity(path, K, H, proj):
     st = hp.oracle_state(wl=0.2, wr=0.1)
