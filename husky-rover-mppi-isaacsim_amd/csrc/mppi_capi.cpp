@@ -91,6 +91,16 @@ struct mppi_ctx {
   float* out_host = nullptr;  // [16H] last complete outputs (host memory)
   float* inj1 = nullptr;
   float* inj2 = nullptr;
+  // precomputed sampling normals (pair kernel, MODE 0): two slots, each tagged with the
+  // Philox step it holds; the next step's normals are generated speculatively on
+  // noise_stream while the GPU is otherwise idle (finish kernel, host gap)
+  float* eps[2] = {nullptr, nullptr};
+  size_t eps_cap = 0;
+  int64_t eps_step[2] = {-1, -1};
+  hipEvent_t eps_ev[2] = {nullptr, nullptr};
+  bool eps_pending[2] = {false, false};
+  hipStream_t noise_stream = nullptr;
+  hipEvent_t ev_roll_done = nullptr;
   int dem_path = 0;
   // last step (for dump)
   bool have_last = false;
@@ -204,8 +214,9 @@ Plan make_plan(const mppi_ctx* c) {
   pl.traj_per_block = pl.block;
   pl.blocks = (int)((K + pl.block - 1) / pl.block);
   const int NW = pl.block / 64;
-  // reduction scratch (mppi_rollout_kernel): w[block] + wave minima, then [leaves][2H+2] doubles
-  const size_t scratch = ((size_t)(pl.block + NW) * sizeof(float) + 15) / 16 * 16 +
+  // reduction scratch (mppi_rollout_kernel): costs[block], w[block] + wave minima, [leaves][2H+2] doubles
+  const size_t scratch = (size_t)pl.block * sizeof(float) +
+                         ((size_t)(pl.block + NW) * sizeof(float) + 15) / 16 * 16 +
                          (size_t)(NW / 4) * (2 * H + 2) * sizeof(double);
   pl.lds_bytes = std::max(pl.lds ? win : (size_t)0, scratch);
   if (c->dem_path == 3 || c->dem_path == 0 || c->dem_path == 4) {
@@ -425,6 +436,65 @@ int wait_done(mppi_ctx* c) {
   }
 }
 
+// Normals of Philox step `step` in an eps slot, generated on the context stream if no
+// slot holds them (first step, or a step counter that did not advance by one).
+int eps_for_step(mppi_ctx* c, const Plan& pl, uint64_t step, int* slot_out) {
+  const size_t need = (size_t)pl.blocks * 2 * H_of(c) * 256;
+  if (need > c->eps_cap) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(c->noise_stream));
+    for (int i = 0; i < 2; ++i) {
+      if (c->eps[i]) HIP_TRY(hipFree(c->eps[i]));
+      c->eps[i] = nullptr;
+      c->eps_step[i] = -1;
+      c->eps_pending[i] = false;
+    }
+    HIP_TRY(hipMalloc(&c->eps[0], need * sizeof(float)));
+    HIP_TRY(hipMalloc(&c->eps[1], need * sizeof(float)));
+    c->eps_cap = need;
+  }
+  const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
+  for (int i = 0; i < 2; ++i) {
+    if (c->eps_step[i] == (int64_t)step) {
+      if (c->eps_pending[i]) {  // generated on noise_stream: order it before this rollout
+        const hipError_t q = hipEventQuery(c->eps_ev[i]);
+        if (q == hipErrorNotReady) HIP_TRY(hipStreamWaitEvent(c->stream, c->eps_ev[i], 0));
+        else if (q != hipSuccess) return fail(MPPI_EHIP, std::string("noise: ") + hipGetErrorString(q));
+        c->eps_pending[i] = false;
+      }
+      *slot_out = i;
+      return MPPI_OK;
+    }
+  }
+  // not precomputed: any in-flight speculative fill must finish before a slot is reused
+  for (int i = 0; i < 2; ++i)
+    if (c->eps_pending[i]) {
+      HIP_TRY(hipStreamWaitEvent(c->stream, c->eps_ev[i], 0));
+      c->eps_pending[i] = false;
+    }
+  const int slot = 0;
+  HIP_TRY(launch_noise(c->p.seed, step * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[slot], c->stream));
+  c->eps_step[slot] = (int64_t)step;
+  c->eps_step[slot ^ 1] = -1;
+  *slot_out = slot;
+  return MPPI_OK;
+}
+
+// After the rollout of `step` (which reads slot `used`) is enqueued: generate the
+// normals of step + 1 into the other slot on noise_stream once that rollout is done.
+int speculate_eps(mppi_ctx* c, const Plan& pl, uint64_t step, int used) {
+  const int other = used ^ 1;
+  const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
+  HIP_TRY(hipEventRecord(c->ev_roll_done, c->stream));
+  HIP_TRY(hipStreamWaitEvent(c->noise_stream, c->ev_roll_done, 0));
+  HIP_TRY(launch_noise(c->p.seed, (step + 1) * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[other],
+                       c->noise_stream));
+  HIP_TRY(hipEventRecord(c->eps_ev[other], c->noise_stream));
+  c->eps_step[other] = (int64_t)(step + 1);
+  c->eps_pending[other] = true;
+  return MPPI_OK;
+}
+
 // Enqueue the rollout kernel for the current state / nominal sequence.
 int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl,
                     const float* unom, const mppi_state& st, const RolloutArgs* dump_args) {
@@ -440,6 +510,12 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   }
   RolloutArgs a;
   fill_rollout(c, pl, st, step, unom, a);
+  int eps_slot = -1;
+  if (pl.pair && mode == 0 && pl.blocks > 0) {
+    rc = eps_for_step(c, pl, step, &eps_slot);
+    if (rc) return rc;
+    a.eps = c->eps[eps_slot];
+  }
   if (dump_args) {
     a.d_traj = dump_args->d_traj;
     a.d_hv = dump_args->d_hv;
@@ -463,6 +539,7 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     c->ev_roll_pending = true;
   }
+  if (eps_slot >= 0 && !dump_args) return speculate_eps(c, pl, step, eps_slot);
   return MPPI_OK;
 }
 
@@ -648,7 +725,11 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   if (hipEventCreateWithFlags(&c->ev_fin_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_tail[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_tail[1], hipEventDisableTiming) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->tail_stream, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithFlags(&c->tail_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->noise_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_roll_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->eps_ev[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->eps_ev[1], hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "side stream / event creation failed"));
   c->out_host = new float[16 * H]();
   std::memset(c->stage, 0, 16 * H * sizeof(float));
@@ -663,6 +744,7 @@ void mppi_destroy(mppi_ctx* c) {
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->tail_stream) hipStreamSynchronize(c->tail_stream);
+  if (c->noise_stream) hipStreamSynchronize(c->noise_stream);
   if (c->Z_owned && c->Z) hipFree(c->Z);
   if (c->cm) hipFree(c->cm);
   for (float* u : c->u_nom)
@@ -683,6 +765,12 @@ void mppi_destroy(mppi_ctx* c) {
     if (c->ev_tail[i]) hipEventDestroy(c->ev_tail[i]);
   }
   if (c->ev_fin_done) hipEventDestroy(c->ev_fin_done);
+  for (int i = 0; i < 2; ++i) {
+    if (c->eps[i]) hipFree(c->eps[i]);
+    if (c->eps_ev[i]) hipEventDestroy(c->eps_ev[i]);
+  }
+  if (c->ev_roll_done) hipEventDestroy(c->ev_roll_done);
+  if (c->noise_stream) hipStreamDestroy(c->noise_stream);
   if (c->tail_stream) hipStreamDestroy(c->tail_stream);
   if (c->inj1) hipFree(c->inj1);
   if (c->inj2) hipFree(c->inj2);

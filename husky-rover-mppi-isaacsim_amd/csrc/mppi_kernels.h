@@ -28,6 +28,7 @@ struct RolloutArgs {
   float x0, y0, h0x, h0y, h0z, wl, wr, gx, gy, s1, s2;
   // sampling
   uint64_t seed, n_base;  // Philox key, block index of (step, t=0)
+  const float* eps;       // pair kernel, MODE 0: this step's normals [blocks][2][H][256] (mppi_noise_kernel)
   const float* u_nom1;
   const float* u_nom2;
   float min_u1, max_u1, min_u2, max_u2;
@@ -98,6 +99,10 @@ hipError_t launch_tail(const FinishArgs& f, hipStream_t st);
 hipError_t launch_selftest(int what, int64_t n, uint64_t seed, unsigned long long* bad, hipStream_t st);
 // counts the significands a in [1, 2) for which cdiv_f(a, b, y) != a / b (IEEE)
 hipError_t launch_cdiv_verify(float b, float y, unsigned* bad, hipStream_t st);
+// The sampling normals of one step (Philox block n_base + t/2 of global trajectory k_offset + k),
+// laid out [blocks][2][H][256]: eps1 rows then eps2 rows, 256 trajectories per row.
+hipError_t launch_noise(uint64_t seed, uint64_t n_base, int64_t k_offset, int blocks, int H, float* eps,
+                        hipStream_t st);
 hipError_t launch_bilinear(const float* Z, int rows, int grid, float x_min, float y_min, float res,
                            const float* xs, const float* ys, float* hs, int64_t n, hipStream_t st);
 

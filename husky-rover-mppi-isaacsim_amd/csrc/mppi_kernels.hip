@@ -398,12 +398,6 @@ __device__ __forceinline__ float wave_min(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
   return v;
 }
-// xor-butterfly order (pairs l, l^32 first) — oracle/mppi_ref.py _wave_tree
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o, 64);
-  return v;
-}
 
 // Record combine a (+) b for element j (oracle/mppi_ref.py combine).
 struct PairScale {
@@ -434,6 +428,10 @@ __device__ __forceinline__ double pair_apply(const PairScale& p, double a, doubl
   if (j == 0) return (double)p.m;
   return (double)p.ea * a + (double)p.eb * b;
 }
+
+template <int TB, int NT, bool EPS = false>
+__device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
+                                             unsigned char* scratch, const float* ub_block);
 
 // =====================================================================  rollout kernel
 // Everything one trajectory carries from step to step.
@@ -646,77 +644,12 @@ __global__ __launch_bounds__(BLOCK) void mppi_rollout_kernel(const RolloutArgs a
   cost = cost + a.w_obs * l.ob;
   if (valid) a.cost_out[kl] = cost;
 
-  // ---- softmax leaf records (DEFINED replacement of critics_warp.py:338-376)
-  // Leaf = 256 trajectories = 4 waves.  m = leaf min, w = dm_expf(-(c-m)/T),
-  // record [m, S, V1[H], V2[H]] with each sum over the leaf taken as
-  //   a_l = (x[l] + x[64+l]) + (x[128+l] + x[192+l])   (float64, l = lane)
-  //   sum = xor-butterfly over the 64 lanes of a_l.
-  __syncthreads();  // LDS window no longer needed: reuse it as reduction scratch
-  constexpr int NL = NW / 4;
-  const int E = 2 * H + 2;
-  float* wbuf = reinterpret_cast<float*>(smem_raw);            // [BLOCK]
-  float* wave_m = wbuf + BLOCK;                                  // [NW]
-  double* red = reinterpret_cast<double*>(smem_raw + ((BLOCK + NW) * 4 + 15) / 16 * 16);  // [NL][E]
-  const float cval = valid ? cost : INFINITY;
-  {
-    const float wm = wave_min(cval);
-    if (lane == 0) wave_m[wave] = wm;
-  }
+  // ---- softmax leaf records (DEFINED replacement of critics_warp.py:338-376), shared code
+  __syncthreads();  // LDS window no longer needed: reuse it for the leaf records
+  float* cost_l = reinterpret_cast<float*>(smem_raw);  // [BLOCK]
+  cost_l[tid] = valid ? cost : INFINITY;
   __syncthreads();
-  const int leaf = wave >> 2;
-  const float m_leaf = fminf(fminf(wave_m[4 * leaf], wave_m[4 * leaf + 1]),
-                             fminf(wave_m[4 * leaf + 2], wave_m[4 * leaf + 3]));
-  {
-    float wgt = 0.0f;
-    if (cval < INFINITY) {
-      bool bad = false;
-      float x = dv<true>(cval - m_leaf, k.rT, bad);
-      if (bad) x = (cval - m_leaf) / a.T;
-      wgt = dm_expf(-x);
-    }
-    wbuf[tid] = wgt;
-  }
-  __syncthreads();  // wbuf complete; ustore rows written by other waves are ordered by the barrier
-  {
-    const int wl = wave & 3;  // this wave's share of the leaf's rows
-    const float* wl4 = wbuf + 256 * leaf + lane;
-    const double w0 = (double)wl4[0], w1 = (double)wl4[64], w2 = (double)wl4[128], w3 = (double)wl4[192];
-    const float* ub = a.ustore + (size_t)blockIdx.x * (2 * H) * BLOCK + 256 * leaf + lane;
-    for (int j = 1 + wl; j < E; j += 4) {
-      double x0 = w0, x1 = w1, x2 = w2, x3 = w3;   // j == 1: S = sum w
-      if (j >= 2) {
-        const float* u = ub + (size_t)(j - 2) * BLOCK;
-        x0 = w0 * (double)u[0];
-        x1 = w1 * (double)u[64];
-        x2 = w2 * (double)u[128];
-        x3 = w3 * (double)u[192];
-      }
-      const double sum = wave_sum((x0 + x1) + (x2 + x3));
-      if (lane == 0) red[leaf * E + j] = sum;
-    }
-  }
-  if (tid < NL) red[tid * E] = 0.0;
-  __syncthreads();
-  // the block's subtree over its NL leaves (oracle/mppi_ref.py tree_reduce order)
-  for (int j = tid; j < E; j += BLOCK) {
-    double val[NL];
-    float lm[NL];
-#pragma unroll
-    for (int q = 0; q < NL; ++q) {
-      lm[q] = fminf(fminf(wave_m[4 * q], wave_m[4 * q + 1]), fminf(wave_m[4 * q + 2], wave_m[4 * q + 3]));
-      val[q] = (j == 0) ? (double)lm[q] : red[q * E + j];
-    }
-#pragma unroll
-    for (int width = NL; width > 1; width >>= 1) {
-#pragma unroll
-      for (int q = 0; q < width / 2; ++q) {
-        const PairScale ps = pair_scale(lm[2 * q], lm[2 * q + 1], a.T);
-        val[q] = pair_apply(ps, val[2 * q], val[2 * q + 1], j);
-        lm[q] = ps.m;  // fminf(m, +inf) = m covers the empty-child modes
-      }
-    }
-    a.nodes[(size_t)blockIdx.x * E + j] = val[0];
-  }
+  leaf_records<BLOCK, BLOCK>(a, cost_l, smem_raw + BLOCK * 4, a.ustore + (size_t)blockIdx.x * (2 * H) * BLOCK);
 }
 
 // =====================================================================  leaf records (shared)
@@ -724,18 +657,16 @@ __global__ __launch_bounds__(BLOCK) void mppi_rollout_kernel(const RolloutArgs a
 // TB trajectories of a workgroup, whose costs are in cost_lds[TB] and sampled
 // controls in ustore rows [2H][TB].  Leaf = 256 trajectories.
 //   m = leaf min, w = dm_expf(-(c - m)/T),
-//   record [m, S, V1[H], V2[H]], each sum over the leaf taken as
-//   a_l = (x[l] + x[64+l]) + (x[128+l] + x[192+l])  (float64, l = lane),
-//   then the xor-butterfly over the 64 lanes of a_l;
+//   record [m, S, V1[H], V2[H]], each sum over the leaf's 256 trajectories the
+//   pairwise tree in index order ((x0+x1)+(x2+x3)) + ... (float64);
 // then the workgroup's subtree over its TB/256 leaves (tree_reduce order).
 // Called by all NT threads; `scratch` is LDS of at least
 // TB*4 + TB/64*4 (rounded to 16) + TB/256*(2H+2)*8 bytes.
-template <int TB, int NT>
+template <int TB, int NT, bool EPS>
 __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
                                              unsigned char* scratch, const float* ub_block) {
   constexpr int NL = TB / 256;
   constexpr int NWL = TB / 64;   // waves' worth of trajectories
-  constexpr int NWAVES = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.H, E = 2 * H + 2;
@@ -761,45 +692,63 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
 #ifdef MPPI_STAMPS
   LEAF_STAMP(1);
 #endif
-  // rows (leaf, j), j in [1, E): lane l of the wave sums trajectories l, 64+l, 128+l, 192+l.
-  // LEAF_UNROLL rows per wave are loaded before any is reduced, so the sampled-control
-  // loads overlap instead of serialising row by row.  (The re-read of the sampled
-  // controls runs at ~4.5 TB/s aggregate: this phase is HBM-bound, profiles/r01_notes.md.)
-  constexpr int LEAF_UNROLL = 5;
+  // rows (leaf, j), j in [1, E): two threads per row, each the pairwise tree over one half
+  // (128 trajectories) of the leaf in index order, the row = (left half) + (right half).
+  // A thread streams its half-row as whole 128-byte lines (8 float4 loads back to back).
   const int NR = NL * (E - 1);
-  for (int r0 = wave; r0 < NR; r0 += NWAVES * LEAF_UNROLL) {
-    float uv[LEAF_UNROLL][4];
-#pragma unroll
-    for (int q = 0; q < LEAF_UNROLL; ++q) {
-      const int r = r0 + q * NWAVES;
-      const int leaf = r / (E - 1), j = 1 + r - leaf * (E - 1);
-      uv[q][0] = uv[q][1] = uv[q][2] = uv[q][3] = 1.0f;  // j == 1: S = sum w
-      if (r < NR && j >= 2) {
-        const float* u = ub_block + (size_t)(j - 2) * TB + 256 * leaf + lane;
-        uv[q][0] = u[0];
-        uv[q][1] = u[64];
-        uv[q][2] = u[128];
-        uv[q][3] = u[192];
-      }
+  for (int it = tid; it < 2 * NR; it += NT) {
+    const int r = it >> 1, half = it & 1;
+    const int leaf = r / (E - 1), j = 1 + r - leaf * (E - 1);
+    const float4* w4 = reinterpret_cast<const float4*>(wbuf + 256 * leaf + 128 * half);
+    const float4* u4 = reinterpret_cast<const float4*>(ub_block + (size_t)(j >= 2 ? j - 2 : 0) * TB +
+                                                       256 * leaf + 128 * half);
+    float nom = 0.f, sg = 0.f, lo = 0.f, hi = 0.f;
+    if constexpr (EPS) {  // rows hold the normals: u = clamp(u_nom[t+1] + sigma*eps) as sampled
+      const int c = (j - 2) >= H ? 1 : 0;
+      const int t = max(j - 2, 0) - c * H;
+      const int ti = min(t + 1, H - 1);
+      nom = c ? a.u_nom2[ti] : a.u_nom1[ti];
+      sg = c ? a.s2 : a.s1;
+      lo = c ? a.min_u2 : a.min_u1;
+      hi = c ? a.max_u2 : a.max_u1;
     }
+    // the half-row's pairwise tree = ((line0 + line1) + (line2 + line3)), each line (8 float4
+    // groups, 32 trajectories) a pairwise tree of its own; one line in registers at a time
+    double s01 = 0.0, s23 = 0.0;
+#pragma unroll 1
+    for (int line = 0; line < 4; ++line) {
+      float4 uq[8];
 #pragma unroll
-    for (int q = 0; q < LEAF_UNROLL; ++q) {
-      const int r = r0 + q * NWAVES;
-      if (r < NR) {
-        const int leaf = r / (E - 1), j = 1 + r - leaf * (E - 1);
-        const float* wl4 = wbuf + 256 * leaf + lane;
-        const double w0 = (double)wl4[0], w1 = (double)wl4[64], w2 = (double)wl4[128], w3 = (double)wl4[192];
-        double x0 = w0, x1 = w1, x2 = w2, x3 = w3;
-        if (j >= 2) {
-          x0 = w0 * (double)uv[q][0];
-          x1 = w1 * (double)uv[q][1];
-          x2 = w2 * (double)uv[q][2];
-          x3 = w3 * (double)uv[q][3];
+      for (int g = 0; g < 8; ++g) uq[g] = (j >= 2) ? u4[8 * line + g] : make_float4(1.f, 1.f, 1.f, 1.f);
+      double gs[8];
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const float4 w = w4[8 * line + g];
+        float4 u = uq[g];
+        if constexpr (EPS) {
+          u.x = clampf(nom + sg * u.x, lo, hi);
+          u.y = clampf(nom + sg * u.y, lo, hi);
+          u.z = clampf(nom + sg * u.z, lo, hi);
+          u.w = clampf(nom + sg * u.w, lo, hi);
         }
-        const double sum = wave_sum((x0 + x1) + (x2 + x3));
-        if (lane == 0) red[leaf * E + j] = sum;
+        double x0 = (double)w.x, x1 = (double)w.y, x2 = (double)w.z, x3 = (double)w.w;  // j == 1: S
+        if (j >= 2) {
+          x0 = x0 * (double)u.x;
+          x1 = x1 * (double)u.y;
+          x2 = x2 * (double)u.z;
+          x3 = x3 * (double)u.w;
+        }
+        gs[g] = (x0 + x1) + (x2 + x3);
       }
+      const double ls = ((gs[0] + gs[1]) + (gs[2] + gs[3])) + ((gs[4] + gs[5]) + (gs[6] + gs[7]));
+      if (line == 0) s01 = ls;
+      else if (line == 1) s01 = s01 + ls;
+      else if (line == 2) s23 = ls;
+      else s23 = s23 + ls;
     }
+    const double hsum = s01 + s23;
+    const double other = __shfl_xor(hsum, 1, 64);  // the partner half (adjacent lane)
+    if (half == 0) red[leaf * E + j] = hsum + other;
   }
 #ifdef MPPI_STAMPS
   LEAF_STAMP(4);
@@ -1161,7 +1110,6 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 #endif
   const int64_t kl = (int64_t)blockIdx.x * TB + tj;
   const bool valid = kl < a.K;
-  const uint64_t kg = (uint64_t)(a.k_offset + kl);
   const int H = a.H;
   Dem<false> dem;
   dem.init(a.Z, nullptr, a.rows, a.grid, 0, 0, 1, 1, a.x_min, a.y_min, a.res, a.rinv_res, a.cdiv_res);
@@ -1173,7 +1121,15 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   // ---------------- per-role state
   Traj s;                       // chain
   float L = a.wl, R = a.wr;     // side: filter
-  float e1b = 0.f, e2b = 0.f;   // side: noise of the odd step of the current Philox block
+  // side, MODE 0: this trajectory's normals, rows [2][H] of 256 (mppi_noise_kernel)
+  const float* eps_row = (MODE == 0) ? a.eps + (size_t)blockIdx.x * (2 * H) * TB + tj : nullptr;
+  float en1 = 0.f, en2 = 0.f;
+  if constexpr (MODE == 0) {
+    if (side) {
+      en1 = eps_row[0];
+      en2 = eps_row[(size_t)H * TB];
+    }
+  }
   float pf_sum = 0.f, sw = 0.f, sp = 0.f, ob = 0.f, last_x = a.x0, last_y = a.y0;
   float lwx = 0.f, lwy = 0.f, lwz = 0.f, rwx = 0.f, rwy = 0.f, rwz = 0.f;
   float cm_pend = 0.f;
@@ -1220,8 +1176,8 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
       wait_ge(f_cons, sc - D + 1);
       const float* ri = ring_in + (sc % D) * 2 * TB + tj;
       const float v = ri[0], wv = ri[TB];
-      float sn, cs;
-      dm_sincosf(wv * a.dt, &sn, &cs);
+      float sn, cs;  // sin/cos of the Rodrigues angle: independent of the chain state, so it
+      dm_sincosf(wv * a.dt, &sn, &cs);  // overlaps the position update (measured cheaper here than in the side)
       float cx = 0.f, cy = 0.f, z = 0.f;
       float q[4];
       if constexpr (PROJ == 3) {
@@ -1258,16 +1214,13 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   } else {
     // ---------------- side wave: produce step p, consume step p - PAIR_LAG
     for (int p = 0; p < H + PAIR_LAG; ++p) {
-      if (p < H) {  // noise, sampling, filter (sampling_warp.py:54-138)
-        wait_ge(f_chain, p - D + 1);
+      if (p < H) {  // sampling, filter (sampling_warp.py:54-138); normals precomputed
         float u1, u2;
         if constexpr (MODE == 0) {
-          float e1, e2;
-          if ((p & 1) == 0) {
-            noise_block(a.seed, a.n_base + (uint64_t)(p >> 1), kg, &e1, &e2, &e1b, &e2b);
-          } else {
-            e1 = e1b;
-            e2 = e2b;
+          const float e1 = en1, e2 = en2;
+          if (p + 1 < H) {  // prefetch the next step's normals
+            en1 = eps_row[(size_t)(p + 1) * TB];
+            en2 = eps_row[(size_t)(H + p + 1) * TB];
           }
           const int ti = min(p + 1, H - 1);
           u1 = clampf(a.u_nom1[ti] + a.s1 * e1, a.min_u1, a.max_u1);
@@ -1276,9 +1229,10 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
           const size_t o = (size_t)(valid ? kl : 0) * H + p;
           u1 = a.inj_u1[o];
           u2 = a.inj_u2[o];
+          ust[(size_t)p * TB] = u1;   // MODE 1: the leaf records read the injected controls back
+          ust[(size_t)(H + p) * TB] = u2;
         }
-        ust[(size_t)p * TB] = u1;
-        ust[(size_t)(H + p) * TB] = u2;
+        wait_ge(f_chain, p - D + 1);
         L = L * a.fa + (u1 * a.fk) * (1.0f - a.fa);
         R = R * a.fa + (u2 * a.fk) * (1.0f - a.fa);
         const float vp = clampf((L + R) / 2.0f, a.vmin, a.vmax);
@@ -1291,6 +1245,7 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
             const size_t o1 = (size_t)kl * H + p;
             if (a.d_u1) a.d_u1[o1] = u1;
             if (a.d_u2) a.d_u2[o1] = u2;
+            if (a.d_w) a.d_w[o1] = wp;
           }
         }
         lds_store_release(f_prod, p + 1);
@@ -1337,7 +1292,6 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
             if (a.d_rw) { a.d_rw[o3] = rx; a.d_rw[o3 + 1] = ry; a.d_rw[o3 + 2] = rz; }
             const size_t o1 = (size_t)kl * H + sc;
             if (a.d_v) a.d_v[o1] = vq;
-            if (a.d_w) a.d_w[o1] = ring_in[(sc % D) * 2 * TB + TB + tj];
           }
         }
         lds_store_release(f_cons, sc + 1);
@@ -1368,7 +1322,10 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   }
 #endif
   __syncthreads();
-  leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
+  if constexpr (MODE == 0)  // rows hold the normals; the leaf recomputes the sampled controls
+    leaf_records<TB, NT, true>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB);
+  else
+    leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
 #ifdef MPPI_STAMPS
   const uint64_t k_t2 = dbg_stamp(), k_r2 = __builtin_amdgcn_s_memrealtime();
   if ((tid & 63) == 0 && blockIdx.x < 64) {
@@ -1827,6 +1784,37 @@ hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool u
 hipError_t launch_tail(const FinishArgs& f, hipStream_t st) {
   const size_t lds = (size_t)15 * f.H * sizeof(float);
   hipLaunchKernelGGL(mppi_tail_kernel, dim3(1), dim3(TAIL_THREADS), lds, st, f);
+  return hipGetLastError();
+}
+
+// The step's sampling normals (sampling_warp.py:54-92 with the Philox noise of
+// DEFINED D1), precomputed so the rollout's side waves only load them: thread =
+// (block, Philox block n = t/2, trajectory); writes eps1/eps2 of steps t, t+1.
+__global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t n_base, int64_t k_offset,
+                                                         int H, float* __restrict__ eps) {
+  const int tj = threadIdx.x;
+  const int NB = (H + 1) >> 1;
+  const int n = blockIdx.x % NB;
+  const int blk = blockIdx.x / NB;
+  const uint64_t kg = (uint64_t)(k_offset + (int64_t)blk * 256 + tj);
+  float a1, a2, b1, b2;
+  noise_block(seed, n_base + (uint64_t)n, kg, &a1, &a2, &b1, &b2);
+  const int t = 2 * n;
+  float* e1 = eps + ((size_t)blk * 2 * H + t) * 256 + tj;
+  float* e2 = e1 + (size_t)H * 256;
+  e1[0] = a1;
+  e2[0] = a2;
+  if (t + 1 < H) {
+    e1[256] = b1;
+    e2[256] = b2;
+  }
+}
+
+hipError_t launch_noise(uint64_t seed, uint64_t n_base, int64_t k_offset, int blocks, int H, float* eps,
+                        hipStream_t st) {
+  const int NB = (H + 1) >> 1;
+  hipLaunchKernelGGL(mppi_noise_kernel, dim3((unsigned)(blocks * NB)), dim3(256), 0, st, seed, n_base,
+                     k_offset, H, eps);
   return hipGetLastError();
 }
 
