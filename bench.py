@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="bounded oracle sample on the host (rank 0, N=1); 0 disables")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--no-bilinear", action="store_true", help="skip the C5 tiled-lookup roofline leg")
     ap.add_argument("--sync", action="store_true",
                     help="report the synchronous mode (no deferred optimal rollout) as the headline")
     return ap.parse_args()
@@ -87,6 +88,60 @@ def cpu_baseline(Z, hw, cm, H, seconds):
     return {"value": n / el, "unit": "MPPI steps/s", "cores": 1, "kind": "port",
             "sample": f"{n} full C3 steps (K={K}, H={H}) of oracle/mppi_ref.py in {el:.1f} s on 1 core "
                       f"of {cpu_model()} (os.cpu_count()={os.cpu_count()})"}
+
+
+def bilinear_bench(torch, device, reps=20):
+    """LDS-tiled DEM lookup at C5 size: 8192^2 DEM @0.025 m, N = 262144*128 queries.
+
+    Queries uniform over the tile, binned by 64x64-cell tile once (untimed: inputs resident);
+    `reps` launches of mppi_bilinear_tiled timed with HIP events on the engine's stream.
+    Algorithmic bytes = the DEM once + 12 B per query (x, y in, h out).
+    """
+    from mppi_amd import _lib
+    G, hw, N = 8192, 102.4, 262144 * 128
+    res = 2 * hw / G
+    xs = torch.linspace(-hw, hw, G, device=device)
+    Z = (0.8 * torch.sin(0.37 * xs)[None, :] * torch.cos(0.23 * xs)[:, None]).contiguous()   # synthetic terrain
+    stream = torch.cuda.Stream(device=device)
+    eng = _lib.Engine(_lib.make_params(256, 8), device.index or 0)
+    eng.set_stream(stream.cuda_stream)
+    eng.set_dem_device(Z.data_ptr(), G, G, hw, keepalive=Z)
+    g = torch.Generator(device=device)
+    g.manual_seed(5)
+    x = (torch.rand(N, device=device, generator=g) * 2 - 1) * hw
+    y = (torch.rand(N, device=device, generator=g) * 2 - 1) * hw
+    nt = eng.bilinear_tiles()
+    xb, yb = torch.empty_like(x), torch.empty_like(y)
+    perm = torch.empty(N, dtype=torch.int64, device=device)
+    off = torch.empty(nt + 1, dtype=torch.int32, device=device)
+    eng.bin_queries(x.data_ptr(), y.data_ptr(), N, xb.data_ptr(), yb.data_ptr(), perm.data_ptr(), off.data_ptr())
+    del perm
+    h = torch.empty_like(x)
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            eng.bilinear_tiled(xb.data_ptr(), yb.data_ptr(), off.data_ptr(), h.data_ptr())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            eng.bilinear_tiled(xb.data_ptr(), yb.data_ptr(), off.data_ptr(), h.data_ptr())
+        e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    alg = G * G * 4 + 12 * N
+    # scattered lookup (no binning, corners through L1/L2) on the same unsorted points, for reference
+    hq = torch.empty_like(x)
+    eng.bilinear_query(x.data_ptr(), y.data_ptr(), hq.data_ptr(), N)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.bilinear_query(x.data_ptr(), y.data_ptr(), hq.data_ptr(), N)
+    scat_ms = (time.perf_counter() - t0) * 1e3
+    eng.close()
+    achieved = alg / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": "mppi_bilinear_tiled_kernel", "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "kernel_avg_ms": round(ms, 4), "algorithmic_bytes_per_launch": alg,
+            "workload": f"C5 tile {G}^2 DEM (synthetic), N={N} uniform queries binned by 64x64 tile",
+            "scattered_query_ms": round(scat_ms, 3)}
 
 
 def main():
@@ -217,6 +272,8 @@ def main():
                 "algorithmic_bytes_per_launch": alg_bytes,
             },
         }
+        if world == 1 and not args.no_bilinear:
+            rec["bilinear_roofline"] = bilinear_bench(torch, torch.device("cuda", local_rank))
         if world == 1 and args.cpu_baseline_seconds > 0:
             rec["cpu_baseline"] = cpu_baseline(Z, hw, cm, H, args.cpu_baseline_seconds)
         print(json.dumps(rec), flush=True)

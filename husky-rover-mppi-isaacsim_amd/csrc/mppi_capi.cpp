@@ -101,6 +101,12 @@ struct mppi_ctx {
   bool eps_pending[2] = {false, false};
   hipStream_t noise_stream = nullptr;
   hipEvent_t ev_roll_done = nullptr;
+  // tiled bilinear binning scratch
+  int* bin_tile_of = nullptr;
+  size_t bin_n_cap = 0;
+  int* bin_counts = nullptr;
+  int* bin_cursor = nullptr;
+  size_t bin_t_cap = 0;
   int dem_path = 0;
   // last step (for dump)
   bool have_last = false;
@@ -770,6 +776,9 @@ void mppi_destroy(mppi_ctx* c) {
     if (c->eps_ev[i]) hipEventDestroy(c->eps_ev[i]);
   }
   if (c->ev_roll_done) hipEventDestroy(c->ev_roll_done);
+  if (c->bin_tile_of) hipFree(c->bin_tile_of);
+  if (c->bin_counts) hipFree(c->bin_counts);
+  if (c->bin_cursor) hipFree(c->bin_cursor);
   if (c->noise_stream) hipStreamDestroy(c->noise_stream);
   if (c->tail_stream) hipStreamDestroy(c->tail_stream);
   if (c->inj1) hipFree(c->inj1);
@@ -1059,6 +1068,58 @@ int mppi_bilinear_query(mppi_ctx* c, const float* x, const float* y, float* h, i
   HIP_TRY(hipSetDevice(c->device));
   if (n == 0) return MPPI_OK;
   HIP_TRY(launch_bilinear(c->Z, c->rows, c->cols, c->x_min, c->y_min, c->res, x, y, h, n, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPPI_OK;
+}
+
+int mppi_bilinear_tiles(mppi_ctx* c, int32_t* ntiles) {
+  if (!c || !ntiles) return fail(MPPI_EINVAL, "null argument");
+  if (!c->Z) return fail(MPPI_ESTATE, "no DEM");
+  *ntiles = ((c->rows + BIL_TILE - 1) / BIL_TILE) * ((c->cols + BIL_TILE - 1) / BIL_TILE);
+  return MPPI_OK;
+}
+
+int mppi_bin_queries(mppi_ctx* c, const float* x, const float* y, int64_t n, float* xs_out, float* ys_out,
+                     int64_t* perm, int32_t* tile_off) {
+  if (!c || !x || !y || !xs_out || !ys_out || !perm || !tile_off) return fail(MPPI_EINVAL, "null argument");
+  if (!c->Z) return fail(MPPI_ESTATE, "no DEM");
+  if (n < 0 || n > INT32_MAX) return fail(MPPI_EINVAL, "n out of range [0, 2^31)");
+  HIP_TRY(hipSetDevice(c->device));
+  int32_t nt = 0;
+  mppi_bilinear_tiles(c, &nt);
+  if ((size_t)std::max<int64_t>(n, 1) > c->bin_n_cap) {
+    if (c->bin_tile_of) HIP_TRY(hipFree(c->bin_tile_of));
+    c->bin_tile_of = nullptr;
+    HIP_TRY(hipMalloc(&c->bin_tile_of, (size_t)std::max<int64_t>(n, 1) * sizeof(int)));
+    c->bin_n_cap = (size_t)std::max<int64_t>(n, 1);
+  }
+  if ((size_t)nt > c->bin_t_cap) {
+    if (c->bin_counts) HIP_TRY(hipFree(c->bin_counts));
+    if (c->bin_cursor) HIP_TRY(hipFree(c->bin_cursor));
+    c->bin_counts = c->bin_cursor = nullptr;
+    HIP_TRY(hipMalloc(&c->bin_counts, (size_t)nt * sizeof(int)));
+    HIP_TRY(hipMalloc(&c->bin_cursor, (size_t)nt * sizeof(int)));
+    c->bin_t_cap = (size_t)nt;
+  }
+  HIP_TRY(launch_bin_queries(x, y, n, c->x_min, c->y_min, c->res, c->rinv_res, c->rinv_res != 0.0f, c->rows,
+                             c->cols, c->bin_tile_of, c->bin_counts, c->bin_cursor, tile_off, xs_out, ys_out,
+                             perm, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPPI_OK;
+}
+
+int mppi_bilinear_tiled(mppi_ctx* c, const float* xs, const float* ys, const int32_t* tile_off, float* h) {
+  if (!c || !xs || !ys || !tile_off || !h) return fail(MPPI_EINVAL, "null argument");
+  if (!c->Z) return fail(MPPI_ESTATE, "no DEM");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(launch_bilinear_tiled(c->Z, c->rows, c->cols, c->x_min, c->y_min, c->res, c->rinv_res,
+                                c->rinv_res != 0.0f, xs, ys, h, tile_off, c->stream));
+  return MPPI_OK;
+}
+
+int mppi_sync(mppi_ctx* c) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return MPPI_OK;
 }

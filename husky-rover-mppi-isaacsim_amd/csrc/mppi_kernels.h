@@ -105,5 +105,13 @@ hipError_t launch_noise(uint64_t seed, uint64_t n_base, int64_t k_offset, int bl
                         hipStream_t st);
 hipError_t launch_bilinear(const float* Z, int rows, int grid, float x_min, float y_min, float res,
                            const float* xs, const float* ys, float* hs, int64_t n, hipStream_t st);
+// LDS-tiled lookup over queries binned by 64x64-cell DEM tile (tile count = ceil(rows/64)*ceil(cols/64))
+constexpr int BIL_TILE = 64;
+hipError_t launch_bin_queries(const float* xs, const float* ys, int64_t n, float x_min, float y_min, float res,
+                              float rinv, int cdiv, int rows, int grid, int* tile_of, int* counts, int* cursor,
+                              int* off, float* xs_out, float* ys_out, int64_t* perm, hipStream_t st);
+hipError_t launch_bilinear_tiled(const float* Z, int rows, int grid, float x_min, float y_min, float res,
+                                 float rinv, int cdiv, const float* xs, const float* ys, float* hs,
+                                 const int* tile_off, hipStream_t st);
 
 }  // namespace mppi

@@ -15,6 +15,8 @@
 // operation in the reference's source order; transcendentals come from
 // mppi_detmath.h.  oracle/mppi_ref.py restates the same sequence in numpy.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "mppi_detmath.h"
@@ -376,7 +378,11 @@ __device__ __forceinline__ int costmap_index(int size, float hw, const Recip& rr
 
 #ifdef MPPI_STAMPS
 // Diagnostic build only (profiles/ubench/stamps.sh): per-wave cycle stamps.
-__device__ uint64_t g_dbg_stamps[64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8];
+__device__ uint64_t g_dbg_stamps[64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8 + 16];
+#define FIN_STAMP(k)                                                                    \
+  do {                                                                                  \
+    if (threadIdx.x == 0) g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + (k)] = dbg_stamp(); \
+  } while (0)
 #define LEAF_STAMP(k)                                                                   \
   do {                                                                                  \
     if (threadIdx.x == 0 && blockIdx.x < 64)                                            \
@@ -1466,6 +1472,9 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
   const int tid = threadIdx.x;
   const int H = f.H;
   const int E = 2 * H + 2;
+#ifdef MPPI_STAMPS
+  FIN_STAMP(0);
+#endif
   // ---------------- (1) tree
   // LDS during the tree: [FIN_LDS_NODES][E] doubles, then PairScale table
   double* lnode = reinterpret_cast<double*>(smem_raw);
@@ -1534,6 +1543,9 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
     __syncthreads();
     n = pairs;
   }
+#ifdef MPPI_STAMPS
+  FIN_STAMP(1);
+#endif
   // root = lnode[0..E) (n == 1) or empty (n == 0)
   if (f.mode == 0) {
     for (int j = tid; j < E; j += FIN_THREADS)
@@ -1566,6 +1578,9 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
       for (int c2 = lane; c2 < f.W; c2 += 64) dst[c2] = src[c2];
     }
   }
+#ifdef MPPI_STAMPS
+  FIN_STAMP(2);
+#endif
   // optimal-sequence wheel filter (sampling_warp.py:120-138, k=3.0, a=0.92): the
   // inputs (u*k)*(1-a) in parallel, only the recurrence L = L*a + in on lane 0
   const float one_m_a = 1.0f - f.oa;
@@ -1605,8 +1620,17 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
   dem.init(f.Z, win, f.rows, f.grid, f.wx0, f.wy0, f.W, f.Wr, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
   // mode 1: the whole optimal rollout; mode 2: its first step only (the pose the
   // closed loop needs now), the rest runs in mppi_tail_kernel on a side stream
+#ifdef MPPI_STAMPS
+  FIN_STAMP(3);
+#endif
   optimal_rollout<LDS>(f, dem, vb, snb, csb, chain, f.mode == 2 ? 1 : H, f.out + 4 * H, tid, FIN_THREADS);
+#ifdef MPPI_STAMPS
+  FIN_STAMP(4);
+#endif
   signal_done(f);
+#ifdef MPPI_STAMPS
+  FIN_STAMP(5);
+#endif
 }
 
 // Deferred optimal rollout (MPPI_isaac.py:696-720) of the sequence a mode-2
@@ -1650,6 +1674,183 @@ __global__ __launch_bounds__(256) void mppi_bilinear_kernel(const float* __restr
     }
     hs[i] = h;
   }
+}
+
+// =====================================================================  tiled bilinear (§8(d))
+// Queries binned by DEM tile (BIL_TS x BIL_TS cells; launch_bin_queries): the
+// workgroup of tile b stages the tile's (TS+1)^2 window (the +1 row/col holds the
+// corners of the tile's last cells, clamped to the map) in LDS with row-coalesced
+// loads, then streams the tile's queries: x, y in, h out, all coalesced.  Every
+// DEM byte is read once and each query moves 12 bytes, the kernel's algorithmic
+// traffic.  Cell index and corners follow projection_warp.py:8-48 exactly as
+// Dem::corners (the same clamping), the height projection_warp.py:70-100.
+constexpr int BIL_TS = 64;
+constexpr int BIL_W = BIL_TS + 1;
+
+// corner rows (r0, r1) and columns (c0, c1) of a query, clamped as Dem::corners
+__device__ __forceinline__ void query_cell(float x, float y, float x_min, float y_min, float res,
+                                           float rinv, int cdiv, int rows, int grid, int& r0, int& c0,
+                                           int& r1, int& c1) {
+  float fi, fj;
+  if (cdiv) {
+    fi = cdiv_f(x - x_min, res, rinv);
+    fj = cdiv_f(y + y_min, res, rinv);
+  } else {
+    fi = (x - x_min) / res;
+    fj = (y + y_min) / res;
+  }
+  const int i = trunc_clamped(fi, -1.0f, (float)grid);
+  const int j = -trunc_clamped(fj, -(float)rows, 1.0f);
+  r0 = clampi(j, 0, rows - 1);
+  c0 = clampi(i, 0, grid - 1);
+  r1 = clampi(j + 1, 0, rows - 1);
+  c1 = clampi(i + 1, 0, grid - 1);
+}
+
+// x / res for the bilinear fraction: the verified reciprocal where it is exact
+// (|quotient| >= 2^-90, see cdiv_f), IEEE otherwise.
+__device__ __forceinline__ float frac_div(float x, float res, float rinv, int cdiv) {
+  if (cdiv) {
+    const float q = cdiv_f(x, res, rinv);
+    if (__builtin_expect(fabsf(q) >= 8.077935669463161e-28f, 1)) return q;  // 2^-90
+  }
+  return x / res;
+}
+
+__global__ __launch_bounds__(256) void mppi_bilinear_tiled_kernel(
+    const float* __restrict__ Z, int rows, int grid, float x_min, float y_min, float res, float rinv,
+    int cdiv, const float* __restrict__ xs, const float* __restrict__ ys, float* __restrict__ hs,
+    const int* __restrict__ tile_off, int ntx) {
+  __shared__ float win[BIL_W * BIL_W];
+  const int tile = blockIdx.x;
+  const int q0 = tile_off[tile], q1 = tile_off[tile + 1];
+  if (q0 == q1) return;
+  const int r0 = (tile / ntx) * BIL_TS, c0 = (tile % ntx) * BIL_TS;
+  {  // stage the window: every load issued before the first LDS store
+    constexpr int NLD = (BIL_W * BIL_W + 255) / 256;
+    float tmp[NLD];
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int wr = idx / BIL_W, wc = idx - wr * BIL_W;
+      tmp[k] = (idx < BIL_W * BIL_W) ? Z[(size_t)min(r0 + wr, rows - 1) * grid + min(c0 + wc, grid - 1)] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      if (idx < BIL_W * BIL_W) win[idx] = tmp[k];
+    }
+  }
+  __syncthreads();
+  // BIL_UNROLL queries per thread per pass, loads issued before any is used
+  constexpr int BIL_UNROLL = 4;
+  for (int qb = q0 + threadIdx.x; qb < q1; qb += 256 * BIL_UNROLL) {
+    float xv[BIL_UNROLL], yv[BIL_UNROLL];
+#pragma unroll
+    for (int u = 0; u < BIL_UNROLL; ++u) {
+      const int q = qb + 256 * u;
+      xv[u] = (q < q1) ? xs[q] : 0.0f;
+      yv[u] = (q < q1) ? ys[q] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < BIL_UNROLL; ++u) {
+      const int q = qb + 256 * u;
+      if (q < q1) {
+        const float x = xv[u], y = yv[u];
+        int ra, ca, rb, cb;
+        query_cell(x, y, x_min, y_min, res, rinv, cdiv, rows, grid, ra, ca, rb, cb);
+        const int wa = (ra - r0) * BIL_W, wb = (rb - r0) * BIL_W;
+        const float qa0 = win[wa + (ca - c0)], qa1 = win[wa + (cb - c0)];
+        const float qb0 = win[wb + (ca - c0)], qb1 = win[wb + (cb - c0)];
+        const float xn = frac_div(x, res, rinv, cdiv), yn = frac_div(y, res, rinv, cdiv);
+        const float x2 = xn - truncf(xn), y2 = yn - truncf(yn);
+        const float a0 = ((1.0f - x2) * (1.0f - y2)) * qa0;
+        const float b0 = (x2 * (1.0f - y2)) * qb0;
+        const float c2 = ((1.0f - x2) * y2) * qa1;
+        const float d0 = (x2 * y2) * qb1;
+        hs[q] = ((a0 + b0) + c2) + d0;
+      }
+    }
+  }
+}
+
+// Binning: tile of each query (the tile holding its first corner cell), counts,
+// exclusive scan, stable-free scatter (order inside a tile is arbitrary; perm maps
+// sorted position -> input index).
+__global__ __launch_bounds__(256) void mppi_bin_count_kernel(const float* xs, const float* ys, int64_t n,
+                                                             float x_min, float y_min, float res, float rinv,
+                                                             int cdiv, int rows, int grid, int ntx,
+                                                             int* __restrict__ tile_of, int* counts) {
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n; q += (int64_t)gridDim.x * 256) {
+    int ra, ca, rb, cb;
+    query_cell(xs[q], ys[q], x_min, y_min, res, rinv, cdiv, rows, grid, ra, ca, rb, cb);
+    const int t = (ra / BIL_TS) * ntx + ca / BIL_TS;
+    tile_of[q] = t;
+    atomicAdd(&counts[t], 1);
+  }
+}
+
+// exclusive scan of counts[ntiles] into off[ntiles+1]; one workgroup of 1024 threads
+__global__ __launch_bounds__(1024) void mppi_bin_scan_kernel(const int* counts, int ntiles, int* off,
+                                                             int* cursor) {
+  __shared__ int part[1024];
+  const int per = (ntiles + 1023) / 1024;
+  const int b = threadIdx.x * per, e = min(b + per, ntiles);
+  int sum = 0;
+  for (int t = b; t < e; ++t) sum += counts[t];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan of the partial sums
+    const int v = (threadIdx.x >= o) ? part[threadIdx.x - o] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int run = (threadIdx.x == 0) ? 0 : part[threadIdx.x - 1];
+  for (int t = b; t < e; ++t) {
+    off[t] = run;
+    cursor[t] = run;
+    run += counts[t];
+  }
+  if (threadIdx.x == 1023) off[ntiles] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void mppi_bin_scatter_kernel(const float* xs, const float* ys, int64_t n,
+                                                               const int* tile_of, int* cursor, float* xs_out,
+                                                               float* ys_out, int64_t* perm) {
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n; q += (int64_t)gridDim.x * 256) {
+    const int pos = atomicAdd(&cursor[tile_of[q]], 1);
+    xs_out[pos] = xs[q];
+    ys_out[pos] = ys[q];
+    perm[pos] = q;
+  }
+}
+
+hipError_t launch_bin_queries(const float* xs, const float* ys, int64_t n, float x_min, float y_min, float res,
+                              float rinv, int cdiv, int rows, int grid, int* tile_of, int* counts, int* cursor,
+                              int* off, float* xs_out, float* ys_out, int64_t* perm, hipStream_t st) {
+  const int ntx = (grid + BIL_TS - 1) / BIL_TS, nty = (rows + BIL_TS - 1) / BIL_TS;
+  const int ntiles = ntx * nty;
+  hipError_t e = hipMemsetAsync(counts, 0, (size_t)ntiles * sizeof(int), st);
+  if (e != hipSuccess) return e;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
+  if (n > 0)
+    hipLaunchKernelGGL(mppi_bin_count_kernel, dim3(blocks), dim3(256), 0, st, xs, ys, n, x_min, y_min, res, rinv,
+                       cdiv, rows, grid, ntx, tile_of, counts);
+  hipLaunchKernelGGL(mppi_bin_scan_kernel, dim3(1), dim3(1024), 0, st, counts, ntiles, off, cursor);
+  if (n > 0)
+    hipLaunchKernelGGL(mppi_bin_scatter_kernel, dim3(blocks), dim3(256), 0, st, xs, ys, n, tile_of, cursor, xs_out,
+                       ys_out, perm);
+  return hipGetLastError();
+}
+
+hipError_t launch_bilinear_tiled(const float* Z, int rows, int grid, float x_min, float y_min, float res,
+                                 float rinv, int cdiv, const float* xs, const float* ys, float* hs,
+                                 const int* tile_off, hipStream_t st) {
+  const int ntx = (grid + BIL_TS - 1) / BIL_TS, nty = (rows + BIL_TS - 1) / BIL_TS;
+  hipLaunchKernelGGL(mppi_bilinear_tiled_kernel, dim3(ntx * nty), dim3(256), 0, st, Z, rows, grid, x_min, y_min,
+                     res, rinv, cdiv, xs, ys, hs, tile_off, ntx);
+  return hipGetLastError();
 }
 
 // =====================================================================  self-test

@@ -91,6 +91,11 @@ _PROTOS = {
     "mppi_get_launch_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]),
     "mppi_bilinear_query": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
     "mppi_selftest": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.POINTER(C.c_int64)]),
+    "mppi_bilinear_tiles": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
+    "mppi_bin_queries": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_void_p]),
+    "mppi_bilinear_tiled": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mppi_sync": (C.c_int, [C.c_void_p]),
 }
 
 _lib = None
@@ -345,6 +350,25 @@ class Engine:
         bad = C.c_int64()
         self._c(self.lib.mppi_selftest(self.ctx, int(what), int(n), int(seed), C.byref(bad)), "mppi_selftest")
         return bad.value
+
+    def bilinear_tiles(self):
+        n = C.c_int32()
+        self._c(self.lib.mppi_bilinear_tiles(self.ctx, C.byref(n)), "mppi_bilinear_tiles")
+        return n.value
+
+    def bin_queries(self, x_ptr, y_ptr, n, xs_ptr, ys_ptr, perm_ptr, off_ptr):
+        self._c(self.lib.mppi_bin_queries(self.ctx, C.c_void_p(int(x_ptr)), C.c_void_p(int(y_ptr)), int(n),
+                                          C.c_void_p(int(xs_ptr)), C.c_void_p(int(ys_ptr)),
+                                          C.c_void_p(int(perm_ptr)), C.c_void_p(int(off_ptr))), "mppi_bin_queries")
+
+    def bilinear_tiled(self, xs_ptr, ys_ptr, off_ptr, h_ptr):
+        """Asynchronous on the engine stream (sync() waits)."""
+        self._c(self.lib.mppi_bilinear_tiled(self.ctx, C.c_void_p(int(xs_ptr)), C.c_void_p(int(ys_ptr)),
+                                             C.c_void_p(int(off_ptr)), C.c_void_p(int(h_ptr))),
+                "mppi_bilinear_tiled")
+
+    def sync(self):
+        self._c(self.lib.mppi_sync(self.ctx), "mppi_sync")
 
     def bilinear_query(self, x_ptr, y_ptr, h_ptr, n):
         self._c(self.lib.mppi_bilinear_query(self.ctx, C.c_void_p(int(x_ptr)), C.c_void_p(int(y_ptr)),

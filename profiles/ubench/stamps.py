@@ -38,12 +38,13 @@ def main():
     H = 100
     eng = _lib.Engine(_lib.make_params(K, H), 0)
     eng.set_dem_path(path)
+    eng.set_async_tail(True)
     eng.set_dem(Z, hw)
     eng.set_costmap(cm, hw)
     eng.set_state(_lib.make_state(-60.0, -5.0, goal_x=65.0, goal_y=10.0))
     for i in range(5):
         eng.step("3d", i)
-    n = 64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8
+    n = 64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8 + 16
     buf = (C.c_uint64 * n)()
     assert lib.mppi_debug_stamps(buf, n) == 0
     allv = np.array(buf, dtype=np.float64)
@@ -65,7 +66,11 @@ def main():
     phases = H + 2
     chain = a[:, :4].reshape(-1, 2) / phases
     side = a[:, 4:].reshape(-1, 2) / phases
-    lf = allv[64 * 16 * 6 + 1024 * 2:].reshape(64, 8)[:nb]
+    lf = allv[64 * 16 * 6 + 1024 * 2: 64 * 16 * 6 + 1024 * 2 + 64 * 8].reshape(64, 8)[:nb]
+    fs = allv[64 * 16 * 6 + 1024 * 2 + 64 * 8:][:6]
+    fd = np.diff(fs)
+    print(f"  finish (mode 2): tree {fd[0]:.0f}  u_opt {fd[1]:.0f}  filter+sincos {fd[2]:.0f}  step0 {fd[3]:.0f}  "
+          f"signal {fd[4]:.0f} cyc")
     print(f"  leaf records: min+exp {(lf[:, 1] - lf[:, 0]).mean():.0f}  rows {(lf[:, 4] - lf[:, 1]).mean():.0f} cyc")
     print(f"K={K} kernel={path}: cycles per step (mean over {nb} blocks)")
     print(f"  chain waves: work {chain[:, 0].mean():8.1f}  wait {chain[:, 1].mean():8.1f}")
