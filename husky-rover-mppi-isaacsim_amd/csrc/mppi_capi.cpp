@@ -100,7 +100,17 @@ struct mppi_ctx {
   hipEvent_t eps_ev[2] = {nullptr, nullptr};
   bool eps_pending[2] = {false, false};
   hipStream_t noise_stream = nullptr;
+  int prio_least = 0, prio_greatest = 0;
+  // tree levels inside the rollout kernel (MPPI_FUSED_FINISH): 0 none (default: measured fastest
+  // with the deferred optimal rollout, profiles/r01_notes.md), 1 the first level, 2 all + the finish
+  int fused_level = 0;
   hipEvent_t ev_roll_done = nullptr;
+  hipEvent_t ev_prev_roll = nullptr;  // recorded after the last rollout that read an eps slot
+  // fused finish: cross-workgroup tree counters / level records
+  unsigned* tree_cnt = nullptr;
+  unsigned* noise_ctr = nullptr;  // [2] in-kernel noise work / exit counters
+  double* tree_nodes = nullptr;
+  size_t tree_cap = 0;
   // tiled bilinear binning scratch
   int* bin_tile_of = nullptr;
   size_t bin_n_cap = 0;
@@ -242,10 +252,10 @@ Plan make_plan(const mppi_ctx* c) {
                                  scratch_ws
                            : (size_t)15 * TB * sizeof(float) + scratch_ws;
   }
-  // finish kernel: tree phase [32][2H+2] doubles + 128*7 PairScale (16 B); tail phase
-  // uo[2H] v[H] w[H] sin[H] cos[H] chain[12H] floats, then the DEM window
-  pl.fin_tree_bytes = (size_t)32 * (2 * H + 2) * sizeof(double) + (size_t)128 * 7 * 16;
-  pl.fin_win_offset = (int)(((size_t)18 * H * sizeof(float) + 15) / 16 * 16);
+  // finish kernel: tree phase [16][2H+2] doubles + 64 x (15 PairScale + 16 m); phase 2
+  // uo[2H] v[H] w[H] sin[H] cos[H] chain[12H] out[16H] floats, then the DEM window
+  pl.fin_tree_bytes = (size_t)16 * (2 * H + 2) * sizeof(double) + (size_t)64 * (15 * 16 + 16 * 4);
+  pl.fin_win_offset = (int)(((size_t)34 * H * sizeof(float) + 15) / 16 * 16);
   // the optimal rollout stages the window only on request: one workgroup loading 150 KB costs
   // more than the L2 latency it saves on 100 serial steps (measured, profiles/r01_notes.md)
   pl.fin_lds = lds_fits && c->dem_path == 1 && (pl.fin_win_offset + win) <= kLdsBytes;
@@ -265,6 +275,24 @@ int ensure_nodes(mppi_ctx* c, int blocks) {
   HIP_TRY(hipMalloc(&c->scratch0, half * sizeof(double)));
   HIP_TRY(hipMalloc(&c->scratch1, half * sizeof(double)));
   c->nodes_cap = need;
+  return MPPI_OK;
+}
+
+// Counters and level records of the in-kernel cross-workgroup tree (fused finish).
+int ensure_tree(mppi_ctx* c, int blocks) {
+  size_t groups = 0;
+  for (int n = blocks; n > 1; n = (n + 15) / 16) groups += (size_t)(n + 15) / 16;  // groups of 16
+  groups = std::max<size_t>(groups, 1);
+  if (groups <= c->tree_cap) return MPPI_OK;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->tree_cnt) HIP_TRY(hipFree(c->tree_cnt));
+  if (c->tree_nodes) HIP_TRY(hipFree(c->tree_nodes));
+  c->tree_cnt = nullptr;
+  c->tree_nodes = nullptr;
+  HIP_TRY(hipMalloc(&c->tree_cnt, groups * sizeof(unsigned)));
+  HIP_TRY(hipMemset(c->tree_cnt, 0, groups * sizeof(unsigned)));
+  HIP_TRY(hipMalloc(&c->tree_nodes, groups * E_of(c) * sizeof(double)));
+  c->tree_cap = groups;
   return MPPI_OK;
 }
 
@@ -487,12 +515,14 @@ int eps_for_step(mppi_ctx* c, const Plan& pl, uint64_t step, int* slot_out) {
 }
 
 // After the rollout of `step` (which reads slot `used`) is enqueued: generate the
-// normals of step + 1 into the other slot on noise_stream once that rollout is done.
+// normals of step + 1 into the other slot on noise_stream, ordered after the previous
+// rollout (the last reader of that slot, ev_roll_done of the previous call).  The
+// noise workgroups cannot share a CU with a rollout workgroup (LDS reservation), so
+// they run on the CUs the rollout kernel has released while its finish completes.
 int speculate_eps(mppi_ctx* c, const Plan& pl, uint64_t step, int used) {
   const int other = used ^ 1;
   const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
-  HIP_TRY(hipEventRecord(c->ev_roll_done, c->stream));
-  HIP_TRY(hipStreamWaitEvent(c->noise_stream, c->ev_roll_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->noise_stream, c->ev_prev_roll, 0));
   HIP_TRY(launch_noise(c->p.seed, (step + 1) * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[other],
                        c->noise_stream));
   HIP_TRY(hipEventRecord(c->eps_ev[other], c->noise_stream));
@@ -503,7 +533,8 @@ int speculate_eps(mppi_ctx* c, const Plan& pl, uint64_t step, int used) {
 
 // Enqueue the rollout kernel for the current state / nominal sequence.
 int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl,
-                    const float* unom, const mppi_state& st, const RolloutArgs* dump_args) {
+                    const float* unom, const mppi_state& st, const RolloutArgs* dump_args,
+                    const FinishArgs* fused = nullptr, int fused_level = 0) {
   if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
   int rc = ensure_nodes(c, pl.blocks);
   if (rc) return rc;
@@ -516,11 +547,29 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   }
   RolloutArgs a;
   fill_rollout(c, pl, st, step, unom, a);
+  if (fused) {
+    rc = ensure_tree(c, pl.blocks);
+    if (rc) return rc;
+    a.fused = fused_level;
+    a.fin = *fused;
+    a.tree_cnt = c->tree_cnt;
+    a.tree_nodes = c->tree_nodes;
+    a.noise_ctr = c->noise_ctr;
+  }
   int eps_slot = -1;
   if (pl.pair && mode == 0 && pl.blocks > 0) {
     rc = eps_for_step(c, pl, step, &eps_slot);
     if (rc) return rc;
     a.eps = c->eps[eps_slot];
+    if (fused && fused_level == 2 && !dump_args) {  // generated by the workgroups that finish early
+      a.eps_next = c->eps[eps_slot ^ 1];
+      a.n_base_next = (step + 1) * (uint64_t)((H_of(c) + 1) / 2);
+      c->eps_step[eps_slot ^ 1] = -1;  // being overwritten
+      if (c->eps_pending[eps_slot ^ 1]) {  // an earlier noise-stream fill of that slot
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->eps_ev[eps_slot ^ 1], 0));
+        c->eps_pending[eps_slot ^ 1] = false;
+      }
+    }
   }
   if (dump_args) {
     a.d_traj = dump_args->d_traj;
@@ -545,24 +594,31 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     c->ev_roll_pending = true;
   }
-  if (eps_slot >= 0 && !dump_args) return speculate_eps(c, pl, step, eps_slot);
+  if (a.eps_next) {  // the kernel leaves the next step's normals in the other slot
+    c->eps_step[eps_slot ^ 1] = (int64_t)(step + 1);
+    c->eps_pending[eps_slot ^ 1] = false;  // same stream: ordered before the next rollout
+  } else if (eps_slot >= 0 && !dump_args) {
+    // no fused epilogue: generate them on the noise stream after this rollout
+    HIP_TRY(hipEventRecord(c->ev_prev_roll, c->stream));
+    return speculate_eps(c, pl, step, eps_slot);
+  }
   return MPPI_OK;
 }
 
-int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const double* recs, int n,
-                   int mode, double* record_out, bool timed) {
-  FinishArgs f;
+// Finish arguments for `mode` (0: rank record, 1: finish; 1 becomes 2 with the deferred
+// optimal rollout): claims the completion sequence number and the tail buffers of the
+// next parity, ordering the context stream after the tail that last used them.
+int prepare_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, int mode, double* record_out,
+                   FinishArgs& f, int& par) {
   fill_finish(c, pl, st, f);
   if (mode == 1 && c->async_tail) mode = 2;
-  f.recs = recs;
-  f.n_recs = n;
   f.mode = mode;
   f.record_out = record_out;
   if (mode >= 1) {
     f.done = c->done;
     f.seq = ++c->seq;
   }
-  const int par = c->tail_par ^ 1;
+  par = c->tail_par ^ 1;
   if (mode == 2) {
     f.tail_in = c->tail_in[par];
     f.tail_out = c->tail_host[par];
@@ -575,38 +631,54 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
       else c->tail_inflight[par] = false;
     }
   }
+  return MPPI_OK;
+}
+
+// The deferred optimal rollout on the side stream, after what the context stream holds.
+int enqueue_tail(mppi_ctx* c, const FinishArgs& f, int par) {
+  HIP_TRY(hipEventRecord(c->ev_fin_done, c->stream));
+  HIP_TRY(hipStreamWaitEvent(c->tail_stream, c->ev_fin_done, 0));
+  if (c->timing) {
+    collect_tail_timing(c);
+    HIP_TRY(hipEventRecord(c->ev[4], c->tail_stream));
+  }
+  HIP_TRY(launch_tail(f, c->tail_stream));
+  if (c->timing) {
+    HIP_TRY(hipEventRecord(c->ev[5], c->tail_stream));
+    c->ev_tail_pending = true;
+  }
+  HIP_TRY(hipEventRecord(c->ev_tail[par], c->tail_stream));
+  c->tail_inflight[par] = true;
+  c->tail_par = par;
+  c->tail_pending = true;
+  return MPPI_OK;
+}
+
+int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const double* recs, int n,
+                   int mode, double* record_out, bool timed) {
+  FinishArgs f;
+  int par = 0;
+  int rc = prepare_finish(c, pl, st, mode, record_out, f, par);
+  if (rc) return rc;
+  f.recs = recs;
+  f.n_recs = n;
   if (n > 1) {
-    int rc = ensure_nodes(c, n);
+    rc = ensure_nodes(c, n);
     if (rc) return rc;
     f.scratch0 = c->scratch0;
     f.scratch1 = c->scratch1;
   }
   if (timed && c->timing) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-  HIP_TRY(launch_finish(f, mode == 0 ? pl.fin_tree_bytes : pl.fin_lds_bytes, c->stream,
-                        mode == 1 && pl.fin_lds));
+  HIP_TRY(launch_finish(f, f.mode == 0 ? pl.fin_tree_bytes : pl.fin_lds_bytes, c->stream,
+                        f.mode == 1 && pl.fin_lds));
   if (timed && c->timing) {
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     c->ev_fin_pending = true;
   }
-  if (mode == 2) {  // the optimal rollout runs on the side stream, overlapping what follows
-    HIP_TRY(hipEventRecord(c->ev_fin_done, c->stream));
-    HIP_TRY(hipStreamWaitEvent(c->tail_stream, c->ev_fin_done, 0));
-    if (c->timing) {
-      collect_tail_timing(c);
-      HIP_TRY(hipEventRecord(c->ev[4], c->tail_stream));
-    }
-    HIP_TRY(launch_tail(f, c->tail_stream));
-    if (c->timing) {
-      HIP_TRY(hipEventRecord(c->ev[5], c->tail_stream));
-      c->ev_tail_pending = true;
-    }
-    HIP_TRY(hipEventRecord(c->ev_tail[par], c->tail_stream));
-    c->tail_inflight[par] = true;
-    c->tail_par = par;
-    c->tail_pending = true;
-  }
+  if (f.mode == 2) return enqueue_tail(c, f, par);
   return MPPI_OK;
 }
+
 
 void fill_outputs(const float* o, int H, mppi_outputs* out) {
   if (out->u1_opt) std::memcpy(out->u1_opt, o, H * sizeof(float));
@@ -665,6 +737,30 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   const Plan pl = make_plan(c);
   if (c->dem_path == 1 && (size_t)pl.W * pl.Wr * sizeof(float) > kLdsBytes)
     return fail(MPPI_EINVAL, "DEM window does not fit in LDS");
+  if (pl.pair && pl.blocks > 0 && c->fused_level == 2) {  // whole finish in the rollout kernel
+    FinishArgs f;
+    int par = 0;
+    rc = prepare_finish(c, pl, c->st, 1, nullptr, f, par);
+    if (rc) return rc;
+    rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr, &f, 2);
+    if (rc) return rc;
+    remember(c, proj, step, mode, pl);
+    if (f.mode == 2) {
+      rc = enqueue_tail(c, f, par);
+      if (rc) return rc;
+    }
+    return copy_outputs(c, out);
+  }
+  if (pl.pair && pl.blocks > 1 && c->fused_level == 1) {  // first tree level in the rollout kernel
+    FinishArgs unused;
+    std::memset(&unused, 0, sizeof(unused));
+    rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr, &unused, 1);
+    if (rc) return rc;
+    remember(c, proj, step, mode, pl);
+    rc = enqueue_finish(c, pl, c->st, c->tree_nodes, (pl.blocks + 15) / 16, 1, nullptr, true);
+    if (rc) return rc;
+    return copy_outputs(c, out);
+  }
   rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr);
   if (rc) return rc;
   remember(c, proj, step, mode, pl);
@@ -702,12 +798,19 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   mppi_ctx* c = new mppi_ctx();
   c->p = p;
   c->device = device;
+  if (const char* e = std::getenv("MPPI_FUSED_FINISH")) c->fused_level = std::min(std::max(std::atoi(e), 0), 2);
+  const char* ep = std::getenv("MPPI_STREAM_PRIO");
+  const bool use_prio = !(ep && std::atoi(ep) == 0);
   const int H = p.num_iterations;
   auto cleanup = [&](int rc) {
     mppi_destroy(c);
     return rc;
   };
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+  // the rollout stream outranks the speculative noise stream at dispatch
+  if (hipDeviceGetStreamPriorityRange(&c->prio_least, &c->prio_greatest) != hipSuccess)
+    return cleanup(fail(MPPI_EHIP, "hipDeviceGetStreamPriorityRange failed"));
+  if (!use_prio) c->prio_least = c->prio_greatest = 0;
+  if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, c->prio_greatest) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipStreamCreate failed"));
   c->own_stream = true;
   if (hipMalloc(&c->u_nom[0], 2 * H * sizeof(float)) != hipSuccess ||
@@ -716,6 +819,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipHostMalloc(&c->stage, 16 * H * sizeof(float), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&c->done, 64, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->cdiv_bad, sizeof(unsigned)) != hipSuccess ||
+      hipMalloc(&c->noise_ctr, 2 * sizeof(unsigned)) != hipSuccess ||
       hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->tail_in[1], 3 * H * sizeof(float)) != hipSuccess ||
@@ -732,14 +836,17 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipEventCreateWithFlags(&c->ev_tail[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_tail[1], hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->tail_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->noise_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->noise_stream, hipStreamNonBlocking, c->prio_least) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_roll_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_prev_roll, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->eps_ev[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->eps_ev[1], hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "side stream / event creation failed"));
   c->out_host = new float[16 * H]();
   std::memset(c->stage, 0, 16 * H * sizeof(float));
   *c->done = 0;
+  if (hipMemset(c->noise_ctr, 0, 2 * sizeof(unsigned)) != hipSuccess)
+    return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
   if (hipDeviceSynchronize() != hipSuccess) return cleanup(fail(MPPI_EHIP, "device sync failed"));
   *out = c;
   return MPPI_OK;
@@ -776,7 +883,11 @@ void mppi_destroy(mppi_ctx* c) {
     if (c->eps_ev[i]) hipEventDestroy(c->eps_ev[i]);
   }
   if (c->ev_roll_done) hipEventDestroy(c->ev_roll_done);
+  if (c->ev_prev_roll) hipEventDestroy(c->ev_prev_roll);
   if (c->bin_tile_of) hipFree(c->bin_tile_of);
+  if (c->tree_cnt) hipFree(c->tree_cnt);
+  if (c->noise_ctr) hipFree(c->noise_ctr);
+  if (c->tree_nodes) hipFree(c->tree_nodes);
   if (c->bin_counts) hipFree(c->bin_counts);
   if (c->bin_cursor) hipFree(c->bin_cursor);
   if (c->noise_stream) hipStreamDestroy(c->noise_stream);
@@ -800,7 +911,7 @@ int mppi_set_stream(mppi_ctx* c, void* s) {
     c->stream = (hipStream_t)s;
     c->own_stream = false;
   } else {
-    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, c->prio_greatest));
     c->own_stream = true;
   }
   return MPPI_OK;
@@ -934,6 +1045,24 @@ int mppi_step_partial(mppi_ctx* c, int32_t proj, uint64_t step, double* record_d
   if (rc) return rc;
   if (!record_dev) return fail(MPPI_EINVAL, "null record buffer");
   const Plan pl = make_plan(c);
+  if (pl.pair && pl.blocks > 0 && c->fused_level == 2) {  // the rank record straight out of the rollout
+    FinishArgs f;
+    int par = 0;
+    rc = prepare_finish(c, pl, c->st, 0, record_dev, f, par);
+    if (rc) return rc;
+    rc = enqueue_rollout(c, proj, step, 0, pl, c->u_nom[c->cur], c->st, nullptr, &f, 2);
+    if (rc) return rc;
+    remember(c, proj, step, 0, pl);
+    return MPPI_OK;
+  }
+  if (pl.pair && pl.blocks > 1 && c->fused_level == 1) {
+    FinishArgs unused;
+    std::memset(&unused, 0, sizeof(unused));
+    rc = enqueue_rollout(c, proj, step, 0, pl, c->u_nom[c->cur], c->st, nullptr, &unused, 1);
+    if (rc) return rc;
+    remember(c, proj, step, 0, pl);
+    return enqueue_finish(c, pl, c->st, c->tree_nodes, (pl.blocks + 15) / 16, 0, record_dev, false);
+  }
   rc = enqueue_rollout(c, proj, step, 0, pl, c->u_nom[c->cur], c->st, nullptr);
   if (rc) return rc;
   remember(c, proj, step, 0, pl);

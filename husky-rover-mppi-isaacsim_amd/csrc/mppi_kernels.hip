@@ -435,6 +435,39 @@ __device__ __forceinline__ double pair_apply(const PairScale& p, double a, doubl
   return (double)p.ea * a + (double)p.eb * b;
 }
 
+// Subtree over an aligned group of G records (log2 G levels of the binary tree):
+// scales of its G-1 pairs, level by level (ps[0 .. G/2) first), from the members' m.
+template <int G>
+__device__ __forceinline__ void group_scales(const float (&m)[G], float T, PairScale (&ps)[G - 1]) {
+  float cur[G];
+#pragma unroll
+  for (int i = 0; i < G; ++i) cur[i] = m[i];
+  int base = 0;
+#pragma unroll
+  for (int w = G / 2; w >= 1; w >>= 1) {
+#pragma unroll
+    for (int i = 0; i < w; ++i) {
+      ps[base + i] = pair_scale(cur[2 * i], cur[2 * i + 1], T);
+      cur[i] = ps[base + i].m;
+    }
+    base += w;
+  }
+}
+template <int G>
+__device__ __forceinline__ double group_apply(const PairScale* ps, const double (&v)[G], int j) {
+  double cur[G];
+#pragma unroll
+  for (int i = 0; i < G; ++i) cur[i] = v[i];
+  int base = 0;
+#pragma unroll
+  for (int w = G / 2; w >= 1; w >>= 1) {
+#pragma unroll
+    for (int i = 0; i < w; ++i) cur[i] = pair_apply(ps[base + i], cur[2 * i], cur[2 * i + 1], j);
+    base += w;
+  }
+  return cur[0];
+}
+
 template <int TB, int NT, bool EPS = false>
 __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
                                              unsigned char* scratch, const float* ub_block);
@@ -1068,6 +1101,150 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_ws_kernel(const RolloutAr
 #endif
 }
 
+template <bool LDS>
+__device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, unsigned char* smem, int tid,
+                                              int nthreads);
+
+// Cross-workgroup softmax tree without a second kernel: the last workgroup of each
+// aligned group of 16 to arrive combines the group's records (four levels of the
+// binary tree, as mppi_finish_kernel / oracle tree_reduce), level by level, until
+// one record remains; that workgroup then stores the rank record (fin.mode 0) or
+// runs the finish (fin.mode 1/2).  Release/acquire fences at device scope make the
+// records written on other XCDs visible; each counter is re-armed by its last
+// arriver for the next launch.
+template <int NT>
+__device__ __forceinline__ bool fused_tree_finish(const RolloutArgs& a, unsigned char* smem, int tid) {
+  const int H = a.H, E = 2 * H + 2;
+  int* flag = reinterpret_cast<int*>(smem);
+  int idx = blockIdx.x, count = gridDim.x;
+  const double* src = a.nodes;
+  double* dst = a.tree_nodes;
+  unsigned* cnt = a.tree_cnt;
+#ifdef MPPI_STAMPS
+  int lvl_dbg = 0;
+  FIN_STAMP(6);
+#endif
+  constexpr int G = 16;  // aligned groups of 16 records: 256 workgroups -> 16 -> 1
+  int levels = (a.fused == 1) ? 1 : 64;  // fused 1: the first level only, mppi_finish_kernel does the rest
+  while (count > 1 && levels-- > 0) {
+    const int g = idx / G;
+    const int gsize = min(G, count - G * g);
+    const int groups = (count + G - 1) / G;
+    __syncthreads();  // this workgroup's record is complete
+    if (tid == 0) {
+      __threadfence();  // release it device-wide
+      const unsigned prev = atomicAdd(&cnt[g], 1u);
+      const int last = prev == (unsigned)(gsize - 1);
+      if (last) cnt[g] = 0u;
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return false;
+    __threadfence();  // acquire the other members' records
+#ifdef MPPI_STAMPS
+    FIN_STAMP(7 + 2 * lvl_dbg);
+#endif
+    // the group's G-1 pair scales once, level by level, into LDS; then every element
+    float* lm = reinterpret_cast<float*>(smem + 16);                      // [G]
+    PairScale* lps = reinterpret_cast<PairScale*>(smem + 16 + 4 * G);      // [G-1]
+    if (tid < G) lm[tid] = (tid < gsize) ? (float)src[(size_t)(G * g + tid) * E] : INFINITY;
+    __syncthreads();
+    int base = 0;
+#pragma unroll
+    for (int w = G / 2; w >= 1; w >>= 1) {
+      PairScale p;
+      if (tid < w) {
+        p = pair_scale(lm[2 * tid], lm[2 * tid + 1], a.T);
+        lps[base + tid] = p;
+      }
+      __syncthreads();
+      if (tid < w) lm[tid] = p.m;
+      __syncthreads();
+      base += w;
+    }
+    for (int j = tid; j < E; j += NT) {
+      double v[G];
+#pragma unroll
+      for (int i = 0; i < G; ++i) v[i] = (i < gsize) ? src[(size_t)(G * g + i) * E + j] : 0.0;
+      dst[(size_t)g * E + j] = group_apply<G>(lps, v, j);
+    }
+    src = dst;
+    dst += (size_t)groups * E;
+    cnt += groups;
+    idx = g;
+    count = groups;
+#ifdef MPPI_STAMPS
+    FIN_STAMP(8 + 2 * lvl_dbg);
+    ++lvl_dbg;
+#endif
+  }
+  __syncthreads();  // src[idx * E ..] is the root (written by this workgroup)
+  if (a.fused == 1) return true;  // first level only: the group records go to mppi_finish_kernel
+  const double* root = src + (size_t)idx * E;
+  if (a.fin.mode == 0) {
+    for (int j = tid; j < E; j += NT) a.fin.record_out[j] = root[j];
+    return true;
+  }
+  const double S = root[1];
+  const float ures = (tid < 2 * H && S > 0.0) ? (float)(root[2 + tid] / S) : 0.0f;
+  __syncthreads();
+  finish_phase2<false>(a.fin, ures, smem, tid, NT);
+  return true;
+}
+
+// The next step's sampling normals (mppi_noise_kernel's work), shared out in chunks of
+// 4 Philox rows x 256 trajectories among the workgroups whose own work is done: they
+// finish at different times (the last one runs the finish), so the generation fills
+// the CUs the kernel would otherwise leave idle.  The last workgroup to leave re-arms
+// the counters.
+template <int NT>
+__device__ __forceinline__ void noise_ahead(const RolloutArgs& a, unsigned char* smem, int tid) {
+  int* sh = reinterpret_cast<int*>(smem);
+  if (a.eps_next) {
+    const int H = a.H;
+    const int NB = (H + 1) >> 1, NB4 = (NB + 3) >> 2;
+    const int total = (int)gridDim.x * NB4;
+    const int tj = tid & 255;
+    __syncthreads();
+    if (tid == 0) sh[0] = (int)atomicAdd(&a.noise_ctr[0], 1u);
+    __syncthreads();
+    int c = sh[0];
+    while (c < total) {
+      __syncthreads();
+      if (tid == 0) sh[0] = (int)atomicAdd(&a.noise_ctr[0], 1u);  // the next chunk, fetched ahead
+      const int blk = c / NB4, n0 = (c - blk * NB4) * 4;
+      const uint64_t kg = (uint64_t)(a.k_offset + (int64_t)blk * 256 + tj);
+#pragma unroll
+      for (int r = 0; r < 4; r += NT / 256) {
+        const int n = n0 + r + (tid >> 8);
+        if (n < NB) {
+          float a1, a2, b1, b2;
+          noise_block(a.seed, a.n_base_next + (uint64_t)n, kg, &a1, &a2, &b1, &b2);
+          const int t = 2 * n;
+          float* e1 = a.eps_next + ((size_t)blk * 2 * H + t) * 256 + tj;
+          float* e2 = e1 + (size_t)H * 256;
+          e1[0] = a1;
+          e2[0] = a2;
+          if (t + 1 < H) {
+            e1[256] = b1;
+            e2[256] = b2;
+          }
+        }
+      }
+      __syncthreads();
+      c = sh[0];
+    }
+  }
+  if (tid == 0 && a.noise_ctr) {
+    __threadfence();
+    const unsigned left = atomicAdd(&a.noise_ctr[1], 1u);
+    if (left == gridDim.x - 1) {  // every workgroup is past its last atomicAdd on [0]
+      a.noise_ctr[0] = 0u;
+      a.noise_ctr[1] = 0u;
+    }
+  }
+}
+
 // =====================================================================  pair-synchronised rollout kernel
 // Same roles as mppi_rollout_ws_kernel (chain wave c and side wave c serve the
 // trajectories 64c..64c+63), but each chain/side PAIR synchronises only with
@@ -1332,6 +1509,12 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
     leaf_records<TB, NT, true>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB);
   else
     leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
+  if constexpr (!DUMP) {
+    if (a.fused) {
+      fused_tree_finish<NT>(a, smem_raw, tid);  // the rings are dead: reuse their LDS
+      if (a.fused == 2) noise_ahead<NT>(a, smem_raw, tid);
+    }
+  }
 #ifdef MPPI_STAMPS
   const uint64_t k_t2 = dbg_stamp(), k_r2 = __builtin_amdgcn_s_memrealtime();
   if ((tid & 63) == 0 && blockIdx.x < 64) {
@@ -1358,33 +1541,64 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 // only the serial chain (chain3d) runs on one lane, sin/cos, heights and wheel
 // contacts are computed by all lanes around it.
 constexpr int FIN_THREADS = 1024;
-constexpr int FIN_LDS_NODES = 32;
-constexpr int FIN_GROUP_CHUNK = 128;   // groups per scale-table fill (7 PairScale each)
-constexpr int FIN_MAX_ITEMS = 8;       // (FIN_LDS_NODES/2) * (2H+2) <= 8192  <=>  H <= 255
+constexpr int FIN_LDS_NODES = 16;
+constexpr int FIN_GROUP_CHUNK = 64;    // groups per scale-table fill (15 PairScale + 16 m each)
+constexpr int FIN_MAX_ITEMS = 4;       // (FIN_LDS_NODES/2) * (2H+2) <= 4096  <=>  H <= 255
 
-// scales of the 7 pairs of a group of 8 (levels 0,1,2) from the members' m
 __device__ __forceinline__ void group8_scales(const float (&m)[8], float T, PairScale (&ps)[7]) {
-  float m1[4], m2[2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    ps[i] = pair_scale(m[2 * i], m[2 * i + 1], T);
-    m1[i] = ps[i].m;
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    ps[4 + i] = pair_scale(m1[2 * i], m1[2 * i + 1], T);
-    m2[i] = ps[4 + i].m;
-  }
-  ps[6] = pair_scale(m2[0], m2[1], T);
+  group_scales<8>(m, T, ps);
+}
+__device__ __forceinline__ double group8_apply(const PairScale* ps, const double (&v)[8], int j) {
+  return group_apply<8>(ps, v, j);
 }
 
-__device__ __forceinline__ double group8_apply(const PairScale* ps, const double (&v)[8], int j) {
-  double a[4], b[2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) a[i] = pair_apply(ps[i], v[2 * i], v[2 * i + 1], j);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) b[i] = pair_apply(ps[4 + i], a[2 * i], a[2 * i + 1], j);
-  return pair_apply(ps[6], b[0], b[1], j);
+// Robot pose with the heading projected on the DEM (projection_warp.py:306-310).
+template <bool LDS>
+__device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>& dem) {
+  const float res_half_neg = (-f.res) / 2.0f;
+  const float res_sq = f.res * f.res;
+  Traj s;
+  s.x = f.x0;
+  s.y = f.y0;
+  bool unused = false;
+  float q[4];
+  dem.template corners<false>(s.x, s.y, q, unused);
+  const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
+  const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
+  const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
+  const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
+  const float d = (f.h0x * nx + f.h0y * ny) + f.h0z * nz;
+  const float tx = f.h0x - d * nx, ty = f.h0y - d * ny, tz = f.h0z - d * nz;
+  const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
+  s.hx = tx / tn;
+  s.hy = ty / tn;
+  s.hz = tz / tn;
+  return s;
+}
+
+// Step 0 of the optimal rollout on one lane (no barrier): traj | hv | lw | rw of the
+// first step into out[0..12), the layout optimal_rollout uses for nsteps = 1.
+template <bool LDS>
+__device__ __forceinline__ void first_step(const FinishArgs& f, const Dem<LDS>& dem, float v, float sn, float cs,
+                                           float* out) {
+  const float res_half_neg = (-f.res) / 2.0f;
+  const float res_sq = f.res * f.res;
+  Traj s = initial_pose(f, dem);
+  const Traj saved = s;
+  float q[4], nx, ny, nz;
+  bool bad = false;
+  chain3d<kChainFast, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+  if (kChainFast && __builtin_expect(bad, 0)) {
+    s = saved;
+    chain3d<false, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+  }
+  StepOut o;
+  bool bad2 = false;
+  wheels3d<false, LDS>(dem, f.off, s.x, s.y, q, nx, ny, nz, s.hx, s.hy, s.hz, o, bad2);
+  out[0] = s.x; out[1] = s.y; out[2] = o.z;
+  out[3] = s.hx; out[4] = s.hy; out[5] = s.hz;
+  out[6] = o.lx; out[7] = o.ly; out[8] = o.lz;
+  out[9] = o.rx; out[10] = o.ry; out[11] = o.rz;
 }
 
 // The 3D rollout of the optimal sequence for `nsteps` steps from the robot pose
@@ -1398,24 +1612,7 @@ __device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem<L
   const float res_half_neg = (-f.res) / 2.0f;
   const float res_sq = f.res * f.res;
   if (tid == 0) {  // the serial chain (projection_warp.py:306-326)
-    Traj s;
-    s.x = f.x0;
-    s.y = f.y0;
-    {
-      bool unused = false;
-      float q[4];
-      dem.template corners<false>(s.x, s.y, q, unused);
-      const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
-      const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
-      const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
-      const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
-      const float d = (f.h0x * nx + f.h0y * ny) + f.h0z * nz;
-      const float tx = f.h0x - d * nx, ty = f.h0y - d * ny, tz = f.h0z - d * nz;
-      const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
-      s.hx = tx / tn;
-      s.hy = ty / tn;
-      s.hz = tz / tn;
-    }
+    Traj s = initial_pose(f, dem);
     float vn = vb[0], sn_n = snb[0], cs_n = csb[0];
     for (int t = 0; t < nsteps; ++t) {
       const float v = vn, sn = sn_n, cs = cs_n;
@@ -1466,6 +1663,136 @@ __device__ __forceinline__ void signal_done(const FinishArgs& f) {
     __hip_atomic_store(f.done, f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Phase 2 of the finish (MPPI_isaac.py:655-720): `ures` = u_opt[tid] for tid < 2H
+// (V/S of the root record); the optimal-sequence filter, the outputs, and the
+// optimal rollout (whole, or step 0 with the rest deferred, f.mode 2), then the
+// completion word.  Called by all `nthreads` threads of one workgroup; smem holds
+// uo[2H] v[H] w[H] sn[H] cs[H] chain[12H] out[16H] floats (+ the DEM window for LDS).
+template <bool LDS>
+__device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, unsigned char* smem, int tid,
+                                              int nthreads) {
+  const int H = f.H;
+  float* uo = reinterpret_cast<float*>(smem);
+  float* vb = uo + 2 * H;
+  float* wb = vb + H;
+  float* snb = wb + H;
+  float* csb = snb + H;
+  float* chain = csb + H;  // [H][12]: x, y, q00, q01, q10, q11, nx, ny, nz, hx, hy, hz
+  // outputs are staged here and stored to f.out (pinned host memory) in one burst at the
+  // end: a workgroup barrier after host stores would wait for their PCIe round trip
+  float* ostage = chain + 12 * H;  // [16H]
+  const int nout = f.mode == 2 ? 4 * H + 12 : 16 * H;
+  const float one_m_a = 1.0f - f.oa;
+  if (tid < 2 * H) {
+    f.u_nom_next[tid] = ures;
+    ostage[tid] = ures;
+    // optimal-sequence wheel filter (sampling_warp.py:120-138, k=3.0, a=0.92): the
+    // inputs (u*k)*(1-a) in parallel, only the recurrence L = L*a + in on lane 0
+    uo[tid] = (ures * f.ok) * one_m_a;
+  }
+  float* win = reinterpret_cast<float*>(smem + f.win_offset);
+  if constexpr (LDS) {
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int r = wave; r < f.Wr; r += nthreads / 64) {
+      const float* src = f.Z + (size_t)(f.wy0 + r) * f.grid + f.wx0;
+      float* dst = win + r * f.W;
+      for (int c2 = lane; c2 < f.W; c2 += 64) dst[c2] = src[c2];
+    }
+  }
+  __syncthreads();
+#ifdef MPPI_STAMPS
+  FIN_STAMP(2);
+#endif
+  Dem<LDS> dem;
+  dem.init(f.Z, win, f.rows, f.grid, f.wx0, f.wy0, f.W, f.Wr, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
+  const int lane = tid & 63, wave = tid >> 6;
+  if (wave == 0) {
+    // the recurrence on every lane of wave 0 (identical values), inputs read 8 at a time
+    // as LDS broadcasts; lane t%64 keeps L_t, R_t and stores them once per 64 steps
+    float L = f.wl, R = f.wr;
+    float myL = 0.0f, myR = 0.0f;
+    int t = 0;
+    for (; t + 8 <= H; t += 8) {
+      float i1[8], i2[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        i1[k] = uo[t + k];
+        i2[k] = uo[H + t + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        L = L * f.oa + i1[k];
+        R = R * f.oa + i2[k];
+        const bool mine = lane == ((t + k) & 63);
+        myL = mine ? L : myL;
+        myR = mine ? R : myR;
+      }
+      if (((t + 8) & 63) == 0) {
+        vb[t + 8 - 64 + lane] = myL;
+        wb[t + 8 - 64 + lane] = myR;
+      }
+    }
+    for (; t < H; ++t) {
+      L = L * f.oa + uo[t];
+      R = R * f.oa + uo[H + t];
+      const bool mine = lane == (t & 63);
+      myL = mine ? L : myL;
+      myR = mine ? R : myR;
+    }
+    if ((H & 63) != 0 && lane < (H & 63)) {  // the last, partial 64-step block
+      vb[(H & ~63) + lane] = myL;
+      wb[(H & ~63) + lane] = myR;
+    }
+#ifdef MPPI_STAMPS
+    FIN_STAMP(12);
+#endif
+  } else if (wave == 1 && f.mode == 2) {
+    if (lane == 0) {  // step 0 of the optimal rollout needs only the first filter step
+      const float L0 = f.wl * f.oa + uo[0], R0 = f.wr * f.oa + uo[H];
+      const float v0 = clampf((L0 + R0) / 2.0f, f.vmin, f.vmax);
+      const float w0 = clampf(((-L0) + R0) / f.rwheel, f.wmin, f.wmax);
+      float sn0, cs0;
+      dm_sincosf(w0 * f.dt, &sn0, &cs0);
+      first_step<LDS>(f, dem, v0, sn0, cs0, ostage + 4 * H);
+    }
+  }
+  __syncthreads();
+  for (int t = tid; t < H; t += nthreads) {
+    const float L = vb[t], R = wb[t];
+    const float v = clampf((L + R) / 2.0f, f.vmin, f.vmax);
+    const float w = clampf(((-L) + R) / f.rwheel, f.wmin, f.wmax);
+    float sn, cs;
+    dm_sincosf(w * f.dt, &sn, &cs);
+    vb[t] = v;
+    wb[t] = w;
+    snb[t] = sn;
+    csb[t] = cs;
+    ostage[2 * H + t] = v;
+    ostage[3 * H + t] = w;
+    if (f.mode == 2) {  // inputs of the deferred optimal rollout (mppi_tail_kernel)
+      f.tail_in[t] = v;
+      f.tail_in[H + t] = sn;
+      f.tail_in[2 * H + t] = cs;
+    }
+  }
+  __syncthreads();
+#ifdef MPPI_STAMPS
+  FIN_STAMP(3);
+#endif
+  // mode 1: the whole optimal rollout; mode 2: its first step only (the pose the
+  // closed loop needs now), the rest runs in mppi_tail_kernel on a side stream
+  if (f.mode != 2) optimal_rollout<LDS>(f, dem, vb, snb, csb, chain, H, ostage + 4 * H, tid, nthreads);
+  __syncthreads();
+  for (int i = tid; i < nout; i += nthreads) f.out[i] = ostage[i];
+#ifdef MPPI_STAMPS
+  FIN_STAMP(4);
+#endif
+  signal_done(f);
+#ifdef MPPI_STAMPS
+  FIN_STAMP(5);
+#endif
+}
+
 template <bool LDS>
 __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishArgs f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -1483,29 +1810,52 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
   int n = f.n_recs;
   double* bufs[2] = {f.scratch0, f.scratch1};
   int flip = 0;
-  while (n > FIN_LDS_NODES) {  // global -> global, groups of 8
-    const int groups = (n + 7) >> 3;
+  while (n > FIN_LDS_NODES) {  // global -> global, aligned groups of 16 (4 tree levels)
+    const int groups = (n + 15) >> 4;
     double* out = bufs[flip];
     for (int g0 = 0; g0 < groups; g0 += FIN_GROUP_CHUNK) {
       const int ng = min(FIN_GROUP_CHUNK, groups - g0);
-      if (tid < ng) {
-        const int g = g0 + tid;
-        float m[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) m[i] = (8 * g + i < n) ? (float)cur[(size_t)(8 * g + i) * E] : INFINITY;
-        PairScale ps[7];
-        group8_scales(m, f.T, ps);
-#pragma unroll
-        for (int i = 0; i < 7; ++i) lps[tid * 7 + i] = ps[i];
+      // pair scales of the chunk's groups, level by level: lm[ng][16] -> lps[ng][15]
+      float* lm = reinterpret_cast<float*>(lps + FIN_GROUP_CHUNK * 15);
+      for (int i = tid; i < ng * 16; i += FIN_THREADS) {
+        const int r = 16 * g0 + i;
+        lm[i] = (r < n) ? (float)cur[(size_t)r * E] : INFINITY;
       }
       __syncthreads();
-      for (int it = tid; it < ng * E; it += FIN_THREADS) {
-        const int gl = it / E, j = it - gl * E;
-        const int g = g0 + gl;
-        double v[8];
+      int base = 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = (8 * g + i < n) ? cur[(size_t)(8 * g + i) * E + j] : 0.0;
-        out[(size_t)g * E + j] = group8_apply(lps + gl * 7, v, j);
+      for (int w = 8; w >= 1; w >>= 1) {
+        PairScale p;
+        const int gl = tid / w, pi = tid - gl * w;
+        const bool act = tid < ng * w;
+        if (act) {
+          p = pair_scale(lm[gl * 16 + 2 * pi], lm[gl * 16 + 2 * pi + 1], f.T);
+          lps[gl * 15 + base + pi] = p;
+        }
+        __syncthreads();
+        if (act) lm[gl * 16 + pi] = p.m;
+        __syncthreads();
+        base += w;
+      }
+      // every element of every group, two items per thread with all 32 loads in flight
+      for (int it0 = tid; it0 < ng * E; it0 += 2 * FIN_THREADS) {
+        double v[2][16];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int it = it0 + q * FIN_THREADS;
+          const int gl = it / E, j = it - gl * E;
+          const int r0 = 16 * (g0 + gl);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) v[q][i] = (it < ng * E && r0 + i < n) ? cur[(size_t)(r0 + i) * E + j] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int it = it0 + q * FIN_THREADS;
+          if (it < ng * E) {
+            const int gl = it / E, j = it - gl * E;
+            out[(size_t)(g0 + gl) * E + j] = group_apply<16>(lps + gl * 15, v[q], j);
+          }
+        }
       }
       __syncthreads();
     }
@@ -1553,84 +1903,11 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
     return;
   }
   // ---------------- (2) optimal sequence
-  // LDS: uo[2H] v[H] w[H] sn[H] cs[H] chain[12H] | window (at f.win_offset)
   const double S = (n == 1) ? lnode[1] : 0.0;
   // u_opt = V / S (DEFINED; zero when no trajectory has a finite cost)
   const float ures = (tid < 2 * H && S > 0.0) ? (float)(lnode[2 + tid] / S) : 0.0f;
   __syncthreads();  // lnode is dead from here on
-  float* uo = reinterpret_cast<float*>(smem_raw);
-  float* vb = uo + 2 * H;
-  float* wb = vb + H;
-  float* snb = wb + H;
-  float* csb = snb + H;
-  float* chain = csb + H;  // [H][12]: x, y, q00, q01, q10, q11, nx, ny, nz, hx, hy, hz
-  if (tid < 2 * H) {
-    uo[tid] = ures;
-    f.u_nom_next[tid] = ures;
-    f.out[tid] = ures;
-  }
-  float* win = reinterpret_cast<float*>(smem_raw + f.win_offset);
-  if constexpr (LDS) {
-    const int lane = tid & 63, wave = tid >> 6;
-    for (int r = wave; r < f.Wr; r += FIN_THREADS / 64) {
-      const float* src = f.Z + (size_t)(f.wy0 + r) * f.grid + f.wx0;
-      float* dst = win + r * f.W;
-      for (int c2 = lane; c2 < f.W; c2 += 64) dst[c2] = src[c2];
-    }
-  }
-#ifdef MPPI_STAMPS
-  FIN_STAMP(2);
-#endif
-  // optimal-sequence wheel filter (sampling_warp.py:120-138, k=3.0, a=0.92): the
-  // inputs (u*k)*(1-a) in parallel, only the recurrence L = L*a + in on lane 0
-  const float one_m_a = 1.0f - f.oa;
-  if (tid < 2 * H) uo[tid] = (uo[tid] * f.ok) * one_m_a;
-  __syncthreads();
-  if (tid == 0) {
-    float L = f.wl, R = f.wr;
-    for (int t = 0; t < H; ++t) {
-      L = L * f.oa + uo[t];
-      R = R * f.oa + uo[H + t];
-      vb[t] = L;
-      wb[t] = R;
-    }
-  }
-  __syncthreads();
-  for (int t = tid; t < H; t += FIN_THREADS) {
-    const float L = vb[t], R = wb[t];
-    vb[t] = clampf((L + R) / 2.0f, f.vmin, f.vmax);
-    wb[t] = clampf(((-L) + R) / f.rwheel, f.wmin, f.wmax);
-  }
-  __syncthreads();
-  for (int t = tid; t < H; t += FIN_THREADS) {
-    float sn, cs;
-    dm_sincosf(wb[t] * f.dt, &sn, &cs);
-    snb[t] = sn;
-    csb[t] = cs;
-    f.out[2 * H + t] = vb[t];
-    f.out[3 * H + t] = wb[t];
-    if (f.mode == 2) {  // inputs of the deferred optimal rollout (mppi_tail_kernel)
-      f.tail_in[t] = vb[t];
-      f.tail_in[H + t] = sn;
-      f.tail_in[2 * H + t] = cs;
-    }
-  }
-  __syncthreads();
-  Dem<LDS> dem;
-  dem.init(f.Z, win, f.rows, f.grid, f.wx0, f.wy0, f.W, f.Wr, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
-  // mode 1: the whole optimal rollout; mode 2: its first step only (the pose the
-  // closed loop needs now), the rest runs in mppi_tail_kernel on a side stream
-#ifdef MPPI_STAMPS
-  FIN_STAMP(3);
-#endif
-  optimal_rollout<LDS>(f, dem, vb, snb, csb, chain, f.mode == 2 ? 1 : H, f.out + 4 * H, tid, FIN_THREADS);
-#ifdef MPPI_STAMPS
-  FIN_STAMP(4);
-#endif
-  signal_done(f);
-#ifdef MPPI_STAMPS
-  FIN_STAMP(5);
-#endif
+  finish_phase2<LDS>(f, ures, smem_raw, tid, FIN_THREADS);
 }
 
 // Deferred optimal rollout (MPPI_isaac.py:696-720) of the sequence a mode-2

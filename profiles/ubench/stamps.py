@@ -67,10 +67,17 @@ def main():
     chain = a[:, :4].reshape(-1, 2) / phases
     side = a[:, 4:].reshape(-1, 2) / phases
     lf = allv[64 * 16 * 6 + 1024 * 2: 64 * 16 * 6 + 1024 * 2 + 64 * 8].reshape(64, 8)[:nb]
-    fs = allv[64 * 16 * 6 + 1024 * 2 + 64 * 8:][:6]
-    fd = np.diff(fs)
+    fs = allv[64 * 16 * 6 + 1024 * 2 + 64 * 8:][:16]
+    fd = np.diff(fs[:6])
     print(f"  finish (mode 2): tree {fd[0]:.0f}  u_opt {fd[1]:.0f}  filter+sincos {fd[2]:.0f}  step0 {fd[3]:.0f}  "
           f"signal {fd[4]:.0f} cyc")
+    if fs[6] > 0:  # fused tree: entry (latest block), per level: acquire -> combined
+        t = fs[6:12] - fs[6]
+        print(f"  fused tree (cyc after the last block entered): " +
+              "  ".join(f"L{k}: start {t[1 + 2 * k]:.0f} done {t[2 + 2 * k]:.0f}" for k in range(2)) +
+              f"  phase2 start {fs[2] - fs[6]:.0f}  end {fs[5] - fs[6]:.0f}")
+    print(f"  phase2: filter loop {fs[12] - fs[2]:.0f}  rest to step0-ready {fs[3] - fs[12]:.0f}  "
+          f"outputs {fs[4] - fs[3]:.0f} signal {fs[5] - fs[4]:.0f} cyc")
     print(f"  leaf records: min+exp {(lf[:, 1] - lf[:, 0]).mean():.0f}  rows {(lf[:, 4] - lf[:, 1]).mean():.0f} cyc")
     print(f"K={K} kernel={path}: cycles per step (mean over {nb} blocks)")
     print(f"  chain waves: work {chain[:, 0].mean():8.1f}  wait {chain[:, 1].mean():8.1f}")
