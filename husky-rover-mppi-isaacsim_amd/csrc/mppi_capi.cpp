@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -104,11 +105,21 @@ struct mppi_ctx {
   // tree levels inside the rollout kernel (MPPI_FUSED_FINISH): 0 none (default: measured fastest
   // with the deferred optimal rollout, profiles/r01_notes.md), 1 the first level, 2 all + the finish
   int fused_level = 0;
+  // host-side step timeline (env MPPI_HOST_TRACE=1, printed by mppi_destroy): microseconds summed
+  // over steps of [previous done seen -> entry, entry -> rollout enqueued, -> all enqueued, wait]
+  bool trace = false;
+  double tr_prev_done = 0, tr_sum[4] = {0, 0, 0, 0}, tr_t0 = 0, tr_t1 = 0, tr_mark[4] = {0, 0, 0, 0};
+  double tr_msum[4] = {0, 0, 0, 0};
+  long tr_n = 0;
+  int wave_prio = 1;  // rollout waves raise their issue priority (env MPPI_WAVE_PRIO=0: off)
   hipEvent_t ev_roll_done = nullptr;
   hipEvent_t ev_prev_roll = nullptr;  // recorded after the last rollout that read an eps slot
   // fused finish: cross-workgroup tree counters / level records
   unsigned* tree_cnt = nullptr;
   unsigned* noise_ctr = nullptr;  // [2] in-kernel noise work / exit counters
+  double* level1 = nullptr;       // finish kernel first-level records
+  size_t level1_cap = 0;
+  unsigned* level1_cnt = nullptr;
   double* tree_nodes = nullptr;
   size_t tree_cap = 0;
   // tiled bilinear binning scratch
@@ -179,6 +190,10 @@ int verified_reciprocal(mppi_ctx* c, float b, float* y_out) {
   return MPPI_OK;
 }
 int E_of(const mppi_ctx* c) { return 2 * c->p.num_iterations + 2; }
+
+double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 int check_ready(mppi_ctx* c) {
   if (!c) return fail(MPPI_EINVAL, "null context");
@@ -547,6 +562,7 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   }
   RolloutArgs a;
   fill_rollout(c, pl, st, step, unom, a);
+  a.wave_prio = c->wave_prio;
   if (fused) {
     rc = ensure_tree(c, pl.blocks);
     if (rc) return rc;
@@ -557,6 +573,7 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     a.noise_ctr = c->noise_ctr;
   }
   int eps_slot = -1;
+  if (c->trace) c->tr_mark[0] = now_us();
   if (pl.pair && mode == 0 && pl.blocks > 0) {
     rc = eps_for_step(c, pl, step, &eps_slot);
     if (rc) return rc;
@@ -583,8 +600,10 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   }
   if (pl.blocks == 0) return MPPI_OK;
   if (c->timing && !dump_args) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  if (c->trace) c->tr_mark[1] = now_us();
   if (pl.pair)
     HIP_TRY(launch_rollout_pair(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr));
+  if (c->trace) c->tr_mark[2] = now_us();
   else if (pl.ws)
     HIP_TRY(launch_rollout_ws(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr));
   else
@@ -668,9 +687,22 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
     f.scratch0 = c->scratch0;
     f.scratch1 = c->scratch1;
   }
+  // first tree level on ceil(n/16) workgroups (one per aligned group of 16 records)
+  const int groups = n > 16 ? (n + 15) / 16 : 1;
+  if (groups > 1) {
+    if ((size_t)groups > c->level1_cap) {
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (c->level1) HIP_TRY(hipFree(c->level1));
+      c->level1 = nullptr;
+      HIP_TRY(hipMalloc(&c->level1, (size_t)groups * E_of(c) * sizeof(double)));
+      c->level1_cap = (size_t)groups;
+    }
+    f.level1 = c->level1;
+    f.level1_cnt = c->level1_cnt;
+  }
   if (timed && c->timing) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   HIP_TRY(launch_finish(f, f.mode == 0 ? pl.fin_tree_bytes : pl.fin_lds_bytes, c->stream,
-                        f.mode == 1 && pl.fin_lds));
+                        f.mode == 1 && pl.fin_lds, groups));
   if (timed && c->timing) {
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     c->ev_fin_pending = true;
@@ -732,6 +764,7 @@ void remember(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
 }
 
 int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out) {
+  if (c && c->trace) c->tr_t0 = now_us();
   int rc = check_ready(c);
   if (rc) return rc;
   const Plan pl = make_plan(c);
@@ -763,10 +796,27 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   }
   rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr);
   if (rc) return rc;
+  if (c->trace) c->tr_t1 = now_us();
   remember(c, proj, step, mode, pl);
   rc = enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 1, nullptr, true);
   if (rc) return rc;
-  return copy_outputs(c, out);
+  if (!c->trace) return copy_outputs(c, out);
+  const double t2 = now_us();
+  rc = copy_outputs(c, out);
+  const double t3 = now_us();
+  if (c->tr_prev_done > 0) {
+    c->tr_sum[0] += c->tr_t0 - c->tr_prev_done;
+    c->tr_sum[1] += c->tr_t1 - c->tr_t0;
+    c->tr_sum[2] += t2 - c->tr_t1;
+    c->tr_sum[3] += t3 - t2;
+    c->tr_msum[0] += c->tr_mark[0] - c->tr_t0;
+    c->tr_msum[1] += c->tr_mark[1] - c->tr_mark[0];
+    c->tr_msum[2] += c->tr_mark[2] - c->tr_mark[1];
+    c->tr_msum[3] += c->tr_t1 - c->tr_mark[2];
+    ++c->tr_n;
+  }
+  c->tr_prev_done = t3;
+  return rc;
 }
 
 }  // namespace
@@ -799,6 +849,8 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   c->p = p;
   c->device = device;
   if (const char* e = std::getenv("MPPI_FUSED_FINISH")) c->fused_level = std::min(std::max(std::atoi(e), 0), 2);
+  if (const char* e = std::getenv("MPPI_HOST_TRACE")) c->trace = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MPPI_WAVE_PRIO")) c->wave_prio = std::atoi(e) != 0;
   const char* ep = std::getenv("MPPI_STREAM_PRIO");
   const bool use_prio = !(ep && std::atoi(ep) == 0);
   const int H = p.num_iterations;
@@ -820,6 +872,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipHostMalloc(&c->done, 64, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->cdiv_bad, sizeof(unsigned)) != hipSuccess ||
       hipMalloc(&c->noise_ctr, 2 * sizeof(unsigned)) != hipSuccess ||
+      hipMalloc(&c->level1_cnt, sizeof(unsigned)) != hipSuccess ||
       hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->tail_in[1], 3 * H * sizeof(float)) != hipSuccess ||
@@ -845,7 +898,8 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   c->out_host = new float[16 * H]();
   std::memset(c->stage, 0, 16 * H * sizeof(float));
   *c->done = 0;
-  if (hipMemset(c->noise_ctr, 0, 2 * sizeof(unsigned)) != hipSuccess)
+  if (hipMemset(c->noise_ctr, 0, 2 * sizeof(unsigned)) != hipSuccess ||
+      hipMemset(c->level1_cnt, 0, sizeof(unsigned)) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
   if (hipDeviceSynchronize() != hipSuccess) return cleanup(fail(MPPI_EHIP, "device sync failed"));
   *out = c;
@@ -854,6 +908,14 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
 
 void mppi_destroy(mppi_ctx* c) {
   if (!c) return;
+  if (c->trace && c->tr_n > 0)
+    std::fprintf(stderr, "mppi host trace (us/step over %ld steps): caller %.1f  enqueue rollout %.1f  "
+                 "enqueue rest %.1f  wait+copy %.1f\n", c->tr_n, c->tr_sum[0] / c->tr_n, c->tr_sum[1] / c->tr_n,
+                 c->tr_sum[2] / c->tr_n, c->tr_sum[3] / c->tr_n);
+  if (c->trace && c->tr_n > 0)
+    std::fprintf(stderr, "mppi host trace, enqueue rollout (us/step): plan+args %.1f  noise slot %.1f  launch %.1f  "
+                 "events+noise launch %.1f\n", c->tr_msum[0] / c->tr_n, c->tr_msum[1] / c->tr_n,
+                 c->tr_msum[2] / c->tr_n, c->tr_msum[3] / c->tr_n);
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->tail_stream) hipStreamSynchronize(c->tail_stream);
@@ -887,6 +949,8 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->bin_tile_of) hipFree(c->bin_tile_of);
   if (c->tree_cnt) hipFree(c->tree_cnt);
   if (c->noise_ctr) hipFree(c->noise_ctr);
+  if (c->level1) hipFree(c->level1);
+  if (c->level1_cnt) hipFree(c->level1_cnt);
   if (c->tree_nodes) hipFree(c->tree_nodes);
   if (c->bin_counts) hipFree(c->bin_counts);
   if (c->bin_cursor) hipFree(c->bin_cursor);

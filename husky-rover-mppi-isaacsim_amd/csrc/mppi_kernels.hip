@@ -381,7 +381,8 @@ __device__ __forceinline__ int costmap_index(int size, float hw, const Recip& rr
 __device__ uint64_t g_dbg_stamps[64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8 + 16];
 #define FIN_STAMP(k)                                                                    \
   do {                                                                                  \
-    if (threadIdx.x == 0) g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + (k)] = dbg_stamp(); \
+    if (threadIdx.x == 0)                                                               \
+      g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #define LEAF_STAMP(k)                                                                   \
   do {                                                                                  \
@@ -1284,12 +1285,20 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   const bool side = wave >= NWC;
   const int tj = side ? tid - TB : tid;  // trajectory within the workgroup
   const int pair = side ? wave - NWC : wave;
+  // issue priority over the deferred optimal rollout of the previous step (mppi_tail_kernel,
+  // priority 0), which shares one CU with a rollout workgroup: it has a whole step of slack
+  if (a.wave_prio) __builtin_amdgcn_s_setprio(2);
   int* f_prod = flags + pair;
   int* f_chain = flags + NWC + pair;
   int* f_cons = flags + 2 * NWC + pair;
 #ifdef MPPI_STAMPS
   const uint64_t k_t0 = dbg_stamp(), k_r0 = __builtin_amdgcn_s_memrealtime();
   uint64_t st_wait = 0;
+  if (blockIdx.x == 0 && tid == 0) {  // previous finish's completion signal -> this kernel's start
+    uint64_t* fs = g_dbg_stamps + 64 * 16 * 6 + 1024 * 2 + 64 * 8;
+    fs[14] = fs[5];
+    fs[15] = k_r0;
+  }
 #endif
   const int64_t kl = (int64_t)blockIdx.x * TB + tj;
   const bool valid = kl < a.K;
@@ -1543,7 +1552,6 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 constexpr int FIN_THREADS = 1024;
 constexpr int FIN_LDS_NODES = 16;
 constexpr int FIN_GROUP_CHUNK = 64;    // groups per scale-table fill (15 PairScale + 16 m each)
-constexpr int FIN_MAX_ITEMS = 4;       // (FIN_LDS_NODES/2) * (2H+2) <= 4096  <=>  H <= 255
 
 __device__ __forceinline__ void group8_scales(const float (&m)[8], float T, PairScale (&ps)[7]) {
   group_scales<8>(m, T, ps);
@@ -1655,12 +1663,17 @@ __device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem<L
   }
 }
 
-// Make every lane's output stores visible system-wide, then publish f.seq.
+// Publish f.seq once every output is in host memory.  The outputs were stored with
+// system-scope (write-through) atomic stores, so completing them (vmcnt) is enough:
+// no cache write-back, whose cost grows with whatever else is dirty in L2 (e.g. the
+// next step's normals being generated on other CUs).
+__device__ __forceinline__ void store_out(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void signal_done(const FinishArgs& f) {
-  __threadfence_system();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0 && f.done)
-    __hip_atomic_store(f.done, f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0 && f.done) __hip_atomic_store(f.done, f.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Phase 2 of the finish (MPPI_isaac.py:655-720): `ures` = u_opt[tid] for tid < 2H
@@ -1783,7 +1796,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
   // closed loop needs now), the rest runs in mppi_tail_kernel on a side stream
   if (f.mode != 2) optimal_rollout<LDS>(f, dem, vb, snb, csb, chain, H, ostage + 4 * H, tid, nthreads);
   __syncthreads();
-  for (int i = tid; i < nout; i += nthreads) f.out[i] = ostage[i];
+  for (int i = tid; i < nout; i += nthreads) store_out(f.out + i, ostage[i]);
 #ifdef MPPI_STAMPS
   FIN_STAMP(4);
 #endif
@@ -1800,7 +1813,7 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
   const int H = f.H;
   const int E = 2 * H + 2;
 #ifdef MPPI_STAMPS
-  FIN_STAMP(0);
+  if (blockIdx.x == 0) FIN_STAMP(0);
 #endif
   // ---------------- (1) tree
   // LDS during the tree: [FIN_LDS_NODES][E] doubles, then PairScale table
@@ -1810,6 +1823,97 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
   int n = f.n_recs;
   double* bufs[2] = {f.scratch0, f.scratch1};
   int flip = 0;
+  if (gridDim.x > 1) {
+    // first level on gridDim.x workgroups: workgroup b combines records [16b, 16b+16) into
+    // f.level1[b]; the last to finish (device-scope counter) carries on with the rest
+    const int b = blockIdx.x;
+    const int gsize = min(16, n - 16 * b);
+    float* lm = reinterpret_cast<float*>(lps + 15);
+    if (tid < 16) lm[tid] = (tid < gsize) ? (float)cur[(size_t)(16 * b + tid) * E] : INFINITY;
+    __syncthreads();
+    int base = 0;
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1) {
+      PairScale p;
+      if (tid < w) {
+        p = pair_scale(lm[2 * tid], lm[2 * tid + 1], f.T);
+        lps[base + tid] = p;
+      }
+      __syncthreads();
+      if (tid < w) lm[tid] = p.m;
+      __syncthreads();
+      base += w;
+    }
+#ifdef MPPI_STAMPS
+    if (b == 0) FIN_STAMP(9);
+#endif
+    // device-scope stores write through the XCD's L2, so no fence has to write the whole
+    // (rollout-dirty) L2 back: completion of these stores (vmcnt) orders them before the count
+    for (int j = tid; j < E; j += FIN_THREADS) {
+      double v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = cur[(size_t)(16 * b + min(i, gsize - 1)) * E + j];
+      __hip_atomic_store(f.level1 + (size_t)b * E + j, group_apply<16>(lps, v, j), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#ifdef MPPI_STAMPS
+    if (b == 0) FIN_STAMP(10);
+#endif
+    int* flag = reinterpret_cast<int*>(lm + 16);
+    if (tid == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(f.level1_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == gridDim.x - 1;
+      if (last) __hip_atomic_store(f.level1_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+#ifdef MPPI_STAMPS
+    FIN_STAMP(13);
+#endif
+    // the level-1 records, read at device scope (past any stale copy in this XCD's L2)
+    n = gridDim.x;
+    if (tid < 16) lm[tid] = (tid < n) ? (float)__hip_atomic_load(f.level1 + (size_t)tid * E, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT)
+                                      : INFINITY;
+    __syncthreads();
+    if (n <= 16) {
+      int base2 = 0;
+#pragma unroll
+      for (int w = 8; w >= 1; w >>= 1) {
+        PairScale p;
+        if (tid < w) {
+          p = pair_scale(lm[2 * tid], lm[2 * tid + 1], f.T);
+          lps[base2 + tid] = p;
+        }
+        __syncthreads();
+        if (tid < w) lm[tid] = p.m;
+        __syncthreads();
+        base2 += w;
+      }
+#ifdef MPPI_STAMPS
+      FIN_STAMP(6);
+#endif
+      for (int j = tid; j < E; j += FIN_THREADS) {
+        double v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          v[i] = __hip_atomic_load(f.level1 + (size_t)min(i, n - 1) * E + j, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        lnode[j] = group_apply<16>(lps, v, j);
+      }
+      n = 1;
+      __syncthreads();
+#ifdef MPPI_STAMPS
+      FIN_STAMP(1);
+#endif
+      goto root_ready;
+    }
+    __threadfence();  // more than 256 level-1 records: the general passes below read them plainly
+    cur = f.level1;
+  }
   while (n > FIN_LDS_NODES) {  // global -> global, aligned groups of 16 (4 tree levels)
     const int groups = (n + 15) >> 4;
     double* out = bufs[flip];
@@ -1841,12 +1945,12 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
       for (int it0 = tid; it0 < ng * E; it0 += 2 * FIN_THREADS) {
         double v[2][16];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int it = it0 + q * FIN_THREADS;
+        for (int q = 0; q < 2; ++q) {  // clamped, unconditional loads (empty members are skipped
+          const int it = min(it0 + q * FIN_THREADS, ng * E - 1);  // by their pair scales)
           const int gl = it / E, j = it - gl * E;
           const int r0 = 16 * (g0 + gl);
 #pragma unroll
-          for (int i = 0; i < 16; ++i) v[q][i] = (it < ng * E && r0 + i < n) ? cur[(size_t)(r0 + i) * E + j] : 0.0;
+          for (int i = 0; i < 16; ++i) v[q][i] = cur[(size_t)min(r0 + i, n - 1) * E + j];
         }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -1863,39 +1967,39 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
     n = groups;
     flip ^= 1;
   }
-  for (int it = tid; it < n * E; it += FIN_THREADS) lnode[it] = cur[it];
-  __syncthreads();
-  while (n > 1) {  // LDS levels
-    const int pairs = (n + 1) >> 1;
-    if (tid < pairs) {
-      const float ma = (float)lnode[(size_t)(2 * tid) * E];
-      const float mb = (2 * tid + 1 < n) ? (float)lnode[(size_t)(2 * tid + 1) * E] : INFINITY;
-      lps[tid] = pair_scale(ma, mb, f.T);
-    }
+  // the last <= 16 records: one aligned group of 16 (empty members padded) -> root in lnode[0..E)
+  if (n > 1) {
+    float* lm = reinterpret_cast<float*>(lps + 15);
+    if (tid < 16) lm[tid] = (tid < n) ? (float)cur[(size_t)tid * E] : INFINITY;
     __syncthreads();
-    double res[FIN_MAX_ITEMS];
+    int base = 0;
 #pragma unroll
-    for (int q = 0; q < FIN_MAX_ITEMS; ++q) {
-      const int it = tid + q * FIN_THREADS;
-      if (it < pairs * E) {
-        const int p = it / E, j = it - p * E;
-        const double va = lnode[(size_t)(2 * p) * E + j];
-        const double vb = (2 * p + 1 < n) ? lnode[(size_t)(2 * p + 1) * E + j] : 0.0;
-        res[q] = pair_apply(lps[p], va, vb, j);
+    for (int w = 8; w >= 1; w >>= 1) {
+      PairScale p;
+      if (tid < w) {
+        p = pair_scale(lm[2 * tid], lm[2 * tid + 1], f.T);
+        lps[base + tid] = p;
       }
+      __syncthreads();
+      if (tid < w) lm[tid] = p.m;
+      __syncthreads();
+      base += w;
     }
-    __syncthreads();
+    for (int j = tid; j < E; j += FIN_THREADS) {
+      double v[16];
 #pragma unroll
-    for (int q = 0; q < FIN_MAX_ITEMS; ++q) {
-      const int it = tid + q * FIN_THREADS;
-      if (it < pairs * E) lnode[it] = res[q];
+      for (int i = 0; i < 16; ++i) v[i] = cur[(size_t)min(i, n - 1) * E + j];
+      lnode[j] = group_apply<16>(lps, v, j);
     }
-    __syncthreads();
-    n = pairs;
+    n = 1;
+  } else {
+    for (int j = tid; j < n * E; j += FIN_THREADS) lnode[j] = cur[j];
   }
+  __syncthreads();
 #ifdef MPPI_STAMPS
   FIN_STAMP(1);
 #endif
+root_ready:
   // root = lnode[0..E) (n == 1) or empty (n == 0)
   if (f.mode == 0) {
     for (int j = tid; j < E; j += FIN_THREADS)
@@ -2251,11 +2355,11 @@ hipError_t launch_rollout_ws(const RolloutArgs& a, int blocks, size_t lds, hipSt
   return launch_ws_m<256, 2>(a, blocks, lds, st, mode, dump);
 }
 
-hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool use_lds) {
+hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool use_lds, int groups) {
   if (use_lds)
-    hipLaunchKernelGGL(mppi_finish_kernel<true>, dim3(1), dim3(FIN_THREADS), lds, st, f);
+    hipLaunchKernelGGL(mppi_finish_kernel<true>, dim3(groups), dim3(FIN_THREADS), lds, st, f);
   else
-    hipLaunchKernelGGL(mppi_finish_kernel<false>, dim3(1), dim3(FIN_THREADS), lds, st, f);
+    hipLaunchKernelGGL(mppi_finish_kernel<false>, dim3(groups), dim3(FIN_THREADS), lds, st, f);
   return hipGetLastError();
 }
 

@@ -43,7 +43,7 @@ def main():
     eng.set_costmap(cm, hw)
     eng.set_state(_lib.make_state(-60.0, -5.0, goal_x=65.0, goal_y=10.0))
     for i in range(5):
-        eng.step("3d", i)
+        eng.step("3d", i, copy=False)
     n = 64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8 + 16
     buf = (C.c_uint64 * n)()
     assert lib.mppi_debug_stamps(buf, n) == 0
@@ -68,17 +68,16 @@ def main():
     side = a[:, 4:].reshape(-1, 2) / phases
     lf = allv[64 * 16 * 6 + 1024 * 2: 64 * 16 * 6 + 1024 * 2 + 64 * 8].reshape(64, 8)[:nb]
     fs = allv[64 * 16 * 6 + 1024 * 2 + 64 * 8:][:16]
-    fd = np.diff(fs[:6])
-    print(f"  finish (mode 2): tree {fd[0]:.0f}  u_opt {fd[1]:.0f}  filter+sincos {fd[2]:.0f}  step0 {fd[3]:.0f}  "
-          f"signal {fd[4]:.0f} cyc")
-    if fs[6] > 0:  # fused tree: entry (latest block), per level: acquire -> combined
-        t = fs[6:12] - fs[6]
-        print(f"  fused tree (cyc after the last block entered): " +
-              "  ".join(f"L{k}: start {t[1 + 2 * k]:.0f} done {t[2 + 2 * k]:.0f}" for k in range(2)) +
-              f"  phase2 start {fs[2] - fs[6]:.0f}  end {fs[5] - fs[6]:.0f}")
-    print(f"  phase2: filter loop {fs[12] - fs[2]:.0f}  rest to step0-ready {fs[3] - fs[12]:.0f}  "
-          f"outputs {fs[4] - fs[3]:.0f} signal {fs[5] - fs[4]:.0f} cyc")
-    print(f"  leaf records: min+exp {(lf[:, 1] - lf[:, 0]).mean():.0f}  rows {(lf[:, 4] - lf[:, 1]).mean():.0f} cyc")
+    us = lambda a, b: (fs[b] - fs[a]) / 100.0  # s_memrealtime: 100 MHz, comparable across CUs
+    if fs[13] > 0:
+        print(f"  finish level1 (us): scales {us(0, 9):.1f}  apply+store {us(9, 10):.1f}  count {us(10, 13):.1f}; "
+              f"last group: scales {us(13, 6):.1f}  apply {us(6, 1):.1f}; phase2 prologue {us(1, 2):.1f}")
+        print(f"  previous finish signal -> this rollout's block 0 start: {us(14, 15):.1f} us")
+        print(f"  finish kernel (us): level1 {us(0, 13):.1f}  rest of tree {us(13, 1):.1f}  "
+              f"filter {us(2, 12):.1f}  v/w/sincos {us(12, 3):.1f}  outputs {us(3, 4):.1f}  signal {us(4, 5):.1f}")
+    else:
+        print(f"  finish kernel (us): tree {us(0, 1):.1f}  filter {us(2, 12):.1f}  v/w/sincos {us(12, 3):.1f}  "
+              f"outputs {us(3, 4):.1f}  signal {us(4, 5):.1f}")
     print(f"K={K} kernel={path}: cycles per step (mean over {nb} blocks)")
     print(f"  chain waves: work {chain[:, 0].mean():8.1f}  wait {chain[:, 1].mean():8.1f}")
     print(f"  side  waves: work {side[:, 0].mean():8.1f}  wait {side[:, 1].mean():8.1f}")
