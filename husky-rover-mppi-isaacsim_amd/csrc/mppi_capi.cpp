@@ -984,6 +984,8 @@ int mppi_set_stream(mppi_ctx* c, void* s) {
 static int check_grid(int32_t rows, int32_t cols, float res) {
   if (rows < 2 || cols < 2) return fail(MPPI_EINVAL, "DEM must be at least 2x2");
   if (!(res > 0.0f)) return fail(MPPI_EINVAL, "DEM resolution must be > 0");
+  if ((int64_t)rows * cols >= ((int64_t)1 << 29))  // kernels address cells with 32-bit byte offsets
+    return fail(MPPI_EINVAL, "DEM larger than 2^29 cells");
   return MPPI_OK;
 }
 
@@ -1319,7 +1321,7 @@ int mppi_sync(mppi_ctx* c) {
 
 int mppi_selftest(mppi_ctx* c, int32_t what, int64_t n, uint64_t seed, int64_t* mismatches) {
   if (!c || !mismatches) return fail(MPPI_EINVAL, "null argument");
-  if (what < 0 || what > 1 || n < 0) return fail(MPPI_EINVAL, "bad selftest arguments");
+  if (what < 0 || what > 3 || n < 0) return fail(MPPI_EINVAL, "bad selftest arguments");
   HIP_TRY(hipSetDevice(c->device));
   unsigned long long* d = nullptr;
   HIP_TRY(hipMalloc(&d, sizeof(*d)));

@@ -293,6 +293,135 @@ __device__ __forceinline__ void chain3d(const Dem<LDS>& dem, float res_half_neg,
   }
 }
 
+// ---------------------------------------------------------------------  lean chain
+// The pair kernel's chain wave issues about one VALU op per 4 cycles on its own,
+// so its step time is mostly instruction count.  chain3d_lean computes the same
+// values as chain3d<true> with fewer instructions:
+//  * range guards folded into running extrema instead of a compare-and-OR per
+//    operand: the smallest frexp exponent over the numerators (a zero numerator
+//    has exponent 0 and passes) and the min / max bit pattern of the squared
+//    norms (non-negative floats order like ints; +NaN and inf land above the
+//    upper bound, -NaN below the lower one);
+//  * divisor = a norm, so the quotient's sign is the numerator's: copysign
+//    replaces the zero-numerator select;
+//  * sqrt of a norm in [2^-80, 2^80] needs no denormal scaling or class fix-up:
+//    hardware sqrt (1 ulp) + the neighbour residual test (correctly rounded).
+// In range: numerators zero or |a| >= 2^-80, squared norms in [2^-80, 2^80] (so
+// divisors in [2^-40, 2^40] and every quotient / residual normal).  A lane out
+// of range redoes the step with chain3d<false> (IEEE), so results never depend
+// on the path; mppi_selftest (what 2, 3) checks the primitives bitwise.
+#ifndef MPPI_LEAN_CHAIN
+#define MPPI_LEAN_CHAIN 1  // diagnostic builds: 0 = chain3d<true> in the pair kernel
+#endif
+struct Lean {
+  int emin;      // min frexp exponent of the numerators
+  int nlo, nhi;  // min / max bit pattern of the squared norms
+};
+constexpr int kLeanEmin = -79;          // |a| >= 2^-80 <=> frexp exponent >= -79
+constexpr int kLeanNlo = 0x17800000;    // 2^-80
+constexpr int kLeanNhi = 0x67800000;    // 2^80
+__device__ __forceinline__ void lean_init(Lean& l) {
+  l.emin = 0;
+  l.nlo = kLeanNhi;
+  l.nhi = kLeanNlo;
+}
+__device__ __forceinline__ bool lean_bad(const Lean& l) {
+  return (l.emin < kLeanEmin) | (l.nlo < kLeanNlo) | (l.nhi > kLeanNhi);
+}
+// correctly rounded sqrt of a normal positive n (neighbour residual test)
+__device__ __forceinline__ float sqrt_cr(float n) {
+  const float s = __builtin_amdgcn_sqrtf(n);
+  const int si = __builtin_bit_cast(int, s);
+  const float sdn = __builtin_bit_cast(float, si - 1), sup = __builtin_bit_cast(float, si + 1);
+  const float rdn = __builtin_fmaf(-sdn, s, n);
+  const float rup = __builtin_fmaf(-sup, s, n);
+  float out = (rdn <= 0.0f) ? sdn : s;
+  return (rup > 0.0f) ? sup : out;
+}
+// 1 / sqrt(n) setup for the quotients a / sqrt(n) (IEEE: sqrt rounded, then each division)
+__device__ __forceinline__ Recip lean_norm(float n, Lean& l) {
+  const int nb = __builtin_bit_cast(int, n);
+  l.nlo = min(l.nlo, nb);
+  l.nhi = max(l.nhi, nb);
+  Recip r;
+  r.b = sqrt_cr(n);
+  const float y0 = __builtin_amdgcn_rcpf(r.b);
+  r.y = __builtin_fmaf(__builtin_fmaf(-r.b, y0, 1.0f), y0, y0);
+  return r;
+}
+__device__ __forceinline__ float lean_div(float a, const Recip& r, Lean& l) {
+  l.emin = min(l.emin, __builtin_amdgcn_frexp_expf(a));
+  const float q0 = a * r.y;
+  const float e0 = __builtin_fmaf(-r.b, q0, a);
+  const float q1 = __builtin_fmaf(e0, r.y, q0);
+  const float e1 = __builtin_fmaf(-r.b, q1, a);
+  const float q2 = __builtin_fmaf(e1, r.y, q1);
+  return __builtin_copysignf(q2, a);
+}
+
+// chain3d<true> with the lean guards (see above); DEM corners through 32-bit
+// offsets from the uniform base (rows * grid < 2^29, checked by mppi_set_dem).
+__device__ __forceinline__ float dem_at32(const float* Z, int off) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(Z) + (uint32_t)(off << 2));
+}
+__device__ __forceinline__ void chain3d_lean(const Dem<false>& dem, float res_half_neg, float res_sq,
+                                             float dt, float v, float sn, float cs, Traj& s, float (&q)[4],
+                                             float& nx, float& ny, float& nz, bool& bad) {
+  Lean l;
+  lean_init(l);
+  {  // _update_position :207-223
+    const Recip r = lean_norm((s.hx * s.hx + s.hy * s.hy) + s.hz * s.hz, l);
+    const float ux = lean_div(s.hx, r, l), uy = lean_div(s.hy, r, l);
+    s.x = s.x + (ux * v) * dt;
+    s.y = s.y + (uy * v) * dt;
+  }
+  {  // projection_warp.py:8-48
+    int i, j;
+    dem.template cell<true>(s.x, s.y, i, j, bad);
+    const int r0 = clampi(j, 0, dem.rows - 1), r1 = clampi(j + 1, 0, dem.rows - 1);
+    const int c0 = clampi(i, 0, dem.grid - 1), c1 = clampi(i + 1, 0, dem.grid - 1);
+    const int o0 = r0 * dem.grid, o1 = r1 * dem.grid;
+    q[0] = dem_at32(dem.Z, o0 + c0);
+    q[1] = dem_at32(dem.Z, o0 + c1);
+    q[2] = dem_at32(dem.Z, o1 + c0);
+    q[3] = dem_at32(dem.Z, o1 + c1);
+  }
+  {  // _normal_on_grid :129-151
+    const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
+    const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
+    const Recip r = lean_norm((vx * vx + vy * vy) + res_sq * res_sq, l);
+    nx = lean_div(vx, r, l);
+    ny = lean_div(vy, r, l);
+    nz = lean_div(res_sq, r, l);
+  }
+  float tx, ty, tz;
+  {  // _get_heading_tangent_vector :168-190
+    const float d = (s.hx * nx + s.hy * ny) + s.hz * nz;
+    tx = s.hx - d * nx;
+    ty = s.hy - d * ny;
+    tz = s.hz - d * nz;
+    const Recip r = lean_norm((tx * tx + ty * ty) + tz * tz, l);
+    tx = lean_div(tx, r, l);
+    ty = lean_div(ty, r, l);
+    tz = lean_div(tz, r, l);
+  }
+  {  // _update_orientation :225-248 (Rodrigues about n)
+    const Recip ro = lean_norm((tx * tx + ty * ty) + tz * tz, l);
+    const float ox = lean_div(tx, ro, l), oy = lean_div(ty, ro, l), oz = lean_div(tz, ro, l);
+    const float crx = ny * oz - nz * oy, cry = nz * ox - nx * oz, crz = nx * oy - ny * ox;
+    const float dn = (nx * ox + ny * oy) + nz * oz;
+    const float omc = 1.0f - cs;
+    const float rx = (ox * cs + crx * sn) + (nx * dn) * omc;
+    const float ry = (oy * cs + cry * sn) + (ny * dn) * omc;
+    const float rz = (oz * cs + crz * sn) + (nz * dn) * omc;
+    const Recip r = lean_norm((rx * rx + ry * ry) + rz * rz, l);
+    s.hx = lean_div(rx, r, l);
+    s.hy = lean_div(ry, r, l);
+    s.hz = lean_div(rz, r, l);
+  }
+  bad |= lean_bad(l);
+}
+
 // Height and wheel contacts of a rollout-step (projection_warp.py:318, :333-348),
 // right = offset * cross(normal, current_hv).
 template <bool F, bool LDS>
@@ -1376,8 +1505,12 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
         float nx, ny, nz;
         bool bad = false;
         const Traj saved = s;
+#if MPPI_LEAN_CHAIN
+        chain3d_lean(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+#else
         chain3d<kChainFast, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-        if (kChainFast && __builtin_expect(bad, 0)) {  // operand outside the fast range: IEEE redo
+#endif
+        if (__builtin_expect(bad, 0)) {  // operand outside the fast range: IEEE redo
           s = saved;
           chain3d<false, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
         }
@@ -2259,11 +2392,26 @@ __global__ __launch_bounds__(256) void mppi_selftest_kernel(int what, int64_t n,
       const float want = a / b;
       const float got = dv1<true>(a, b, flagged);
       if (!flagged && f_bits(want) != f_bits(got)) ++local;
-    } else {
+    } else if (what == 1) {
       const float x = fabsf(a);
       const float want = sqrtf(x);
       const float got = sq<true>(x, flagged);
       if (!flagged && f_bits(want) != f_bits(got)) ++local;
+    } else {  // 2, 3: lean normalisation (a, b, c) / sqrt(a^2 + b^2 + c^2) of chain3d_lean
+      const U4 r2 = philox4x32_10(U4{(uint32_t)i, (uint32_t)(i >> 32), 0x5e1fu, 0x1ea4u}, (uint32_t)seed,
+                                  (uint32_t)(seed >> 32));
+      // what 3: c dominant (exponent in [-30, 30)), a and b anywhere in [-50, 50]
+      const float c = (what == 3) ? bits_f((r2.x & 0x807FFFFFu) | ((127u - 30u + r2.y % 60u) << 23))
+                                  : mk(r2.x, r2.y);
+      const float n = (a * a + b * b) + c * c;
+      const float sr = sqrtf(n);
+      Lean l;
+      lean_init(l);
+      const Recip rr = lean_norm(n, l);
+      const float g0 = lean_div(a, rr, l), g1 = lean_div(b, rr, l), g2 = lean_div(c, rr, l);
+      if (!lean_bad(l) && (f_bits(rr.b) != f_bits(sr) || f_bits(g0) != f_bits(a / sr) ||
+                           f_bits(g1) != f_bits(b / sr) || f_bits(g2) != f_bits(c / sr)))
+        ++local;
     }
   }
   if (local) atomicAdd(bad_count, local);

@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmppi_hip.so")
+# MPPI_LIB_PATH: an alternative build of the same library (diagnostic A/B builds)
+LIB_PATH = os.environ.get("MPPI_LIB_PATH") or os.path.join(_HERE, "libmppi_hip.so")
 
 MPPI_OK = 0
 PROJ = {"2d": 2, "3d": 3, 2: 2, 3: 3}

@@ -104,7 +104,8 @@ int mppi_set_stream(mppi_ctx* ctx, void* hip_stream);
 
 /* self.Z_wp = wp.array(surface.Z.flatten()) (MPPI_isaac.py:460): copies the
  * row-major rows x cols DEM to the device.  x_min = y_min = -half_width and
- * resolution = 2*half_width/grid_size as in the launch args (:560-564). */
+ * resolution = 2*half_width/grid_size as in the launch args (:560-564).
+ * rows * cols < 2^29 (MPPI_EINVAL otherwise). */
 int mppi_set_dem(mppi_ctx* ctx, const float* z_host, int32_t rows, int32_t cols, float x_min,
                  float y_min, float resolution);
 
@@ -214,8 +215,10 @@ int mppi_sync(mppi_ctx* ctx);
 
 /* Device self-test of the engine's exact-arithmetic fast paths: what = 0 checks
  * the shared-reciprocal division against IEEE a/b, what = 1 the sqrt path
- * against IEEE sqrtf, on n random operands; *mismatches receives the count of
- * results that differ in any bit (0 expected). */
+ * against IEEE sqrtf, what = 2 / 3 the lean normalisation of the pair kernel's
+ * chain (sqrt of a squared norm and three quotients; 3 with one dominant
+ * component) against IEEE sqrtf and a/b, on n random operands; *mismatches
+ * receives the count of in-range results that differ in any bit (0 expected). */
 int mppi_selftest(mppi_ctx* ctx, int32_t what, int64_t n, uint64_t seed, int64_t* mismatches);
 
 #ifdef __cplusplus

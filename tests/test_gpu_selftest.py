@@ -6,7 +6,8 @@ import helpers as hp
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("what,name", [(0, "division"), (1, "sqrt")])
+@pytest.mark.parametrize("what,name", [(0, "division"), (1, "sqrt"), (2, "lean normalisation"),
+                                       (3, "lean normalisation, dominant component")])
 def test_fast_paths_bitwise(what, name):
     st = hp.oracle_state()
     Z, hw, cm = hp.c3_scene()
