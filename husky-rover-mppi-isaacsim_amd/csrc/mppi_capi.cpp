@@ -601,14 +601,15 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   if (pl.blocks == 0) return MPPI_OK;
   if (c->timing && !dump_args) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   if (c->trace) c->tr_mark[1] = now_us();
-  if (pl.pair)
+  if (pl.pair) {
     HIP_TRY(launch_rollout_pair(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr));
-  if (c->trace) c->tr_mark[2] = now_us();
-  else if (pl.ws)
+  } else if (pl.ws) {
     HIP_TRY(launch_rollout_ws(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr));
-  else
+  } else {
     HIP_TRY(launch_rollout(a, pl.block, pl.blocks, pl.lds_bytes, c->stream, pl.lds, proj, mode,
                            dump_args != nullptr));
+  }
+  if (c->trace) c->tr_mark[2] = now_us();
   if (c->timing && !dump_args) {
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     c->ev_roll_pending = true;
