@@ -267,7 +267,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "mppi_rollout_ws_kernel" if args.dem_path in ("auto", "ws") else "mppi_rollout_kernel",
+                "kernel": {"auto": "mppi_rollout_pair_kernel", "pair": "mppi_rollout_pair_kernel",
+                           "ws": "mppi_rollout_ws_kernel"}.get(args.dem_path, "mppi_rollout_kernel"),
                 "kernel_avg_ms": round(k_avg_ms, 5),
                 "algorithmic_bytes_per_launch": alg_bytes,
             },

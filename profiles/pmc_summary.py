@@ -15,7 +15,7 @@ from collections import defaultdict
 
 def short(name):
     name = name.strip('"')
-    for key in ("mppi_rollout_ws_kernel", "mppi_rollout_kernel", "mppi_finish_kernel", "mppi_bilinear_kernel"):
+    for key in ("mppi_rollout_pair_kernel", "mppi_rollout_ws_kernel", "mppi_noise_kernel", "mppi_tail_kernel", "mppi_rollout_kernel", "mppi_finish_kernel", "mppi_bilinear_kernel"):
         if key in name:
             return key
     return name.split("(")[0][:60]
@@ -38,9 +38,11 @@ def main(root):
             d["hbm_bytes_per_launch"] = d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]
         if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d and d["TCC_HIT_sum"] + d["TCC_MISS_sum"] > 0:
             d["l2_hit_rate"] = d["TCC_HIT_sum"] / (d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
-    roll = out.get("mppi_rollout_ws_kernel") or out.get("mppi_rollout_kernel", {})
+    roll = (out.get("mppi_rollout_pair_kernel") or out.get("mppi_rollout_ws_kernel")
+            or out.get("mppi_rollout_kernel", {}))
     summary = {"K": 65536, "H": 100, "kernels": out,
-               "hbm_bytes_per_launch": roll.get("hbm_bytes_per_launch")}
+               "hbm_bytes_per_launch": roll.get("hbm_bytes_per_launch"),
+               "kernel": next((k for k, v in out.items() if v is roll), None)}
     print(json.dumps(summary, indent=1))
 
 
