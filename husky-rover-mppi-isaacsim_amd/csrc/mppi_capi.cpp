@@ -264,7 +264,7 @@ Plan make_plan(const mppi_ctx* c) {
     const size_t scratch_ws = ((size_t)(TB + TB / 64) * 4 + 15) / 16 * 16 +
                               (size_t)(TB / 256) * (2 * H + 2) * sizeof(double);
     pl.lds_bytes = pl.pair ? (size_t)(6 * PAIR_RING + 1) * TB * sizeof(float) + 4 * (TB / 64) * sizeof(int) +
-                                 scratch_ws
+                                 (size_t)((2 * H + 3) & ~3) * sizeof(float) + scratch_ws
                            : (size_t)15 * TB * sizeof(float) + scratch_ws;
   }
   // finish kernel: tree phase [16][2H+2] doubles + 64 x (15 PairScale + 16 m); phase 2

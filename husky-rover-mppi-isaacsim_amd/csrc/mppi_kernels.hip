@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <stdint.h>
 
 #include "mppi_detmath.h"
@@ -1387,15 +1388,26 @@ __device__ __forceinline__ void noise_ahead(const RolloutArgs& a, unsigned char*
 //                  consume p-L (needs chained > p - L)           -> consumed = p - L + 1
 // with L = PAIR_LAG; deadlock-free for 0 < L < D (the chain's waits are always
 // satisfied by side iterations that do not wait on it).  Bitwise identical results.
-constexpr int PAIR_D = 8;
-constexpr int PAIR_LAG = 4;
+#ifndef MPPI_PAIR_LAG
+#define MPPI_PAIR_LAG 4
+#endif
+constexpr int PAIR_D = MPPI_PAIR_D;
+constexpr int PAIR_LAG = MPPI_PAIR_LAG;
 static_assert(PAIR_LAG > 0 && PAIR_LAG < PAIR_D, "ring depth must exceed the consume lag");
+static_assert(PAIR_LAG % 2 == 0, "the side loop pairs even and odd steps");
 
+// The flags and the rings are LDS, so the acquire / release fences are restricted to
+// the local address space: a plain workgroup-scope release also orders the wave's
+// global loads (s_waitcnt vmcnt(0) before every flag store), which would drain the
+// side wave's prefetches (normals, costmap, wheel heights) at every publication.
 __device__ __forceinline__ int lds_load_acquire(const int* f) {
-  return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  return v;
 }
 __device__ __forceinline__ void lds_store_release(int* f, int v) {
-  __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 template <int TB, int PROJ, int MODE, bool DUMP>
@@ -1408,7 +1420,8 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   float* ring_out = ring_in + D * 2 * TB;                // [D][4][TB]: x, y, cx, cy
   float* cost_lds = ring_out + D * 4 * TB;               // [TB]
   int* flags = reinterpret_cast<int*>(cost_lds + TB);    // [4][NWC]: produced, chained, consumed, -
-  unsigned char* scratch = reinterpret_cast<unsigned char*>(flags + 4 * NWC);
+  float* unom_lds = reinterpret_cast<float*>(flags + 4 * NWC);  // [2H] u_nom1 | u_nom2 (padded to 4)
+  unsigned char* scratch = reinterpret_cast<unsigned char*>(unom_lds + ((2 * a.H + 3) & ~3));
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool side = wave >= NWC;
@@ -1438,6 +1451,11 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   const float res_sq = a.res * a.res;
   bool nobad = false;
   if (tid < 4 * NWC) flags[tid] = 0;
+  // the nominal sequence in LDS: the side wave reads one element per step, and a vector
+  // load there would make every wait for it (vmcnt is in order) also wait for the normals
+  // prefetched just before it
+  if constexpr (MODE == 0)
+    for (int i = tid; i < 2 * H; i += NT) unom_lds[i] = i < H ? a.u_nom1[i] : a.u_nom2[i - H];
 
   // ---------------- per-role state
   Traj s;                       // chain
@@ -1453,7 +1471,6 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   }
   float pf_sum = 0.f, sw = 0.f, sp = 0.f, ob = 0.f, last_x = a.x0, last_y = a.y0;
   float lwx = 0.f, lwy = 0.f, lwz = 0.f, rwx = 0.f, rwy = 0.f, rwz = 0.f;
-  float cm_pend = 0.f;
   float* ust = a.ustore + (size_t)blockIdx.x * (2 * H) * TB + tj;
 
   if (!side) {  // initial projection at the robot pose (projection_warp.py:306-310)
@@ -1538,18 +1555,33 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
     }
   } else {
     // ---------------- side wave: produce step p, consume step p - PAIR_LAG
-    for (int p = 0; p < H + PAIR_LAG; ++p) {
+    // Unrolled by two (even / odd steps, PAIR_LAG even so both have the same parity)
+    // so that every value loaded for a later half stays in its own registers: a
+    // loop-carried copy of a load in flight makes the compiler wait for it (vmcnt(0))
+    // at the back edge, and vmcnt is in order, so the normals prefetched for the next
+    // step would also be waited for at the first wheel-height wait.  Loads:
+    //  * normals of step p + 2 into the registers that served step p, after its consume;
+    //  * costmap value of step sc, used (obstacle critic) in the other half;
+    //  * wheel heights of the EVEN steps only (the slope critic, critics_warp.py:220-267,
+    //    reads lw/rw at i, i+2 for even i; odd-step contacts are computed only for
+    //    DUMP), used one half later.
+    float eA1 = en1, eA2 = en2, eB1 = 0.f, eB2 = 0.f;  // normals of the even / odd step
+    if constexpr (MODE == 0) {
+      const int t1 = min(1, H - 1);
+      eB1 = eps_row[(size_t)t1 * TB];
+      eB2 = eps_row[(size_t)(H + t1) * TB];
+    }
+    float cmA = 0.f, cmB = 0.f;                        // costmap value of the even / odd step
+    float elx = 0.f, ely = 0.f, elz = 0.f, erx = 0.f, ery = 0.f, erz = 0.f;  // even step's contacts
+    auto half = [&](auto odd_tag, int p, float& e1r, float& e2r, float& cm_mine, float& cm_prev)
+                    __attribute__((always_inline)) {
+      constexpr bool ODD = decltype(odd_tag)::value;
       if (p < H) {  // sampling, filter (sampling_warp.py:54-138); normals precomputed
         float u1, u2;
         if constexpr (MODE == 0) {
-          const float e1 = en1, e2 = en2;
-          if (p + 1 < H) {  // prefetch the next step's normals
-            en1 = eps_row[(size_t)(p + 1) * TB];
-            en2 = eps_row[(size_t)(H + p + 1) * TB];
-          }
           const int ti = min(p + 1, H - 1);
-          u1 = clampf(a.u_nom1[ti] + a.s1 * e1, a.min_u1, a.max_u1);
-          u2 = clampf(a.u_nom2[ti] + a.s2 * e2, a.min_u2, a.max_u2);
+          u1 = clampf(unom_lds[ti] + a.s1 * e1r, a.min_u1, a.max_u1);
+          u2 = clampf(unom_lds[H + ti] + a.s2 * e2r, a.min_u2, a.max_u2);
         } else {
           const size_t o = (size_t)(valid ? kl : 0) * H + p;
           u1 = a.inj_u1[o];
@@ -1581,37 +1613,49 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
         const float* ro = ring_out + (sc % D) * 4 * TB + tj;
         const float x = ro[0], y = ro[TB], cx = ro[2 * TB], cy = ro[3 * TB];
         const float vq = ring_in[(sc % D) * 2 * TB + tj];  // v of step sc (slot not reused yet)
-        float lx = 0.f, ly = 0.f, lz = 0.f, rx = 0.f, ry = 0.f, rz = 0.f;
-        if constexpr (PROJ == 3) {
-          lx = x + cx;
-          ly = y + cy;
-          lz = dem.template point<false>(lx, ly, nobad);
-          rx = x - cx;
-          ry = y - cy;
-          rz = dem.template point<false>(rx, ry, nobad);
+        if constexpr (!ODD) {  // contacts of an even step: heights in flight until the odd half
+          if constexpr (PROJ == 3) {
+            elx = x + cx;
+            ely = y + cy;
+            elz = dem.template point<false>(elx, ely, nobad);
+            erx = x - cx;
+            ery = y - cy;
+            erz = dem.template point<false>(erx, ery, nobad);
+          }
         }
         Recip rcm;
         rcm.b = a.res_c;
-        const float cm_now =
-            a.cm[costmap_index<false>(a.cm_size, a.hw, rcm, x, y, nobad, a.rinv_res_c, a.cdiv_res_c)];
+        cm_mine = a.cm[costmap_index<false>(a.cm_size, a.hw, rcm, x, y, nobad, a.rinv_res_c, a.cdiv_res_c)];
         const float pft = pf_sum + 10.0f * (fabsf(x - a.gx) + fabsf(y - a.gy));
         pf_sum = (sc < H - 1) ? pft : pf_sum;   // _path_follow_critic sum over t < H-1
         last_x = x;
         last_y = y;
-        if ((sc & 1) == 0) {  // _avoid_slope_wheels terms (i, i+2), even i < H-3
-          const float term = slope_term<false>(lwx, lwy, lwz, lx, ly, lz, rwx, rwy, rwz, rx, ry, rz, nobad);
-          sw = (sc >= 2 && sc - 2 < H - 3) ? sw + term : sw;
-          lwx = lx; lwy = ly; lwz = lz;
-          rwx = rx; rwy = ry; rwz = rz;
+        if constexpr (ODD) {  // _avoid_slope_wheels term (i, i+2) of the even step i = sc - 1 < H-3
+          const int se = sc - 1;
+          const float term = slope_term<false>(lwx, lwy, lwz, elx, ely, elz, rwx, rwy, rwz, erx, ery, erz, nobad);
+          sw = (se >= 2 && se - 2 < H - 3) ? sw + term : sw;
+          lwx = elx; lwy = ely; lwz = elz;
+          rwx = erx; rwy = ery; rwz = erz;
         }
         const float spt = sp + (a.vmax - vq) / (vq + 0.0001f);  // _maximise_speed
         sp = a.speed_on ? spt : sp;
-        // _avoid_obstacle: the costmap value gathered in the previous consume
-        const float ob1 = (cm_pend > a.thr) ? ob + a.pen : ob;
-        ob = (sc > 0) ? ob1 + cm_pend : ob;
-        cm_pend = cm_now;
+        // _avoid_obstacle: the costmap value gathered in the other half (step sc - 1)
+        const float ob1 = (cm_prev > a.thr) ? ob + a.pen : ob;
+        ob = (sc > 0) ? ob1 + cm_prev : ob;
         if constexpr (DUMP) {
           if (valid) {
+            float lx = elx, ly = ely, lz = elz, rx = erx, ry = ery, rz = erz;
+            if (ODD) {
+              lx = ly = lz = rx = ry = rz = 0.f;
+              if constexpr (PROJ == 3) {
+                lx = x + cx;
+                ly = y + cy;
+                lz = dem.template point<false>(lx, ly, nobad);
+                rx = x - cx;
+                ry = y - cy;
+                rz = dem.template point<false>(rx, ry, nobad);
+              }
+            }
             const size_t o3 = ((size_t)kl * H + sc) * 3;
             if (a.d_lw) { a.d_lw[o3] = lx; a.d_lw[o3 + 1] = ly; a.d_lw[o3 + 2] = lz; }
             if (a.d_rw) { a.d_rw[o3] = rx; a.d_rw[o3 + 1] = ry; a.d_rw[o3 + 2] = rz; }
@@ -1621,9 +1665,19 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
         }
         lds_store_release(f_cons, sc + 1);
       }
+      if constexpr (MODE == 0) {  // prefetch the normals of step p + 2 into the registers just freed
+        const int tn = min(p + 2, H - 1);
+        e1r = eps_row[(size_t)tn * TB];
+        e2r = eps_row[(size_t)(H + tn) * TB];
+      }
+    };
+    for (int p = 0; p < H + PAIR_LAG; p += 2) {
+      half(std::false_type{}, p, eA1, eA2, cmA, cmB);
+      if (p + 1 < H + PAIR_LAG) half(std::true_type{}, p + 1, eB1, eB2, cmB, cmA);
     }
-    if (cm_pend > a.thr) ob = ob + a.pen;  // last step's obstacle term
-    ob = ob + cm_pend;
+    const float cm_last = ((H - 1) & 1) ? cmB : cmA;
+    if (cm_last > a.thr) ob = ob + a.pen;  // last step's obstacle term
+    ob = ob + cm_last;
     // _evaluate_trajectories_kernel (critics_warp.py:325-329)
     float pf;
     if (a.pf_far) {
@@ -1764,7 +1818,10 @@ __device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem<L
       const Traj saved = s;
       float q[4], nx, ny, nz;
       bool bad = false;
-      chain3d<kChainFast, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+      if constexpr (!LDS && MPPI_LEAN_CHAIN)  // the rollout chain's arithmetic (bitwise equal)
+        chain3d_lean(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+      else
+        chain3d<kChainFast, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
       if (kChainFast && __builtin_expect(bad, 0)) {
         s = saved;
         chain3d<false, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
@@ -2521,30 +2578,37 @@ hipError_t launch_tail(const FinishArgs& f, hipStream_t st) {
 // DEFINED D1), precomputed so the rollout's side waves only load them: thread =
 // (block, Philox block n = t/2, trajectory); writes eps1/eps2 of steps t, t+1.
 __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t n_base, int64_t k_offset,
-                                                         int H, float* __restrict__ eps) {
+                                                         int H, int n_blocks, float* __restrict__ eps) {
   const int tj = threadIdx.x;
   const int NB = (H + 1) >> 1;
-  const int n = blockIdx.x % NB;
-  const int blk = blockIdx.x / NB;
-  const uint64_t kg = (uint64_t)(k_offset + (int64_t)blk * 256 + tj);
-  float a1, a2, b1, b2;
-  noise_block(seed, n_base + (uint64_t)n, kg, &a1, &a2, &b1, &b2);
-  const int t = 2 * n;
-  float* e1 = eps + ((size_t)blk * 2 * H + t) * 256 + tj;
-  float* e2 = e1 + (size_t)H * 256;
-  e1[0] = a1;
-  e2[0] = a2;
-  if (t + 1 < H) {
-    e1[256] = b1;
-    e2[256] = b2;
+  for (int64_t g = blockIdx.x; g < (int64_t)n_blocks * NB; g += gridDim.x) {
+    const int n = (int)(g % NB);
+    const int64_t blk = g / NB;
+    const uint64_t kg = (uint64_t)(k_offset + blk * 256 + tj);
+    float a1, a2, b1, b2;
+    noise_block(seed, n_base + (uint64_t)n, kg, &a1, &a2, &b1, &b2);
+    const int t = 2 * n;
+    float* e1 = eps + ((size_t)blk * 2 * H + t) * 256 + tj;
+    float* e2 = e1 + (size_t)H * 256;
+    e1[0] = a1;
+    e2[0] = a2;
+    if (t + 1 < H) {
+      e1[256] = b1;
+      e2[256] = b2;
+    }
   }
 }
 
+constexpr int64_t kNoiseMaxGroups = 4 * 256;
 hipError_t launch_noise(uint64_t seed, uint64_t n_base, int64_t k_offset, int blocks, int H, float* eps,
                         hipStream_t st) {
+  // Grid capped at 4 workgroups (16 waves) per CU: the noise of step i+1 is generated
+  // while the finish of step i runs, and a full-size grid fills every wave slot ahead of
+  // the finish's one 16-wave workgroup, which then waits for the whole noise kernel.
   const int NB = (H + 1) >> 1;
-  hipLaunchKernelGGL(mppi_noise_kernel, dim3((unsigned)(blocks * NB)), dim3(256), 0, st, seed, n_base,
-                     k_offset, H, eps);
+  const int64_t total = (int64_t)blocks * NB;
+  const unsigned grid = (unsigned)std::min<int64_t>(total, kNoiseMaxGroups);
+  hipLaunchKernelGGL(mppi_noise_kernel, dim3(grid), dim3(256), 0, st, seed, n_base, k_offset, H, blocks, eps);
   return hipGetLastError();
 }
 
