@@ -59,6 +59,8 @@ struct mppi_ctx {
   // DEM
   float* Z = nullptr;
   bool Z_owned = false;
+  float4* ntab = nullptr;  // per-cell normals of the DEM, (rows+1) x (cols+1) (mppi_normal_table_kernel)
+  size_t ntab_cap = 0;
   size_t Z_cap = 0;
   int rows = 0, cols = 0;
   float x_min = 0, y_min = 0, res = 0;
@@ -320,6 +322,7 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   a.k_offset = p.k_offset;
   a.H = H;
   a.Z = c->Z;
+  a.ntab = c->ntab;
   a.rows = c->rows;
   a.grid = c->cols;
   a.x_min = c->x_min;
@@ -399,6 +402,7 @@ void fill_finish(const mppi_ctx* c, const Plan& pl, const mppi_state& st, Finish
   f.u_nom_next = c->u_nom[c->cur ^ 1];
   f.out = c->stage;
   f.Z = c->Z;
+  f.ntab = c->ntab;
   f.rows = c->rows;
   f.grid = c->cols;
   f.x_min = c->x_min;
@@ -922,6 +926,7 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->tail_stream) hipStreamSynchronize(c->tail_stream);
   if (c->noise_stream) hipStreamSynchronize(c->noise_stream);
   if (c->Z_owned && c->Z) hipFree(c->Z);
+  if (c->ntab) hipFree(c->ntab);
   if (c->cm) hipFree(c->cm);
   for (float* u : c->u_nom)
     if (u) hipFree(u);
@@ -990,6 +995,23 @@ static int check_grid(int32_t rows, int32_t cols, float res) {
   return MPPI_OK;
 }
 
+// The DEM's per-cell normal table (read by the rollout chain instead of four corners +
+// a normalisation per step); rebuilt whenever the DEM is set.  Ends synchronised.
+static int build_normal_table(mppi_ctx* c) {
+  const size_t bytes = ((size_t)c->rows + 1) * ((size_t)c->cols + 1) * sizeof(float4);
+  if (bytes > c->ntab_cap) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->ntab) HIP_TRY(hipFree(c->ntab));
+    c->ntab = nullptr;
+    c->ntab_cap = 0;
+    HIP_TRY(hipMalloc(&c->ntab, bytes));
+    c->ntab_cap = bytes;
+  }
+  HIP_TRY(launch_normal_table(c->Z, c->rows, c->cols, c->res, c->ntab, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MPPI_OK;
+}
+
 int mppi_set_dem(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float x_min, float y_min,
                  float resolution) {
   if (!c || !z) return fail(MPPI_EINVAL, "null argument");
@@ -1014,6 +1036,8 @@ int mppi_set_dem(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float 
   c->x_min = x_min;
   c->y_min = y_min;
   c->res = resolution;
+  rc = build_normal_table(c);
+  if (rc) return rc;
   return verified_reciprocal(c, resolution, &c->rinv_res);
 }
 
@@ -1035,6 +1059,8 @@ int mppi_set_dem_device(mppi_ctx* c, const float* z, int32_t rows, int32_t cols,
   c->x_min = x_min;
   c->y_min = y_min;
   c->res = resolution;
+  rc = build_normal_table(c);
+  if (rc) return rc;
   return verified_reciprocal(c, resolution, &c->rinv_res);
 }
 

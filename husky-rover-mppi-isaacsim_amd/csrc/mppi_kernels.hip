@@ -138,6 +138,7 @@ struct Dem {
   Recip rres;  // fast-path reciprocal of res (res is validated on the host)
   float rinv;  // verified reciprocal for cdiv_f (cdiv != 0)
   int cdiv;
+  const float4* N = nullptr;  // per-cell normals (normal_cell), global path only
 
   __device__ __forceinline__ void init(const float* Z_, const float* win_, int rows_, int grid_,
                                        int wx0_, int wy0_, int W_, int Wr_, float x_min_,
@@ -208,6 +209,13 @@ struct Dem {
       q[2] = Z[(size_t)r1 * grid + c0];
       q[3] = Z[(size_t)r1 * grid + c1];
     }
+  }
+  // normal of the cell (i, j) from the table: i in [-1, grid], j in [-1, rows] as cell()
+  // returns them; i = grid selects the same corners as i = grid - 1 (both clamp to the last
+  // column), so the table has (rows + 1) x (grid + 1) entries
+  __device__ __forceinline__ float4 normal_cell(int i, int j) const {
+    const int ii = min(i, grid - 1) + 1, jj = min(j, rows - 1) + 1;
+    return N[(uint32_t)(jj * (grid + 1) + ii)];
   }
   template <bool F>
   __device__ __forceinline__ float point(float x, float y, bool& bad) const {
@@ -365,6 +373,9 @@ __device__ __forceinline__ float lean_div(float a, const Recip& r, Lean& l) {
 __device__ __forceinline__ float dem_at32(const float* Z, int off) {
   return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(Z) + (uint32_t)(off << 2));
 }
+// NTAB: the normal comes from the per-cell table (dem.N, the IEEE normal of the same
+// four corners) and q is not filled in.
+template <bool NTAB = false>
 __device__ __forceinline__ void chain3d_lean(const Dem<false>& dem, float res_half_neg, float res_sq,
                                              float dt, float v, float sn, float cs, Traj& s, float (&q)[4],
                                              float& nx, float& ny, float& nz, bool& bad) {
@@ -376,24 +387,33 @@ __device__ __forceinline__ void chain3d_lean(const Dem<false>& dem, float res_ha
     s.x = s.x + (ux * v) * dt;
     s.y = s.y + (uy * v) * dt;
   }
-  {  // projection_warp.py:8-48
+  if constexpr (NTAB) {  // projection_warp.py:8-48 + _normal_on_grid :129-151 (per-cell table)
     int i, j;
     dem.template cell<true>(s.x, s.y, i, j, bad);
-    const int r0 = clampi(j, 0, dem.rows - 1), r1 = clampi(j + 1, 0, dem.rows - 1);
-    const int c0 = clampi(i, 0, dem.grid - 1), c1 = clampi(i + 1, 0, dem.grid - 1);
-    const int o0 = r0 * dem.grid, o1 = r1 * dem.grid;
-    q[0] = dem_at32(dem.Z, o0 + c0);
-    q[1] = dem_at32(dem.Z, o0 + c1);
-    q[2] = dem_at32(dem.Z, o1 + c0);
-    q[3] = dem_at32(dem.Z, o1 + c1);
-  }
-  {  // _normal_on_grid :129-151
-    const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
-    const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
-    const Recip r = lean_norm((vx * vx + vy * vy) + res_sq * res_sq, l);
-    nx = lean_div(vx, r, l);
-    ny = lean_div(vy, r, l);
-    nz = lean_div(res_sq, r, l);
+    const float4 nv = dem.normal_cell(i, j);
+    nx = nv.x;
+    ny = nv.y;
+    nz = nv.z;
+  } else {
+    {  // projection_warp.py:8-48
+      int i, j;
+      dem.template cell<true>(s.x, s.y, i, j, bad);
+      const int r0 = clampi(j, 0, dem.rows - 1), r1 = clampi(j + 1, 0, dem.rows - 1);
+      const int c0 = clampi(i, 0, dem.grid - 1), c1 = clampi(i + 1, 0, dem.grid - 1);
+      const int o0 = r0 * dem.grid, o1 = r1 * dem.grid;
+      q[0] = dem_at32(dem.Z, o0 + c0);
+      q[1] = dem_at32(dem.Z, o0 + c1);
+      q[2] = dem_at32(dem.Z, o1 + c0);
+      q[3] = dem_at32(dem.Z, o1 + c1);
+    }
+    {  // _normal_on_grid :129-151
+      const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
+      const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
+      const Recip r = lean_norm((vx * vx + vy * vy) + res_sq * res_sq, l);
+      nx = lean_div(vx, r, l);
+      ny = lean_div(vy, r, l);
+      nz = lean_div(res_sq, r, l);
+    }
   }
   float tx, ty, tz;
   {  // _get_heading_tangent_vector :168-190
@@ -1447,6 +1467,7 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   const int H = a.H;
   Dem<false> dem;
   dem.init(a.Z, nullptr, a.rows, a.grid, 0, 0, 1, 1, a.x_min, a.y_min, a.res, a.rinv_res, a.cdiv_res);
+  dem.N = a.ntab;
   const float res_half_neg = (-a.res) / 2.0f;
   const float res_sq = a.res * a.res;
   bool nobad = false;
@@ -1523,7 +1544,8 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
         bool bad = false;
         const Traj saved = s;
 #if MPPI_LEAN_CHAIN
-        chain3d_lean(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+        chain3d_lean<true>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+        if constexpr (DUMP) dem.template corners<false>(s.x, s.y, q, nobad);  // heights: dump only
 #else
         chain3d<kChainFast, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
 #endif
@@ -1573,10 +1595,15 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
     }
     float cmA = 0.f, cmB = 0.f;                        // costmap value of the even / odd step
     float elx = 0.f, ely = 0.f, elz = 0.f, erx = 0.f, ery = 0.f, erz = 0.f;  // even step's contacts
-    auto half = [&](auto odd_tag, int p, float& e1r, float& e2r, float& cm_mine, float& cm_prev)
-                    __attribute__((always_inline)) {
+    // PROD / CONS: the half produces step p / consumes step sc = p - PAIR_LAG for sure
+    // (no runtime test: branch-free loads let the compiler count vmcnt exactly); with
+    // neither set, both are tested at run time (the few halves at the ends).
+    auto half = [&](auto odd_tag, auto prod_tag, auto cons_tag, int p, float& e1r, float& e2r,
+                    float& cm_mine, float& cm_prev) __attribute__((always_inline)) {
       constexpr bool ODD = decltype(odd_tag)::value;
-      if (p < H) {  // sampling, filter (sampling_warp.py:54-138); normals precomputed
+      constexpr bool PROD = decltype(prod_tag)::value, CONS = decltype(cons_tag)::value;
+      constexpr bool GUARD = !PROD && !CONS;
+      if (PROD || (GUARD && p < H)) {  // sampling, filter (sampling_warp.py:54-138); normals precomputed
         float u1, u2;
         if constexpr (MODE == 0) {
           const int ti = min(p + 1, H - 1);
@@ -1608,7 +1635,7 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
         lds_store_release(f_prod, p + 1);
       }
       const int sc = p - PAIR_LAG;
-      if (sc >= 0) {  // wheel contacts + critics of step sc (projection_warp.py:333-348, critics_warp.py)
+      if (CONS || (GUARD && sc >= 0 && sc < H)) {  // contacts + critics of step sc (projection_warp.py:333-348)
         wait_ge(f_chain, sc + 1);
         const float* ro = ring_out + (sc % D) * 4 * TB + tj;
         const float x = ro[0], y = ro[TB], cx = ro[2 * TB], cy = ro[3 * TB];
@@ -1671,9 +1698,22 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
         e2r = eps_row[(size_t)(H + tn) * TB];
       }
     };
-    for (int p = 0; p < H + PAIR_LAG; p += 2) {
-      half(std::false_type{}, p, eA1, eA2, cmA, cmB);
-      if (p + 1 < H + PAIR_LAG) half(std::true_type{}, p + 1, eB1, eB2, cmB, cmA);
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    int p = 0;
+    for (const int p1 = min(H, PAIR_LAG) & ~1; p < p1; p += 2) {  // produce only
+      half(F_{}, T_{}, F_{}, p, eA1, eA2, cmA, cmB);
+      half(T_{}, T_{}, F_{}, p + 1, eB1, eB2, cmB, cmA);
+    }
+    if (p == PAIR_LAG) {  // steady state: produce p, consume p - PAIR_LAG
+      for (; p + 1 < H; p += 2) {
+        half(F_{}, T_{}, T_{}, p, eA1, eA2, cmA, cmB);
+        half(T_{}, T_{}, T_{}, p + 1, eB1, eB2, cmB, cmA);
+      }
+    }
+    for (; p < H + PAIR_LAG; p += 2) {  // the ends, tested per half
+      half(F_{}, F_{}, F_{}, p, eA1, eA2, cmA, cmB);
+      if (p + 1 < H + PAIR_LAG) half(T_{}, F_{}, F_{}, p + 1, eB1, eB2, cmB, cmA);
     }
     const float cm_last = ((H - 1) & 1) ? cmB : cmA;
     if (cm_last > a.thr) ob = ob + a.pen;  // last step's obstacle term
@@ -1819,7 +1859,7 @@ __device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem<L
       float q[4], nx, ny, nz;
       bool bad = false;
       if constexpr (!LDS && MPPI_LEAN_CHAIN)  // the rollout chain's arithmetic (bitwise equal)
-        chain3d_lean(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+        chain3d_lean<true>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
       else
         chain3d<kChainFast, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
       if (kChainFast && __builtin_expect(bad, 0)) {
@@ -1836,7 +1876,11 @@ __device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem<L
   __syncthreads();
   for (int t = tid; t < nsteps; t += nthreads) {  // heights + wheel contacts, all lanes
     const float* ch = chain + 12 * t;
-    const float q[4] = {ch[2], ch[3], ch[4], ch[5]};
+    float q[4] = {ch[2], ch[3], ch[4], ch[5]};
+    if constexpr (!LDS && MPPI_LEAN_CHAIN) {  // the chain read the normal table: corners here
+      bool unused = false;
+      dem.template corners<false>(ch[0], ch[1], q, unused);
+    }
     StepOut o;
     bool bad = false;
     wheels3d<kFastMath, LDS>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
@@ -1908,6 +1952,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
 #endif
   Dem<LDS> dem;
   dem.init(f.Z, win, f.rows, f.grid, f.wx0, f.wy0, f.W, f.Wr, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
+  dem.N = f.ntab;
   const int lane = tid & 63, wave = tid >> 6;
   if (wave == 0) {
     // the recurrence on every lane of wave 0 (identical values), inputs read 8 at a time
@@ -2219,6 +2264,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void mppi_tail_kernel(const FinishArg
   __syncthreads();
   Dem<false> dem;
   dem.init(f.Z, nullptr, f.rows, f.grid, 0, 0, 1, 1, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
+  dem.N = f.ntab;
   optimal_rollout<false>(f, dem, vb, snb, csb, chain, H, f.tail_out, tid, TAIL_THREADS);
 }
 
@@ -2571,6 +2617,40 @@ hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool u
 hipError_t launch_tail(const FinishArgs& f, hipStream_t st) {
   const size_t lds = (size_t)15 * f.H * sizeof(float);
   hipLaunchKernelGGL(mppi_tail_kernel, dim3(1), dim3(TAIL_THREADS), lds, st, f);
+  return hipGetLastError();
+}
+
+// Per-cell surface normals (projection_warp.py:129-151 `_normal_on_grid` on the four
+// corners that projection_warp.py:8-48 selects for a cell), built once per DEM: entry
+// (j + 1, i + 1) for the cell indices i in [-1, grid - 1], j in [-1, rows - 1] that
+// Dem::cell produces (i = grid and j = rows select the same clamped corners as grid - 1
+// and rows - 1).  IEEE float operations in the reference order, i.e. exactly the normal
+// the rollout chain computed per step before (chain3d<false> / chain3d_lean agree on
+// it bit for bit), so reading it from the table changes no result.
+__global__ __launch_bounds__(256) void mppi_normal_table_kernel(const float* __restrict__ Z, int rows, int grid,
+                                                                float res, float4* __restrict__ out) {
+  const int64_t cols = (int64_t)grid + 1;
+  const int64_t n = ((int64_t)rows + 1) * cols;
+  const float res_half_neg = (-res) / 2.0f;
+  const float res_sq = res * res;
+  for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < n; g += (int64_t)gridDim.x * 256) {
+    const int j = (int)(g / cols) - 1, i = (int)(g % cols) - 1;
+    const int r0 = clampi(j, 0, rows - 1), r1 = clampi(j + 1, 0, rows - 1);
+    const int c0 = clampi(i, 0, grid - 1), c1 = clampi(i + 1, 0, grid - 1);
+    const float q0 = Z[(size_t)r0 * grid + c0], q1 = Z[(size_t)r0 * grid + c1];
+    const float q2 = Z[(size_t)r1 * grid + c0], q3 = Z[(size_t)r1 * grid + c1];
+    bool unused = false;
+    const float vx = res_half_neg * (((q1 - q0) - q2) + q3);
+    const float vy = res_half_neg * (((q2 - q0) - q1) + q3);
+    const Recip r = rc<false>(sq<false>((vx * vx + vy * vy) + res_sq * res_sq, unused), unused);
+    out[g] = make_float4(dv<false>(vx, r, unused), dv<false>(vy, r, unused), dv<false>(res_sq, r, unused), 0.0f);
+  }
+}
+
+hipError_t launch_normal_table(const float* Z, int rows, int grid, float res, float4* out, hipStream_t st) {
+  const int64_t n = ((int64_t)rows + 1) * ((int64_t)grid + 1);
+  const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(mppi_normal_table_kernel, dim3(blocks), dim3(256), 0, st, Z, rows, grid, res, out);
   return hipGetLastError();
 }
 

@@ -111,7 +111,8 @@ int mppi_set_dem(mppi_ctx* ctx, const float* z_host, int32_t rows, int32_t cols,
 
 /* controller.Z_wp = DEM_warp rebinding (visual_terrain_stack_full_terrain.py:567):
  * binds a DEM already resident in device memory (zero copy; the caller keeps
- * it alive and unchanged while steps run). */
+ * it alive and unchanged while steps run: the per-cell normal table the rollout
+ * reads is derived from it here, so bind it again after changing it). */
 int mppi_set_dem_device(mppi_ctx* ctx, const float* z_device, int32_t rows, int32_t cols,
                         float x_min, float y_min, float resolution);
 
