@@ -50,6 +50,7 @@ def parse():
                     help="bounded oracle sample on the host (rank 0, N=1); 0 disables")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     ap.add_argument("--no-bilinear", action="store_true", help="skip the C5 tiled-lookup roofline leg")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 full-step leg (K=262144, H=128, 8192^2 DEM)")
     ap.add_argument("--sync", action="store_true",
                     help="report the synchronous mode (no deferred optimal rollout) as the headline")
     return ap.parse_args()
@@ -142,6 +143,44 @@ def bilinear_bench(torch, device, reps=20):
             "kernel_avg_ms": round(ms, 4), "algorithmic_bytes_per_launch": alg,
             "workload": f"C5 tile {G}^2 DEM (synthetic), N={N} uniform queries binned by 64x64 tile",
             "scattered_query_ms": round(scat_ms, 3)}
+
+
+def c5_bench(device_index, steps=50, warmup=10):
+    """Config C5 (BASELINE.json configs[4]) on one GPU: K=262144, H=128 on the 8192^2 DEM @0.025 m.
+
+    Same step and timing as the headline (inputs resident, outputs in host memory every step,
+    deferred optimal rollout); reported beside the headline, not as `value`.
+    """
+    from mppi_amd import _lib, scene
+    Z, hw, cm = scene.scene_c5()
+    K, H = 262144, 128
+    eng = _lib.Engine(_lib.make_params(K, H), device_index)
+    eng.set_dem(Z, hw)
+    eng.set_costmap(cm, hw)
+    eng.set_state(_lib.make_state(0.0, 0.0, (1.0, 0.0, 0.0), goal_x=80.0, goal_y=20.0))
+    eng.set_async_tail(True)
+    for i in range(warmup):
+        eng.step("3d", i, copy=False)
+    eng.sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        eng.step("3d", warmup + i, copy=False)
+    eng.outputs()
+    eng.sync()
+    el = time.perf_counter() - t0
+    eng.set_timing(True)
+    for i in range(10):
+        eng.step("3d", warmup + steps + i, copy=False)
+    eng.outputs()
+    roll_ms, fin_ms, n = eng.timing()
+    eng.close()
+    k_ms = roll_ms / max(n, 1)
+    alg = BYTES_PER_ROLLOUT_STEP * K * H
+    return {"workload": "C5: K=262144, H=128, 8192^2 DEM @0.025 m (synthetic craters + fBm), 1024^2 costmap",
+            "steps_per_s": round(steps / el, 3), "ms_per_step": round(el / steps * 1e3, 4),
+            "rollout_kernel_avg_ms": round(k_ms, 4), "finish_kernel_avg_ms": round(fin_ms / max(n, 1), 4),
+            "rollout_achieved_GBs": round(alg / (k_ms * 1e-3) / 1e9, 1),
+            "rollout_frac_of_hbm_peak": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def main():
@@ -275,6 +314,8 @@ def main():
         }
         if world == 1 and not args.no_bilinear:
             rec["bilinear_roofline"] = bilinear_bench(torch, torch.device("cuda", local_rank))
+        if world == 1 and not args.no_c5:
+            rec["c5"] = c5_bench(local_rank)
         if world == 1 and args.cpu_baseline_seconds > 0:
             rec["cpu_baseline"] = cpu_baseline(Z, hw, cm, H, args.cpu_baseline_seconds)
         print(json.dumps(rec), flush=True)
