@@ -13,8 +13,10 @@
 #include <cstring>
 #include <string>
 #include <unordered_map>
+#include <vector>
 
 #include "mppi.h"
+#include "mppi_costmap.h"
 #include "mppi_kernels.h"
 
 using namespace mppi;
@@ -69,6 +71,7 @@ struct mppi_ctx {
   size_t cm_cap = 0;
   int cm_size = 0;
   float cm_hw = 0, cm_res = 0;
+  CostmapScratch cms;  // mppi_build_costmap scratch
   // verified division-by-constant reciprocals (0 = use the IEEE division)
   float rinv_res = 0, rinv_res_c = 0;
   unsigned* cdiv_bad = nullptr;  // device counter for launch_cdiv_verify
@@ -824,7 +827,96 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   return rc;
 }
 
+
+// ---- obstacle costmap builder (mppi_build_costmap / mppi_costmap_builder_*) ----
+
+void costmap_free(CostmapScratch& sc) {
+  if (sc.occ) hipFree(sc.occ);
+  if (sc.first) hipFree(sc.first);
+  if (sc.last) hipFree(sc.last);
+  if (sc.g2) hipFree(sc.g2);
+  if (sc.d2) hipFree(sc.d2);
+  if (sc.range) hipFree(sc.range);
+  if (sc.obs) hipFree(sc.obs);
+  if (sc.xs) hipFree(sc.xs);
+  sc = CostmapScratch{};
+}
+
+int costmap_check(const double* obstacles, int32_t n, int32_t size, int32_t power) {
+  if (n < 0 || (n > 0 && !obstacles)) return fail(MPPI_EINVAL, "obstacles: null pointer or negative count");
+  if (size < 2 || size > COSTMAP_MAX_SIZE) return fail(MPPI_EINVAL, "costmap size must be in [2, 8192]");
+  if (power < 0) return fail(MPPI_EINVAL, "costmap power must be >= 0");
+  return MPPI_OK;
+}
+
+// Host staging for one build, with float64 arithmetic in the reference's order
+// (MPPI_isaac.py:363-370): x_local = y_global - y0, y_local = x_global - x0,
+// total_radius = r_obs/2 + r_robot + 0.1, squared with libm pow as CPython's `**`;
+// grid coordinates as np.linspace(-hw, hw, size) (i*step + start, last = stop).
+// The vectors must outlive the stream work (the caller synchronises).
+int costmap_stage(CostmapScratch& sc, const double* obstacles, int32_t n, int32_t size, double hw, double ox,
+                  double oy, double r_robot, std::vector<double>& obs, std::vector<double>& xs, hipStream_t st) {
+  const size_t cells = (size_t)size * size;
+  const size_t nseg = (size_t)(size + COSTMAP_SEG - 1) / COSTMAP_SEG;
+  if (cells > sc.cells_cap) {
+    HIP_TRY(hipStreamSynchronize(st));
+    for (void* p : {(void*)sc.occ, (void*)sc.first, (void*)sc.last, (void*)sc.g2, (void*)sc.d2})
+      if (p) HIP_TRY(hipFree(p));
+    sc.occ = nullptr;
+    sc.first = sc.last = sc.g2 = sc.d2 = nullptr;
+    sc.cells_cap = 0;
+    HIP_TRY(hipMalloc(&sc.occ, cells));
+    HIP_TRY(hipMalloc(&sc.first, nseg * size * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&sc.last, nseg * size * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&sc.g2, cells * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&sc.d2, cells * sizeof(int32_t)));
+    sc.cells_cap = cells;
+  }
+  if (!sc.range) HIP_TRY(hipMalloc(&sc.range, 2 * sizeof(int32_t)));
+  const size_t nobs = (size_t)std::max<int32_t>(n, 1);
+  if (nobs > sc.obs_cap) {
+    HIP_TRY(hipStreamSynchronize(st));
+    if (sc.obs) HIP_TRY(hipFree(sc.obs));
+    sc.obs = nullptr;
+    HIP_TRY(hipMalloc(&sc.obs, nobs * 3 * sizeof(double)));
+    sc.obs_cap = nobs;
+  }
+  if ((size_t)size > sc.xs_cap) {
+    HIP_TRY(hipStreamSynchronize(st));
+    if (sc.xs) HIP_TRY(hipFree(sc.xs));
+    sc.xs = nullptr;
+    HIP_TRY(hipMalloc(&sc.xs, (size_t)size * sizeof(double)));
+    sc.xs_cap = (size_t)size;
+  }
+  obs.assign(nobs * 3, 0.0);
+  for (int32_t k = 0; k < n; ++k) {
+    const double xg = obstacles[3 * k], yg = obstacles[3 * k + 1], r = obstacles[3 * k + 2];
+    const double tr = r / 2 + r_robot + 0.1;
+    obs[3 * k + 0] = yg - oy;
+    obs[3 * k + 1] = xg - ox;
+    obs[3 * k + 2] = std::pow(tr, 2.0);
+  }
+  xs.resize(size);
+  const double start = -hw, stop = hw;
+  const double step = (stop - start) / (double)(size - 1);
+  for (int32_t i = 0; i < size; ++i) xs[i] = (double)i * step + start;
+  xs[size - 1] = stop;
+  HIP_TRY(hipMemcpyAsync(sc.obs, obs.data(), nobs * 3 * sizeof(double), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(sc.xs, xs.data(), (size_t)size * sizeof(double), hipMemcpyHostToDevice, st));
+  return MPPI_OK;
+}
+
 }  // namespace
+
+struct mppi_costmap_builder {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  CostmapScratch sc;
+  float* out = nullptr;
+  size_t out_cap = 0;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  double last_ms = 0;
+};
 
 extern "C" {
 
@@ -928,6 +1020,7 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->Z_owned && c->Z) hipFree(c->Z);
   if (c->ntab) hipFree(c->ntab);
   if (c->cm) hipFree(c->cm);
+  costmap_free(c->cms);
   for (float* u : c->u_nom)
     if (u) hipFree(u);
   if (c->cost) hipFree(c->cost);
@@ -1360,6 +1453,102 @@ int mppi_selftest(mppi_ctx* c, int32_t what, int64_t n, uint64_t seed, int64_t* 
   hipFree(d);
   if (e != hipSuccess) return fail(MPPI_EHIP, std::string("selftest: ") + hipGetErrorString(e));
   *mismatches = (int64_t)h;
+  return MPPI_OK;
+}
+
+int mppi_build_costmap(mppi_ctx* c, const double* obstacles, int32_t n, int32_t size, double half_width,
+                       double origin_x, double origin_y, double r_robot, int32_t power, float* out_host) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  int rc = costmap_check(obstacles, n, size, power);
+  if (rc) return rc;
+  const float res = (float)(2 * half_width / size);  // Surface.costmap_resolution (MPPI_isaac.py:272)
+  if (!(res > 0.0f)) return fail(MPPI_EINVAL, "costmap resolution must be > 0");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t bytes = (size_t)size * size * sizeof(float);
+  if (bytes > c->cm_cap) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->cm) HIP_TRY(hipFree(c->cm));
+    c->cm = nullptr;
+    c->cm_cap = 0;
+    HIP_TRY(hipMalloc(&c->cm, bytes));
+    c->cm_cap = bytes;
+  }
+  std::vector<double> obs, xs;
+  rc = costmap_stage(c->cms, obstacles, n, size, half_width, origin_x, origin_y, r_robot, obs, xs, c->stream);
+  if (rc) return rc;
+  HIP_TRY(launch_costmap_build(c->cms, n, size, power, c->cm, c->stream));
+  if (out_host) HIP_TRY(hipMemcpyAsync(out_host, c->cm, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->cm_size = size;
+  c->cm_hw = (float)half_width;
+  c->cm_res = res;
+  return verified_reciprocal(c, res, &c->rinv_res_c);
+}
+
+int mppi_costmap_builder_create(int32_t device, mppi_costmap_builder** out) {
+  if (!out) return fail(MPPI_EINVAL, "null argument");
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(device));
+  auto* b = new mppi_costmap_builder();
+  b->device = device;
+  if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&b->ev[0]) != hipSuccess || hipEventCreate(&b->ev[1]) != hipSuccess) {
+    mppi_costmap_builder_destroy(b);
+    return fail(MPPI_EHIP, "costmap builder: stream/event creation failed");
+  }
+  *out = b;
+  return MPPI_OK;
+}
+
+void mppi_costmap_builder_destroy(mppi_costmap_builder* b) {
+  if (!b) return;
+  hipSetDevice(b->device);
+  if (b->stream) hipStreamSynchronize(b->stream);
+  costmap_free(b->sc);
+  if (b->out) hipFree(b->out);
+  for (auto& e : b->ev)
+    if (e) hipEventDestroy(e);
+  if (b->stream) hipStreamDestroy(b->stream);
+  delete b;
+}
+
+int mppi_costmap_builder_build(mppi_costmap_builder* b, const double* obstacles, int32_t n, int32_t size,
+                               double half_width, double origin_x, double origin_y, double r_robot, int32_t power,
+                               float* out_host, float* out_device) {
+  if (!b) return fail(MPPI_EINVAL, "null builder");
+  int rc = costmap_check(obstacles, n, size, power);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(b->device));
+  const size_t bytes = (size_t)size * size * sizeof(float);
+  float* dst = out_device;
+  if (!dst) {
+    if (bytes > b->out_cap) {
+      HIP_TRY(hipStreamSynchronize(b->stream));
+      if (b->out) HIP_TRY(hipFree(b->out));
+      b->out = nullptr;
+      b->out_cap = 0;
+      HIP_TRY(hipMalloc(&b->out, bytes));
+      b->out_cap = bytes;
+    }
+    dst = b->out;
+  }
+  std::vector<double> obs, xs;
+  rc = costmap_stage(b->sc, obstacles, n, size, half_width, origin_x, origin_y, r_robot, obs, xs, b->stream);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(b->ev[0], b->stream));
+  HIP_TRY(launch_costmap_build(b->sc, n, size, power, dst, b->stream));
+  HIP_TRY(hipEventRecord(b->ev[1], b->stream));
+  if (out_host) HIP_TRY(hipMemcpyAsync(out_host, dst, bytes, hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
+  b->last_ms = ms;
+  return MPPI_OK;
+}
+
+int mppi_costmap_builder_last_ms(mppi_costmap_builder* b, double* ms) {
+  if (!b || !ms) return fail(MPPI_EINVAL, "null argument");
+  *ms = b->last_ms;
   return MPPI_OK;
 }
 

@@ -1,0 +1,32 @@
+// On-device obstacle costmap builder:
+// Surface.create_obstacles_costmap, thesis_master/warp_implementation/MPPI_isaac.py:361-378.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mppi {
+
+// Device scratch for one build of a size x size costmap (grown on demand by the caller).
+struct CostmapScratch {
+  uint8_t* occ = nullptr;    // [size*size] 1 = inside an inflated obstacle disc
+  int32_t* first = nullptr;  // [segments*size] first occupied row of each column segment (-1: none)
+  int32_t* last = nullptr;   // [segments*size] last occupied row of each column segment (-1: none)
+  int32_t* g2 = nullptr;     // [size*size] squared vertical distance to the nearest obstacle (column pass)
+  int32_t* d2 = nullptr;     // [size*size] squared Euclidean distance (row pass)
+  int32_t* range = nullptr;  // [2] min / max of d2
+  double* obs = nullptr;     // [n*3] (x_local, y_local, total_radius) per obstacle
+  double* xs = nullptr;      // [size] np.linspace(-hw, hw, size)
+  size_t cells_cap = 0, obs_cap = 0, xs_cap = 0;
+};
+
+constexpr int COSTMAP_SEG = 32;         // rows per column segment of the column pass
+constexpr int COSTMAP_MAX_SIZE = 8192;  // (2*size+1)^2 must fit int32 (the no-obstacle marker)
+
+// Enqueue the whole build on `st`: raster -> exact EDT (column pass, row pass) -> min/max ->
+// min-max normalise -> (1 - d)^power, written to out[size*size] (device, float32, row-major).
+// sc.obs / sc.xs must already hold the n obstacle triples and the size grid coordinates.
+hipError_t launch_costmap_build(const CostmapScratch& sc, int n_obs, int size, int power, float* out,
+                                hipStream_t st);
+
+}  // namespace mppi

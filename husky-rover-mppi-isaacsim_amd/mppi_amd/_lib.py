@@ -54,6 +54,7 @@ class MppiState(C.Structure):
 
 
 _FP = C.POINTER(C.c_float)
+_DP = C.POINTER(C.c_double)
 
 
 class MppiOutputs(C.Structure):
@@ -97,6 +98,13 @@ _PROTOS = {
                                    C.c_void_p, C.c_void_p]),
     "mppi_bilinear_tiled": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mppi_sync": (C.c_int, [C.c_void_p]),
+    "mppi_build_costmap": (C.c_int, [C.c_void_p, _DP, C.c_int32, C.c_int32, C.c_double, C.c_double,
+                                     C.c_double, C.c_double, C.c_int32, _FP]),
+    "mppi_costmap_builder_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
+    "mppi_costmap_builder_destroy": (None, [C.c_void_p]),
+    "mppi_costmap_builder_build": (C.c_int, [C.c_void_p, _DP, C.c_int32, C.c_int32, C.c_double, C.c_double,
+                                             C.c_double, C.c_double, C.c_int32, _FP, C.c_void_p]),
+    "mppi_costmap_builder_last_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
 }
 
 _lib = None
@@ -133,6 +141,53 @@ def load_library(path: str = LIB_PATH):
 
 def _fp(a):
     return a.ctypes.data_as(_FP)
+
+
+def _obstacles(obstacles):
+    """Obstacle list [(x_global, y_global, r_obs), ...] -> contiguous float64 [n, 3] (n may be 0)."""
+    a = np.ascontiguousarray(np.asarray(obstacles, dtype=np.float64).reshape(-1, 3))
+    return a, a.ctypes.data_as(_DP)
+
+
+class CostmapBuilder:
+    """Surface.create_obstacles_costmap (MPPI_isaac.py:361-378) on the GPU, no controller context needed.
+
+    build(...) returns the size x size float32 costmap as an ndarray (the reference returns one);
+    with out_device=<pointer> the map is written to caller-owned device memory instead.
+    """
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        self.device = int(device)
+        h = C.c_void_p()
+        _check(self.lib, self.lib.mppi_costmap_builder_create(self.device, C.byref(h)),
+               "mppi_costmap_builder_create")
+        self.h = h
+
+    def build(self, obstacles, origin, size, half_width, r_robot, power=20, out_device=None):
+        obs, optr = _obstacles(obstacles)
+        out = None if out_device is not None else np.empty((size, size), np.float32)
+        _check(self.lib, self.lib.mppi_costmap_builder_build(
+            self.h, optr, obs.shape[0], int(size), float(half_width), float(origin[0]), float(origin[1]),
+            float(r_robot), int(power), None if out is None else _fp(out),
+            None if out_device is None else C.c_void_p(int(out_device))), "mppi_costmap_builder_build")
+        return out
+
+    def last_ms(self):
+        ms = C.c_double()
+        _check(self.lib, self.lib.mppi_costmap_builder_last_ms(self.h, C.byref(ms)), "mppi_costmap_builder_last_ms")
+        return ms.value
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            self.lib.mppi_costmap_builder_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def _check(lib, rc, what):
@@ -243,6 +298,16 @@ class Engine:
         if resolution is None:
             resolution = 2.0 * half_width / size
         self._c(self.lib.mppi_set_costmap(self.ctx, _fp(cm), size, half_width, resolution), "mppi_set_costmap")
+
+    def build_costmap(self, obstacles, origin, size, half_width, r_robot, power=20, copy_out=True):
+        """Surface.create_obstacles_costmap + costmap_wp.assign in one device pass
+        (visual_terrain_stack_full_terrain.py:561-563); returns the map if copy_out."""
+        obs, optr = _obstacles(obstacles)
+        out = np.empty((size, size), np.float32) if copy_out else None
+        self._c(self.lib.mppi_build_costmap(self.ctx, optr, obs.shape[0], int(size), float(half_width),
+                                            float(origin[0]), float(origin[1]), float(r_robot), int(power),
+                                            None if out is None else _fp(out)), "mppi_build_costmap")
+        return out
 
     def set_state(self, state: MppiState):
         self._c(self.lib.mppi_set_state(self.ctx, C.byref(state)), "mppi_set_state")

@@ -134,10 +134,18 @@ class Surface:
     def import_obstacles_costmap(self, costmap_file):
         return np.load(costmap_file, allow_pickle=False)
 
+    # device the HIP costmap builder runs on (the reference's Warp arrays live on "cuda" = device 0)
+    device = 0
+
     def create_obstacles_costmap(self, obstacles, origin):
-        """MPPI_isaac.py:361-378 with scipy's exact EDT in place of cv2.distanceTransform."""
-        return scene.surface_obstacles_costmap(self.costmap_size, self.half_width, obstacles, origin,
-                                               self.r_robot)
+        """MPPI_isaac.py:361-378 on the GPU (csrc/mppi_costmap.hip): disc raster, exact EDT in place of
+        cv2.distanceTransform, min-max normalise, (1 - d)**20; returns the ndarray."""
+        from . import _lib
+        b = getattr(self, "_builder", None)
+        if b is None:
+            b = self._builder = _lib.CostmapBuilder(self.device)
+        self.obstacles = obstacles
+        return b.build(obstacles, origin, self.costmap_size, self.half_width, self.r_robot, power=20)
 
 
 # =====================================================================  Robot
@@ -296,6 +304,17 @@ class MPPI_Controller:
         self.surface.costmap = np.asarray(flat, np.float32).reshape(
             self.surface.costmap_size, self.surface.costmap_size)
         self._upload_costmap(self.surface.costmap)
+
+    def rebuild_costmap(self, obstacles, origin):
+        """surface.costmap = surface.create_obstacles_costmap(rocks, origin) + costmap_wp.assign(...)
+        (visual_terrain_stack_full_terrain.py:561-563) in one device pass: the map is built in the
+        engine's own costmap buffer (no upload) and copied back once for surface.costmap."""
+        if self.engine is None:
+            raise RuntimeError("call warp_setup() first")
+        s = self.surface
+        s.obstacles = obstacles
+        s.costmap = self.engine.build_costmap(obstacles, origin, s.costmap_size, s.half_width, s.r_robot, 20)
+        return s.costmap
 
     @property
     def Z_wp(self):

@@ -1,0 +1,42 @@
+"""CPU: the obstacle-costmap restatement (oracle/costmap_ref.py, MPPI_isaac.py:361-378).
+
+Pins the exact-EDT call against an exhaustive search, and the raster against the reference's
+frame convention (x_local = y_global - y0 marks a COLUMN coordinate, y_local = x_global - x0 a
+ROW coordinate of meshgrid(linspace(-hw, hw, size))).  cv2.distanceTransform itself is
+"parity unpinned" (cv2 is absent).
+"""
+import numpy as np
+import pytest
+
+from oracle import costmap_ref as CR
+
+
+def _rocks(n, extent, seed):
+    rng = np.random.RandomState(seed)
+    return [[rng.uniform(-extent, extent), rng.uniform(-extent, extent), rng.uniform(0.0, 0.8)] for _ in range(n)]
+
+
+@pytest.mark.parametrize("size,n,seed", [(48, 6, 0), (65, 15, 1), (80, 40, 2)])
+def test_edt_matches_bruteforce(size, n, seed):
+    occ = CR.raster(_rocks(n, 9.0, seed), (0.4, -0.7), size, 10.0, 1.2)
+    assert occ.any() and not occ.all()
+    assert np.array_equal(CR.edt(occ), CR.edt_bruteforce(occ))
+
+
+def test_raster_frame_swap():
+    # one small rock at global (x, y) = (2, -3), origin (0, 0): its disc is centred on
+    # X = y_global = -3 (column), Y = x_global = 2 (row)
+    size, hw = 101, 10.0
+    occ = CR.raster([[2.0, -3.0, 0.0]], (0.0, 0.0), size, hw, 0.05)   # total radius 0.15 < cell 0.2
+    js, is_ = np.nonzero(occ)
+    x = np.linspace(-hw, hw, size)
+    assert len(js) == 1 and x[is_[0]] == pytest.approx(-3.0) and x[js[0]] == pytest.approx(2.0)
+
+
+def test_edge_cases():
+    size = 32
+    assert np.array_equal(CR.create_obstacles_costmap([], (0, 0), size, 5.0, 1.2), np.ones((size, size), np.float32))
+    full = CR.create_obstacles_costmap([[0.0, 0.0, 100.0]], (0, 0), size, 5.0, 1.2)
+    assert np.array_equal(full, np.ones((size, size), np.float32))
+    cm = CR.create_obstacles_costmap(_rocks(5, 4.0, 3), (0, 0), size, 5.0, 0.3)
+    assert cm.dtype == np.float32 and cm.max() == 1.0 and cm.min() == 0.0
