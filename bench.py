@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     ap.add_argument("--no-bilinear", action="store_true", help="skip the C5 tiled-lookup roofline leg")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 full-step leg (K=262144, H=128, 8192^2 DEM)")
+    ap.add_argument("--no-costmap", action="store_true", help="skip the obstacle-costmap builder leg")
     ap.add_argument("--sync", action="store_true",
                     help="report the synchronous mode (no deferred optimal rollout) as the headline")
     return ap.parse_args()
@@ -181,6 +182,38 @@ def c5_bench(device_index, steps=50, warmup=10):
             "rollout_kernel_avg_ms": round(k_ms, 4), "finish_kernel_avg_ms": round(fin_ms / max(n, 1), 4),
             "rollout_achieved_GBs": round(alg / (k_ms * 1e-3) / 1e9, 1),
             "rollout_frac_of_hbm_peak": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+COSTMAP_BYTES_PER_CELL = 23   # occ 1+1+1, g2 4+4, d2 4+4, out 4 (csrc/mppi_costmap.hip)
+
+
+def costmap_bench(device_index, reps=20, cpu=True):
+    """Surface.create_obstacles_costmap (MPPI_isaac.py:361-378) on the GPU: a 1024^2 costmap (the C5
+    map, grid 8192 / 8) from 750 rocks, HIP-event device time per build; the oracle (numpy raster +
+    scipy exact EDT, 1 core) on the same input once for reference."""
+    from mppi_amd import _lib
+    rng = np.random.RandomState(99)
+    rocks = [[rng.uniform(-95, 95), rng.uniform(-95, 95), rng.uniform(0.0, 0.8)] for _ in range(750)]
+    size, hw = 1024, 102.4
+    b = _lib.CostmapBuilder(device_index)
+    for _ in range(3):
+        b.build(rocks, (0.0, 0.0), size, hw, 1.2)
+    dev_ms, t0 = 0.0, time.perf_counter()
+    for _ in range(reps):
+        b.build(rocks, (0.0, 0.0), size, hw, 1.2)
+        dev_ms += b.last_ms()
+    call_ms = (time.perf_counter() - t0) / reps * 1e3
+    b.close()
+    dev_ms /= reps
+    rec = {"workload": "1024^2 costmap @0.2 m from 750 rocks (exact EDT, power 20)",
+           "kernel_ms": round(dev_ms, 4), "call_ms_incl_d2h": round(call_ms, 3),
+           "achieved_GBs": round(COSTMAP_BYTES_PER_CELL * size * size / (dev_ms * 1e-3) / 1e9, 1)}
+    if cpu:
+        from oracle import costmap_ref as CR
+        t0 = time.perf_counter()
+        CR.create_obstacles_costmap(rocks, (0.0, 0.0), size, hw, 1.2)
+        rec["cpu_oracle_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+    return rec
 
 
 def main():
@@ -316,6 +349,8 @@ def main():
             rec["bilinear_roofline"] = bilinear_bench(torch, torch.device("cuda", local_rank))
         if world == 1 and not args.no_c5:
             rec["c5"] = c5_bench(local_rank)
+        if world == 1 and not args.no_costmap:
+            rec["costmap_builder"] = costmap_bench(local_rank, cpu=args.cpu_baseline_seconds > 0)
         if world == 1 and args.cpu_baseline_seconds > 0:
             rec["cpu_baseline"] = cpu_baseline(Z, hw, cm, H, args.cpu_baseline_seconds)
         print(json.dumps(rec), flush=True)

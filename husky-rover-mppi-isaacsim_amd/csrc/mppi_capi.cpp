@@ -18,6 +18,7 @@
 #include "mppi.h"
 #include "mppi_costmap.h"
 #include "mppi_kernels.h"
+#include "mppi_python25d.h"
 
 using namespace mppi;
 
@@ -1549,6 +1550,56 @@ int mppi_costmap_builder_build(mppi_costmap_builder* b, const double* obstacles,
 int mppi_costmap_builder_last_ms(mppi_costmap_builder* b, double* ms) {
   if (!b || !ms) return fail(MPPI_EINVAL, "null argument");
   *ms = b->last_ms;
+  return MPPI_OK;
+}
+
+int mppi_rollout_python25d(mppi_ctx* c, int64_t n, int32_t H, const double* x0, const double* y0,
+                           const double* heading, const double* lin_vel, const double* ang_vel, double dt,
+                           double half_width, double resolution, double bound, double* traj, int32_t* valid) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  if (n < 0 || H < 1) return fail(MPPI_EINVAL, "python25d: need n >= 0 and H >= 1");
+  if (n == 0) return MPPI_OK;
+  if (!x0 || !y0 || !heading || !lin_vel || !ang_vel || !traj || !valid)
+    return fail(MPPI_EINVAL, "python25d: null argument");
+  if (!c->Z) return fail(MPPI_ESTATE, "python25d: set a DEM first");
+  if (!(resolution > 0.0) || !(half_width > 0.0)) return fail(MPPI_EINVAL, "python25d: bad grid geometry");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const size_t nH = (size_t)n * H;
+  const size_t bytes = (5 * (size_t)n + 2 * nH + 3 * nH) * sizeof(double) + (size_t)n * sizeof(int32_t);
+  char* buf = nullptr;
+  HIP_TRY(hipMalloc(&buf, bytes));
+  double* d = (double*)buf;
+  P25Args a;
+  a.Z = c->Z;
+  a.rows = c->rows;
+  a.cols = c->cols;
+  a.hw = half_width;
+  a.res = resolution;
+  a.xstep = (half_width - -half_width) / (double)(c->cols - 1);
+  a.ystep = (half_width - -half_width) / (double)(c->rows - 1);
+  a.dt = dt;
+  a.bound = bound;
+  a.n = n;
+  a.H = H;
+  a.x0 = d;
+  a.y0 = d + n;
+  a.hd = d + 2 * n;
+  a.v = d + 5 * n;
+  a.w = a.v + nH;
+  a.traj = d + 5 * n + 2 * nH;
+  a.valid = (int32_t*)(a.traj + 3 * nH);
+  hipError_t e = hipMemcpyAsync((void*)a.x0, x0, n * sizeof(double), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync((void*)a.y0, y0, n * sizeof(double), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync((void*)a.hd, heading, 3 * n * sizeof(double), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync((void*)a.v, lin_vel, nH * sizeof(double), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync((void*)a.w, ang_vel, nH * sizeof(double), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = launch_python25d(a, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(traj, a.traj, 3 * nH * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(valid, a.valid, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(buf);
+  if (e != hipSuccess) return fail(MPPI_EHIP, std::string("python25d: ") + hipGetErrorString(e));
   return MPPI_OK;
 }
 

@@ -105,6 +105,8 @@ _PROTOS = {
     "mppi_costmap_builder_build": (C.c_int, [C.c_void_p, _DP, C.c_int32, C.c_int32, C.c_double, C.c_double,
                                              C.c_double, C.c_double, C.c_int32, _FP, C.c_void_p]),
     "mppi_costmap_builder_last_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
+    "mppi_rollout_python25d": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, _DP, _DP, _DP, _DP, _DP, C.c_double,
+                                         C.c_double, C.c_double, C.c_double, _DP, C.POINTER(C.c_int32)]),
 }
 
 _lib = None
@@ -308,6 +310,26 @@ class Engine:
                                             float(origin[0]), float(origin[1]), float(r_robot), int(power),
                                             None if out is None else _fp(out)), "mppi_build_costmap")
         return out
+
+    def rollout_python25d(self, x0, y0, heading, lin_vel, ang_vel, dt, half_width, resolution, bound=20.0):
+        """debug.generate_trajectory_25D (debug.py:312-364) for K trajectories on this context's DEM, float64.
+
+        Returns (traj [K, H, 3], valid [K] bool); valid is False where the reference returns None."""
+        v = np.ascontiguousarray(lin_vel, np.float64)
+        w = np.ascontiguousarray(ang_vel, np.float64)
+        K, H = v.shape
+        assert w.shape == (K, H)
+        x0 = np.ascontiguousarray(np.broadcast_to(np.asarray(x0, np.float64), (K,)))
+        y0 = np.ascontiguousarray(np.broadcast_to(np.asarray(y0, np.float64), (K,)))
+        hd = np.ascontiguousarray(np.broadcast_to(np.asarray(heading, np.float64).reshape(-1, 3), (K, 3)))
+        traj = np.zeros((K, H, 3), np.float64)
+        valid = np.zeros(K, np.int32)
+        dp = lambda a: a.ctypes.data_as(_DP)  # noqa: E731
+        self._c(self.lib.mppi_rollout_python25d(self.ctx, K, H, dp(x0), dp(y0), dp(hd), dp(v), dp(w), float(dt),
+                                                float(half_width), float(resolution), float(bound), dp(traj),
+                                                valid.ctypes.data_as(C.POINTER(C.c_int32))),
+                "mppi_rollout_python25d")
+        return traj, valid.astype(bool)
 
     def set_state(self, state: MppiState):
         self._c(self.lib.mppi_set_state(self.ctx, C.byref(state)), "mppi_set_state")

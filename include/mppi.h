@@ -246,6 +246,21 @@ int mppi_bilinear_tiled(mppi_ctx* ctx, const float* xs_dev, const float* ys_dev,
 /* Wait for all work enqueued on the context stream. */
 int mppi_sync(mppi_ctx* ctx);
 
+/* ---- reference-integrator mode "python25d"  ----
+ * generate_trajectory_25D of thesis_master/python_mppi_projection/debug.py:312-364,
+ * the reference's numpy 2.5D integrator, for n trajectories at once, in float64,
+ * on the context's DEM (row j at y = linspace(-half_width, half_width, rows)[j],
+ * as debug.py's meshgrid; `resolution` as its `resolution` argument).  Inputs
+ * (host): x0, y0 [n], heading [n*3], lin_vel, ang_vel [n*H] trajectory-major;
+ * outputs (host): traj [n*H*3] (x, y, height per step), valid [n] (0 where the
+ * reference returns None: the trajectory left |x|, |y| < bound, debug.py:359;
+ * its rows from that step on are 0).  Synchronous.  Not on the MPPI step path:
+ * it lets whole trajectories be compared with the reference's own function. */
+int mppi_rollout_python25d(mppi_ctx* ctx, int64_t n, int32_t H, const double* x0, const double* y0,
+                           const double* heading, const double* lin_vel, const double* ang_vel,
+                           double dt, double half_width, double resolution, double bound,
+                           double* traj, int32_t* valid);
+
 /* Device self-test of the engine's exact-arithmetic fast paths: what = 0 checks
  * the shared-reciprocal division against IEEE a/b, what = 1 the sqrt path
  * against IEEE sqrtf, what = 2 / 3 the lean normalisation of the pair kernel's

@@ -19,6 +19,12 @@ philox_rocrand.txt
     rocRAND Philox4x32-10 known answers (philox_kat.cpp, compiled here with
     hipcc and run on the host): seed, subsequence, block, 4 x uint32.
 
+python25d.npz
+    Whole trajectories of the reference's numpy integrator
+    debug.generate_trajectory_25D (debug.py:312-364), imported from the
+    read-only reference tree, on its own 400^2 scene (Z stored as float32):
+    the fixture for the HIP "python25d" reference-integrator mode.
+
 step_small.npz
     Regression vectors of the CPU restatement (oracle/mppi_ref.py) for whole
     MPPI steps on a small self-contained scene (200^2 DEM, 25^2 costmap stored
@@ -173,8 +179,55 @@ def make_steps():
     print("step_small.npz:", list(STEP_CASES))
 
 
+# python25d cases: (K, H, dt, start extent, v range, w step std, seed)
+P25_CASES = {
+    "demo": (40, 250, 0.01, 15.0, (0.5, 2.5), 0.05, 11),
+    "escape": (24, 200, 0.045, 12.0, (1.5, 2.5), 0.1, 12),
+}
+
+
+def make_python25d():
+    """Whole trajectories of the reference's numpy integrator debug.generate_trajectory_25D
+    (debug.py:312-364) on its own 400^2 / 20 m scene (module globals X, Y, Z, resolution;
+    Z rounded to float32 so the GPU sees the same heights).  Velocity sequences are seeded
+    random walks in the style of generate_linear/angular_velocities (:415-461).  A trajectory
+    for which the reference raises IndexError (x or y in [19.9, 20): its i+1 / j+1 corner is
+    past the grid) is redrawn; one it returns None for is stored with valid = False."""
+    dbg = load_debug()
+    Z32 = np.asarray(dbg.Z, np.float32)
+    Zr = Z32.astype(np.float64)
+    data = {"Z": Z32, "hw": np.float64(dbg.half_width), "res": np.float64(dbg.resolution),
+            "grid": np.int64(Z32.shape[0])}
+    for name, (K, H, dt, ext, vr, wstd, seed) in P25_CASES.items():
+        rng = np.random.default_rng(seed)
+        rows = {k: [] for k in ("x0", "y0", "heading", "v", "w", "traj", "valid")}
+        while len(rows["x0"]) < K:
+            x0, y0 = rng.uniform(-ext, ext, 2)
+            hd = np.array([rng.normal(), rng.normal(), 0.0])
+            v = np.clip(rng.uniform(*vr) + np.cumsum(rng.normal(0, 0.1, H)), vr[0], vr[1])
+            w = np.clip(np.cumsum(rng.normal(0, wstd, H)), -0.5, 0.5)
+            try:
+                tr = dbg.generate_trajectory_25D(x0, y0, hd.copy(), v, w, dt, H, dbg.resolution, dbg.X, dbg.Y, Zr)
+            except IndexError:
+                continue
+            rows["x0"].append(x0)
+            rows["y0"].append(y0)
+            rows["heading"].append(hd)
+            rows["v"].append(v)
+            rows["w"].append(w)
+            rows["valid"].append(tr is not None)
+            rows["traj"].append(np.zeros((H, 3)) if tr is None else tr)
+        for k, val in rows.items():
+            data[f"{name}/{k}"] = np.asarray(val)
+        data[f"{name}/dt"] = np.float64(dt)
+        print(f"python25d {name}: K={K} H={H} valid={int(np.sum(rows['valid']))}")
+    np.savez_compressed(os.path.join(HERE, "python25d.npz"), **data)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["primitives", "philox", "steps"]
+    which = sys.argv[1:] or ["primitives", "philox", "steps", "python25d"]
+    if "python25d" in which:
+        make_python25d()
     if "primitives" in which:
         make_primitives()
     if "philox" in which:
