@@ -1411,6 +1411,9 @@ __device__ __forceinline__ void noise_ahead(const RolloutArgs& a, unsigned char*
 #ifndef MPPI_PAIR_LAG
 #define MPPI_PAIR_LAG 4
 #endif
+#ifndef MPPI_FLAG_CACHE
+#define MPPI_FLAG_CACHE 1  // diagnostic builds: 0 = read the partner's counter at every wait
+#endif
 constexpr int PAIR_D = MPPI_PAIR_D;
 constexpr int PAIR_LAG = MPPI_PAIR_LAG;
 static_assert(PAIR_LAG > 0 && PAIR_LAG < PAIR_D, "ring depth must exceed the consume lag");
@@ -1518,11 +1521,20 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   }
   __syncthreads();  // flags initialised
 
-  auto wait_ge = [&](const int* f, int target) __attribute__((always_inline)) {
+  // Wait until *f >= target; `seen` caches the last value this wave acquired from f.  The
+  // counters only grow, and everything published before a value is visible to the wave
+  // once it has acquired that value, so a cached value that already covers the target
+  // needs no LDS read and no fence (the partner usually runs several steps ahead).
+  auto wait_ge = [&](const int* f, int target, int& seen) __attribute__((always_inline)) {
+#if MPPI_FLAG_CACHE
+    if (seen >= target) return;
+#endif
 #ifdef MPPI_STAMPS
     const uint64_t t0 = dbg_stamp();
 #endif
-    while (lds_load_acquire(f) < target) __builtin_amdgcn_s_sleep(1);
+    int v;
+    while ((v = lds_load_acquire(f)) < target) __builtin_amdgcn_s_sleep(1);
+    seen = v;
 #ifdef MPPI_STAMPS
     st_wait += dbg_stamp() - t0;
 #endif
@@ -1530,9 +1542,10 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 
   if (!side) {
     // ---------------- chain wave: the serial projection, one step per iteration
+    int seen_prod = 0, seen_cons = 0;
     for (int sc = 0; sc < H; ++sc) {
-      wait_ge(f_prod, sc + 1);
-      wait_ge(f_cons, sc - D + 1);
+      wait_ge(f_prod, sc + 1, seen_prod);
+      wait_ge(f_cons, sc - D + 1, seen_cons);
       const float* ri = ring_in + (sc % D) * 2 * TB + tj;
       const float v = ri[0], wv = ri[TB];
       float sn, cs;  // sin/cos of the Rodrigues angle: independent of the chain state, so it
@@ -1587,6 +1600,7 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
     //  * wheel heights of the EVEN steps only (the slope critic, critics_warp.py:220-267,
     //    reads lw/rw at i, i+2 for even i; odd-step contacts are computed only for
     //    DUMP), used one half later.
+    int seen_chain = 0;                                 // last acquired value of f_chain
     float eA1 = en1, eA2 = en2, eB1 = 0.f, eB2 = 0.f;  // normals of the even / odd step
     if constexpr (MODE == 0) {
       const int t1 = min(1, H - 1);
@@ -1616,7 +1630,7 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
           ust[(size_t)p * TB] = u1;   // MODE 1: the leaf records read the injected controls back
           ust[(size_t)(H + p) * TB] = u2;
         }
-        wait_ge(f_chain, p - D + 1);
+        wait_ge(f_chain, p - D + 1, seen_chain);
         L = L * a.fa + (u1 * a.fk) * (1.0f - a.fa);
         R = R * a.fa + (u2 * a.fk) * (1.0f - a.fa);
         const float vp = clampf((L + R) / 2.0f, a.vmin, a.vmax);
@@ -1636,7 +1650,7 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
       }
       const int sc = p - PAIR_LAG;
       if (CONS || (GUARD && sc >= 0 && sc < H)) {  // contacts + critics of step sc (projection_warp.py:333-348)
-        wait_ge(f_chain, sc + 1);
+        wait_ge(f_chain, sc + 1, seen_chain);
         const float* ro = ring_out + (sc % D) * 4 * TB + tj;
         const float x = ro[0], y = ro[TB], cx = ro[2 * TB], cy = ro[3 * TB];
         const float vq = ring_in[(sc % D) * 2 * TB + tj];  // v of step sc (slot not reused yet)

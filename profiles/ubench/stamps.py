@@ -21,7 +21,8 @@ def build():
     csrc = os.path.join(PKG, "csrc")
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
            "-fPIC", "-shared", "-DMPPI_STAMPS", f"-I{ROOT}/include", f"-I{csrc}", "-x", "hip",
-           os.path.join(csrc, "mppi_kernels.hip"), os.path.join(csrc, "mppi_capi.cpp"), "-o", SO]
+           *[os.path.join(csrc, f) for f in ("mppi_kernels.hip", "mppi_costmap.hip", "mppi_python25d.hip",
+                                            "mppi_capi.cpp")], "-o", SO]
     subprocess.run(cmd, check=True)
 
 
