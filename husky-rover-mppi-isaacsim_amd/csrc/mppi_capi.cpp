@@ -39,6 +39,7 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 constexpr size_t kLdsBytes = 160 * 1024;
+constexpr int kEpsSlots = 3;
 
 struct Plan {
   bool lds = false;       // rollout kernel DEM path
@@ -101,16 +102,22 @@ struct mppi_ctx {
   // precomputed sampling normals (pair kernel, MODE 0): two slots, each tagged with the
   // Philox step it holds; the next step's normals are generated speculatively on
   // noise_stream while the GPU is otherwise idle (finish kernel, host gap)
-  float* eps[2] = {nullptr, nullptr};
+  // sampling normals, one slot per step in flight: the rollout's, the next step's and the
+  // one after (generated two steps ahead, so the noise kernel is never on the step's path)
+  float* eps[kEpsSlots] = {nullptr, nullptr, nullptr};
   size_t eps_cap = 0;
-  int64_t eps_step[2] = {-1, -1};
-  hipEvent_t eps_ev[2] = {nullptr, nullptr};
-  bool eps_pending[2] = {false, false};
+  int64_t eps_step[kEpsSlots] = {-1, -1, -1};
+  hipEvent_t eps_ev[kEpsSlots] = {nullptr, nullptr, nullptr};
+  bool eps_pending[kEpsSlots] = {false, false, false};
+  int noise_ahead = 2;  // steps of normals generated ahead (env MPPI_NOISE_AHEAD=1: the next only)
   hipStream_t noise_stream = nullptr;
   int prio_least = 0, prio_greatest = 0;
   // tree levels inside the rollout kernel (MPPI_FUSED_FINISH): 0 none (default: measured fastest
   // with the deferred optimal rollout, profiles/r01_notes.md), 1 the first level, 2 all + the finish
   int fused_level = 0;
+  // finish: 1 = column-split kernel (mppi_colfin_kernel) where it applies, 0 = the record tree
+  // (env MPPI_COLFIN=0)
+  int colfin = 1;
   // host-side step timeline (env MPPI_HOST_TRACE=1, printed by mppi_destroy): microseconds summed
   // over steps of [previous done seen -> entry, entry -> rollout enqueued, -> all enqueued, wait]
   bool trace = false;
@@ -500,18 +507,17 @@ int eps_for_step(mppi_ctx* c, const Plan& pl, uint64_t step, int* slot_out) {
   if (need > c->eps_cap) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipStreamSynchronize(c->noise_stream));
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kEpsSlots; ++i) {
       if (c->eps[i]) HIP_TRY(hipFree(c->eps[i]));
       c->eps[i] = nullptr;
       c->eps_step[i] = -1;
       c->eps_pending[i] = false;
     }
-    HIP_TRY(hipMalloc(&c->eps[0], need * sizeof(float)));
-    HIP_TRY(hipMalloc(&c->eps[1], need * sizeof(float)));
+    for (int i = 0; i < kEpsSlots; ++i) HIP_TRY(hipMalloc(&c->eps[i], need * sizeof(float)));
     c->eps_cap = need;
   }
   const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kEpsSlots; ++i) {
     if (c->eps_step[i] == (int64_t)step) {
       if (c->eps_pending[i]) {  // generated on noise_stream: order it before this rollout
         const hipError_t q = hipEventQuery(c->eps_ev[i]);
@@ -524,33 +530,58 @@ int eps_for_step(mppi_ctx* c, const Plan& pl, uint64_t step, int* slot_out) {
     }
   }
   // not precomputed: any in-flight speculative fill must finish before a slot is reused
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < kEpsSlots; ++i)
     if (c->eps_pending[i]) {
       HIP_TRY(hipStreamWaitEvent(c->stream, c->eps_ev[i], 0));
       c->eps_pending[i] = false;
     }
   const int slot = 0;
   HIP_TRY(launch_noise(c->p.seed, step * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[slot], c->stream));
+  for (int i = 0; i < kEpsSlots; ++i) c->eps_step[i] = -1;
   c->eps_step[slot] = (int64_t)step;
-  c->eps_step[slot ^ 1] = -1;
   *slot_out = slot;
   return MPPI_OK;
 }
 
-// After the rollout of `step` (which reads slot `used`) is enqueued: generate the
-// normals of step + 1 into the other slot on noise_stream, ordered after the previous
-// rollout (the last reader of that slot, ev_roll_done of the previous call).  The
-// noise workgroups cannot share a CU with a rollout workgroup (LDS reservation), so
-// they run on the CUs the rollout kernel has released while its finish completes.
+// A slot other than `used` that holds none of the steps in (step, step + ahead]: the
+// stalest one (its last reader is a rollout enqueued before the current one).
+int eps_victim(const mppi_ctx* c, int used, uint64_t step, int ahead) {
+  for (int i = 0; i < kEpsSlots; ++i) {
+    if (i == used) continue;
+    const int64_t s = c->eps_step[i];
+    if (s > (int64_t)step && s <= (int64_t)step + ahead) continue;
+    return i;
+  }
+  return -1;
+}
+
+// After the rollout of `step` (which reads slot `used`) is enqueued: make sure the normals
+// of steps step + 1 .. step + noise_ahead are generated or in flight, on noise_stream and
+// ordered after this rollout (every earlier reader of a reused slot precedes it on the
+// context stream).  In steady state that is one launch, of step + 2's normals, which then
+// has the finish, the host round trip and the whole next step to complete, so the next
+// rollout never waits for it (with one step ahead it raced the finish: profiles/r01_notes.md).
+// The noise workgroups run on the CUs the rollout kernel has released.
 int speculate_eps(mppi_ctx* c, const Plan& pl, uint64_t step, int used) {
-  const int other = used ^ 1;
   const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
-  HIP_TRY(hipStreamWaitEvent(c->noise_stream, c->ev_prev_roll, 0));
-  HIP_TRY(launch_noise(c->p.seed, (step + 1) * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[other],
-                       c->noise_stream));
-  HIP_TRY(hipEventRecord(c->eps_ev[other], c->noise_stream));
-  c->eps_step[other] = (int64_t)(step + 1);
-  c->eps_pending[other] = true;
+  bool waited = false;
+  for (int d = 1; d <= c->noise_ahead; ++d) {
+    const uint64_t target = step + (uint64_t)d;
+    bool have = false;
+    for (int i = 0; i < kEpsSlots; ++i) have |= c->eps_step[i] == (int64_t)target;
+    if (have) continue;
+    const int slot = eps_victim(c, used, step, c->noise_ahead);
+    if (slot < 0) return fail(MPPI_ESTATE, "no free noise slot");
+    if (!waited) {
+      HIP_TRY(hipStreamWaitEvent(c->noise_stream, c->ev_prev_roll, 0));
+      waited = true;
+    }
+    HIP_TRY(launch_noise(c->p.seed, target * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[slot],
+                         c->noise_stream));
+    HIP_TRY(hipEventRecord(c->eps_ev[slot], c->noise_stream));
+    c->eps_step[slot] = (int64_t)target;
+    c->eps_pending[slot] = true;
+  }
   return MPPI_OK;
 }
 
@@ -580,19 +611,23 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     a.tree_nodes = c->tree_nodes;
     a.noise_ctr = c->noise_ctr;
   }
-  int eps_slot = -1;
+  int eps_slot = -1, next_slot = -1;
   if (c->trace) c->tr_mark[0] = now_us();
   if (pl.pair && mode == 0 && pl.blocks > 0) {
     rc = eps_for_step(c, pl, step, &eps_slot);
     if (rc) return rc;
     a.eps = c->eps[eps_slot];
     if (fused && fused_level == 2 && !dump_args) {  // generated by the workgroups that finish early
-      a.eps_next = c->eps[eps_slot ^ 1];
+      next_slot = eps_victim(c, eps_slot, step, 0);
+      if (next_slot < 0) return fail(MPPI_ESTATE, "no free noise slot");
+      a.eps_next = c->eps[next_slot];
       a.n_base_next = (step + 1) * (uint64_t)((H_of(c) + 1) / 2);
-      c->eps_step[eps_slot ^ 1] = -1;  // being overwritten
-      if (c->eps_pending[eps_slot ^ 1]) {  // an earlier noise-stream fill of that slot
-        HIP_TRY(hipStreamWaitEvent(c->stream, c->eps_ev[eps_slot ^ 1], 0));
-        c->eps_pending[eps_slot ^ 1] = false;
+      for (int i = 0; i < kEpsSlots; ++i)  // the next step's normals come from this kernel only
+        if (c->eps_step[i] == (int64_t)(step + 1)) c->eps_step[i] = -1;
+      c->eps_step[next_slot] = -1;  // being overwritten
+      if (c->eps_pending[next_slot]) {  // an earlier noise-stream fill of that slot
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->eps_ev[next_slot], 0));
+        c->eps_pending[next_slot] = false;
       }
     }
   }
@@ -623,8 +658,8 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     c->ev_roll_pending = true;
   }
   if (a.eps_next) {  // the kernel leaves the next step's normals in the other slot
-    c->eps_step[eps_slot ^ 1] = (int64_t)(step + 1);
-    c->eps_pending[eps_slot ^ 1] = false;  // same stream: ordered before the next rollout
+    c->eps_step[next_slot] = (int64_t)(step + 1);
+    c->eps_pending[next_slot] = false;  // same stream: ordered before the next rollout
   } else if (eps_slot >= 0 && !dump_args) {
     // no fused epilogue: generate them on the noise stream after this rollout
     HIP_TRY(hipEventRecord(c->ev_prev_roll, c->stream));
@@ -695,6 +730,30 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
     if (rc) return rc;
     f.scratch0 = c->scratch0;
     f.scratch1 = c->scratch1;
+  }
+  // column-split finish (default): one launch, no partial-tree handoff between workgroups
+  int cf_P = 0, cf_ncol = 0, cf_groups = 0;
+  size_t cf_lds = 0;
+  if (c->colfin && !(f.mode == 1 && pl.fin_lds) && colfin_shape(n, H_of(c), &cf_P, &cf_ncol, &cf_groups, &cf_lds)) {
+    const size_t need = (size_t)E_of(c);  // f.level1 carries the 2H u_opt floats
+    if (c->level1_cap < 1 || c->level1_cap * (size_t)E_of(c) < need) {
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (c->level1) HIP_TRY(hipFree(c->level1));
+      c->level1 = nullptr;
+      HIP_TRY(hipMalloc(&c->level1, need * sizeof(double)));
+      c->level1_cap = 1;
+    }
+    f.level1 = c->level1;
+    f.level1_cnt = c->level1_cnt;
+    const size_t lds = std::max(cf_lds, f.mode == 0 ? (size_t)0 : pl.fin_lds_bytes);
+    if (timed && c->timing) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    HIP_TRY(launch_colfin(f, lds, c->stream, cf_P, cf_ncol, cf_groups));
+    if (timed && c->timing) {
+      HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+      c->ev_fin_pending = true;
+    }
+    if (f.mode == 2) return enqueue_tail(c, f, par);
+    return MPPI_OK;
   }
   // first tree level on ceil(n/16) workgroups (one per aligned group of 16 records)
   const int groups = n > 16 ? (n + 15) / 16 : 1;
@@ -948,6 +1007,8 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   c->device = device;
   if (const char* e = std::getenv("MPPI_FUSED_FINISH")) c->fused_level = std::min(std::max(std::atoi(e), 0), 2);
   if (const char* e = std::getenv("MPPI_HOST_TRACE")) c->trace = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MPPI_COLFIN")) c->colfin = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MPPI_NOISE_AHEAD")) c->noise_ahead = std::atoi(e) == 1 ? 1 : 2;
   if (const char* e = std::getenv("MPPI_WAVE_PRIO")) c->wave_prio = std::atoi(e) != 0;
   const char* ep = std::getenv("MPPI_STREAM_PRIO");
   const bool use_prio = !(ep && std::atoi(ep) == 0);
@@ -991,7 +1052,8 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipEventCreateWithFlags(&c->ev_roll_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_prev_roll, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->eps_ev[0], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->eps_ev[1], hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&c->eps_ev[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->eps_ev[2], hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "side stream / event creation failed"));
   c->out_host = new float[16 * H]();
   std::memset(c->stage, 0, 16 * H * sizeof(float));
@@ -1040,7 +1102,7 @@ void mppi_destroy(mppi_ctx* c) {
     if (c->ev_tail[i]) hipEventDestroy(c->ev_tail[i]);
   }
   if (c->ev_fin_done) hipEventDestroy(c->ev_fin_done);
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kEpsSlots; ++i) {
     if (c->eps[i]) hipFree(c->eps[i]);
     if (c->eps_ev[i]) hipEventDestroy(c->eps_ev[i]);
   }

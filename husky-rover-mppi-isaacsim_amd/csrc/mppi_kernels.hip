@@ -1790,6 +1790,9 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 // (MPPI_isaac.py:672-692) and the 3D rollout of the optimal sequence (:696-720):
 // only the serial chain (chain3d) runs on one lane, sin/cos, heights and wheel
 // contacts are computed by all lanes around it.
+#ifndef MPPI_FIN_PRIO
+#define MPPI_FIN_PRIO 0
+#endif
 constexpr int FIN_THREADS = 1024;
 constexpr int FIN_LDS_NODES = 16;
 constexpr int FIN_GROUP_CHUNK = 64;    // groups per scale-table fill (15 PairScale + 16 m each)
@@ -2058,6 +2061,9 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
 template <bool LDS>
 __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishArgs f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+#if MPPI_FIN_PRIO
+  __builtin_amdgcn_s_setprio(3);
+#endif
   const int tid = threadIdx.x;
   const int H = f.H;
   const int E = 2 * H + 2;
@@ -2261,6 +2267,153 @@ root_ready:
   const float ures = (tid < 2 * H && S > 0.0) ? (float)(lnode[2 + tid] / S) : 0.0f;
   __syncthreads();  // lnode is dead from here on
   finish_phase2<LDS>(f, ures, smem_raw, tid, FIN_THREADS);
+}
+
+// ---------------------------------------------------------------------  column-split finish
+// The same tree as mppi_finish_kernel (D2: binary, adjacent pairs, leaves padded with
+// empty records to a power of two P >= 16; an empty member passes its partner through,
+// so the padding does not change the root), split by COLUMN instead of by record: every
+// workgroup builds the whole pair-scale table from the n leaf minima (it depends on
+// nothing else) and reduces its own slice of the 2H+2 columns over all n records.  No
+// workgroup waits for another's partial tree; the only handoff is the u_opt slice each
+// stores before the device-scope counter, and the last workgroup to arrive runs phase 2.
+// One round trip through global memory instead of two (level 1, then the last group) or
+// more (n > 256), and every level but the 4 in registers is an LDS pass.
+// LDS: PairScale[P - 1] | m[P] | m[P / 2] | partial[ncol + 1][P / 16] doubles.
+constexpr int COLFIN_PMAX = 4096;  // leaf records (K <= 1,048,576 per context)
+__device__ __forceinline__ int colfin_level_base(int P, int l) { return P - (P >> l); }
+
+__global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishArgs f, int P, int ncol) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+#if MPPI_FIN_PRIO
+  __builtin_amdgcn_s_setprio(3);  // the serial step path outranks the next step's noise waves
+#endif
+#ifdef MPPI_STAMPS
+  if (blockIdx.x == 0) FIN_STAMP(0);
+#endif
+  const int tid = threadIdx.x;
+  const int H = f.H;
+  const int E = 2 * H + 2;
+  const int n = f.n_recs;
+  const double* recs = f.recs;
+  PairScale* lps = reinterpret_cast<PairScale*>(smem_raw);
+  float* mA = reinterpret_cast<float*>(lps + (P - 1));
+  float* mB = mA + P;
+  double* part = reinterpret_cast<double*>(mB + P / 2);  // [ncol + 1][P / 16], 8-byte aligned (P >= 16)
+  // this workgroup's columns: [c0, c1) plus column 1 (S) as slot ncol when c0 > 1
+  const int c0 = (int)blockIdx.x * ncol;
+  const int c1 = min(E, c0 + ncol);
+  const int nc = c1 - c0;
+  const bool extra_s = c0 > 1;
+  const int ncols = nc + (extra_s ? 1 : 0);
+  const int NG = P >> 4;  // register groups of 16 leaves per column
+  // (1) leaf values of (column, group) items in registers; loads issued before the scale
+  //     table is built so their latency overlaps it
+  const int items = ncols * NG;
+  const int it_c = tid % ncols, it_g = tid / ncols;
+  const bool has_item = tid < items;
+  const int col = (it_c < nc) ? c0 + it_c : 1;
+  double v[16];
+  if (has_item) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = min(16 * it_g + i, n - 1);
+      v[i] = recs[(size_t)r * E + col];
+    }
+  }
+  for (int i = tid; i < P; i += FIN_THREADS) mA[i] = (i < n) ? (float)recs[(size_t)i * E] : INFINITY;
+  __syncthreads();
+  // (2) pair scales, level by level (level l has P >> (l + 1) pairs)
+  float* src = mA;
+  float* dst = mB;
+  for (int l = 0; (P >> (l + 1)) >= 1; ++l) {
+    const int w = P >> (l + 1);
+    const int base = colfin_level_base(P, l);
+    for (int i = tid; i < w; i += FIN_THREADS) {
+      const PairScale ps = pair_scale(src[2 * i], src[2 * i + 1], f.T);
+      lps[base + i] = ps;
+      dst[i] = ps.m;
+    }
+    __syncthreads();
+    float* t = src;
+    src = dst;
+    dst = t;
+  }
+#ifdef MPPI_STAMPS
+  if (blockIdx.x == 0) FIN_STAMP(9);
+#endif
+  // (3) the 4 lowest levels of every item in registers
+  if (has_item) {
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const int w = 8 >> l;
+      const PairScale* ps = lps + colfin_level_base(P, l) + it_g * w;
+#pragma unroll
+      for (int i = 0; i < w; ++i) v[i] = pair_apply(ps[i], v[2 * i], v[2 * i + 1], col);
+    }
+    part[it_c * NG + it_g] = v[0];
+  }
+  __syncthreads();
+  // (4) the remaining log2(NG) levels in LDS, in place (stride doubling)
+  int lvl = 4;
+  for (int stride = 1; stride < NG; stride *= 2, ++lvl) {
+    const int w = NG / (2 * stride);
+    const PairScale* ps = lps + colfin_level_base(P, lvl);
+    for (int it = tid; it < ncols * w; it += FIN_THREADS) {
+      const int c = it % ncols, i = it / ncols;
+      const int cc = (c < nc) ? c0 + c : 1;
+      double* pc = part + c * NG;
+      pc[2 * stride * i] = pair_apply(ps[i], pc[2 * stride * i], pc[2 * stride * i + stride], cc);
+    }
+    __syncthreads();
+  }
+#ifdef MPPI_STAMPS
+  if (blockIdx.x == 0) FIN_STAMP(10);
+#endif
+  // root of slot c: part[c * NG]
+  if (f.mode == 0) {
+    for (int c = tid; c < nc; c += FIN_THREADS) f.record_out[c0 + c] = part[c * NG];
+    return;
+  }
+  const double S = extra_s ? part[nc * NG] : part[(1 - c0) * NG];
+  // u_opt of this slice (columns 2 + t), stored write-through at device scope, then the count
+  for (int c = tid; c < nc; c += FIN_THREADS) {
+    const int j = c0 + c;
+    if (j >= 2) {
+      const float u = (S > 0.0) ? (float)(part[c * NG] / S) : 0.0f;
+      __hip_atomic_store(reinterpret_cast<float*>(f.level1) + (j - 2), u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (gridDim.x > 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(mA);
+    if (tid == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(f.level1_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == gridDim.x - 1;
+      if (last) __hip_atomic_store(f.level1_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#ifdef MPPI_STAMPS
+  FIN_STAMP(13);
+#endif
+  const float ures = (tid < 2 * H)
+                         ? __hip_atomic_load(reinterpret_cast<const float*>(f.level1) + tid, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)
+                         : 0.0f;
+  __syncthreads();  // the tree's LDS is dead from here on
+#ifdef MPPI_STAMPS
+  FIN_STAMP(6);
+  FIN_STAMP(1);
+#endif
+  finish_phase2<false>(f, ures, smem_raw, tid, FIN_THREADS);
 }
 
 // Deferred optimal rollout (MPPI_isaac.py:696-720) of the sequence a mode-2
@@ -2625,6 +2778,29 @@ hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool u
     hipLaunchKernelGGL(mppi_finish_kernel<true>, dim3(groups), dim3(FIN_THREADS), lds, st, f);
   else
     hipLaunchKernelGGL(mppi_finish_kernel<false>, dim3(groups), dim3(FIN_THREADS), lds, st, f);
+  return hipGetLastError();
+}
+
+// Column-split finish (mppi_colfin_kernel): P = leaves padded to a power of two >= 16,
+// ncol columns per workgroup; returns the LDS bytes the tree needs in *lds_tree.
+int colfin_shape(int n, int H, int* P_out, int* ncol_out, int* groups_out, size_t* lds_tree) {
+  if (n < 1 || n > COLFIN_PMAX) return 0;
+  int P = 16;
+  while (P < n) P *= 2;
+  const int E = 2 * H + 2;
+  // about 64 workgroups, at least 2 columns each
+  const int ncol = std::max(2, (E + 63) / 64);
+  const int groups = (E + ncol - 1) / ncol;
+  *P_out = P;
+  *ncol_out = ncol;
+  *groups_out = groups;
+  *lds_tree = (size_t)(P - 1) * sizeof(PairScale) + (size_t)(P + P / 2) * sizeof(float) +
+              (size_t)(ncol + 1) * (P / 16) * sizeof(double);
+  return 1;
+}
+
+hipError_t launch_colfin(const FinishArgs& f, size_t lds, hipStream_t st, int P, int ncol, int groups) {
+  hipLaunchKernelGGL(mppi_colfin_kernel, dim3(groups), dim3(FIN_THREADS), lds, st, f, P, ncol);
   return hipGetLastError();
 }
 
