@@ -51,6 +51,7 @@ struct Plan {
   int wx0 = 0, wy0 = 0, W = 1, Wr = 1;
   size_t lds_bytes = 0, fin_lds_bytes = 0, fin_tree_bytes = 0;
   int fin_win_offset = 0;
+  int ucache_steps = 0;   // pair kernel: steps whose sampled controls stay in LDS for the leaf
 };
 
 }  // namespace
@@ -118,6 +119,9 @@ struct mppi_ctx {
   // finish: 1 = column-split kernel (mppi_colfin_kernel) where it applies, 0 = the record tree
   // (env MPPI_COLFIN=0)
   int colfin = 1;
+  // pair kernel: keep the first steps' sampled controls in spare LDS for the leaf reduction
+  // (env MPPI_UCACHE=0: re-read every normals row)
+  int ucache = 1;
   // host-side step timeline (env MPPI_HOST_TRACE=1, printed by mppi_destroy): microseconds summed
   // over steps of [previous done seen -> entry, entry -> rollout enqueued, -> all enqueued, wait]
   bool trace = false;
@@ -279,6 +283,18 @@ Plan make_plan(const mppi_ctx* c) {
     pl.lds_bytes = pl.pair ? (size_t)(6 * PAIR_RING + 1) * TB * sizeof(float) + 4 * (TB / 64) * sizeof(int) +
                                  (size_t)((2 * H + 3) & ~3) * sizeof(float) + scratch_ws
                            : (size_t)15 * TB * sizeof(float) + scratch_ws;
+    if (pl.pair && c->ucache) {
+      // the rest of the CU's LDS keeps the sampled controls of the first steps ([2][T][TB]
+      // floats, 16-byte aligned after the scratch), so the leaf reduction re-reads only the
+      // other steps' normals from HBM (all workgroups reduce at once: a bandwidth burst)
+      // room is left for the deferred optimal rollout of the previous step (mppi_tail_kernel,
+      // 15H floats), which runs beside a rollout workgroup on one CU
+      const size_t base = (pl.lds_bytes + 15) / 16 * 16;
+      const size_t row2 = (size_t)2 * (TB + 4) * sizeof(float);  // UCACHE_ROW: one float4 of bank skew
+      const size_t budget = kLdsBytes - ((size_t)15 * H * sizeof(float) + 2047) / 1024 * 1024;
+      pl.ucache_steps = base < budget ? (int)std::min<size_t>((size_t)H, (budget - base) / row2) : 0;
+      if (pl.ucache_steps > 0) pl.lds_bytes = base + (size_t)pl.ucache_steps * row2;
+    }
   }
   // finish kernel: tree phase [16][2H+2] doubles + 64 x (15 PairScale + 16 m); phase 2
   // uo[2H] v[H] w[H] sin[H] cos[H] chain[12H] out[16H] floats, then the DEM window
@@ -330,6 +346,7 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   const int H = p.num_iterations;
   std::memset(&a, 0, sizeof(a));
   a.K = p.num_trajectories;
+  a.ucache_steps = pl.ucache_steps;
   a.k_offset = p.k_offset;
   a.H = H;
   a.Z = c->Z;
@@ -1008,6 +1025,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   if (const char* e = std::getenv("MPPI_FUSED_FINISH")) c->fused_level = std::min(std::max(std::atoi(e), 0), 2);
   if (const char* e = std::getenv("MPPI_HOST_TRACE")) c->trace = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_COLFIN")) c->colfin = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MPPI_UCACHE")) c->ucache = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_NOISE_AHEAD")) c->noise_ahead = std::atoi(e) == 1 ? 1 : 2;
   if (const char* e = std::getenv("MPPI_WAVE_PRIO")) c->wave_prio = std::atoi(e) != 0;
   const char* ep = std::getenv("MPPI_STREAM_PRIO");

@@ -619,9 +619,13 @@ __device__ __forceinline__ double group_apply(const PairScale* ps, const double 
   return cur[0];
 }
 
+// LDS row stride (floats) of the pair kernel's control cache: 256 trajectories + one float4 of
+// skew, so the leaf's lanes (one row each) hit different banks
+constexpr int UCACHE_ROW = 256 + 4;
 template <int TB, int NT, bool EPS = false>
 __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
-                                             unsigned char* scratch, const float* ub_block);
+                                             unsigned char* scratch, const float* ub_block,
+                                             const float* ucache = nullptr, int uc_steps = 0);
 
 // =====================================================================  rollout kernel
 // Everything one trajectory carries from step to step.
@@ -854,7 +858,8 @@ __global__ __launch_bounds__(BLOCK) void mppi_rollout_kernel(const RolloutArgs a
 // TB*4 + TB/64*4 (rounded to 16) + TB/256*(2H+2)*8 bytes.
 template <int TB, int NT, bool EPS>
 __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
-                                             unsigned char* scratch, const float* ub_block) {
+                                             unsigned char* scratch, const float* ub_block,
+                                             const float* ucache, int uc_steps) {
   constexpr int NL = TB / 256;
   constexpr int NWL = TB / 64;   // waves' worth of trajectories
   const int tid = threadIdx.x, lane = tid & 63;
@@ -893,6 +898,7 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
     const float4* u4 = reinterpret_cast<const float4*>(ub_block + (size_t)(j >= 2 ? j - 2 : 0) * TB +
                                                        256 * leaf + 128 * half);
     float nom = 0.f, sg = 0.f, lo = 0.f, hi = 0.f;
+    bool cached = false;  // the sampled controls of this row are in LDS (no normals re-read)
     if constexpr (EPS) {  // rows hold the normals: u = clamp(u_nom[t+1] + sigma*eps) as sampled
       const int c = (j - 2) >= H ? 1 : 0;
       const int t = max(j - 2, 0) - c * H;
@@ -901,6 +907,11 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
       sg = c ? a.s2 : a.s1;
       lo = c ? a.min_u2 : a.min_u1;
       hi = c ? a.max_u2 : a.max_u1;
+      if (j >= 2 && t < uc_steps) {
+        cached = true;
+        u4 = reinterpret_cast<const float4*>(ucache + (size_t)(c * uc_steps + t) * UCACHE_ROW + 256 * leaf +
+                                             128 * half);
+      }
     }
     // the half-row's pairwise tree = ((line0 + line1) + (line2 + line3)), each line (8 float4
     // groups, 32 trajectories) a pairwise tree of its own; one line in registers at a time
@@ -915,7 +926,7 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
       for (int g = 0; g < 8; ++g) {
         const float4 w = w4[8 * line + g];
         float4 u = uq[g];
-        if constexpr (EPS) {
+        if (EPS && !cached) {
           u.x = clampf(nom + sg * u.x, lo, hi);
           u.y = clampf(nom + sg * u.y, lo, hi);
           u.z = clampf(nom + sg * u.z, lo, hi);
@@ -1445,6 +1456,12 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   int* flags = reinterpret_cast<int*>(cost_lds + TB);    // [4][NWC]: produced, chained, consumed, -
   float* unom_lds = reinterpret_cast<float*>(flags + 4 * NWC);  // [2H] u_nom1 | u_nom2 (padded to 4)
   unsigned char* scratch = reinterpret_cast<unsigned char*>(unom_lds + ((2 * a.H + 3) & ~3));
+  static_assert(TB == 256, "UCACHE_ROW assumes 256 trajectories per workgroup");
+  // sampled controls of steps [0, ucache_steps) for leaf_records: [2][ucache_steps][UCACHE_ROW] after
+  // the leaf scratch (layout of make_plan in mppi_capi.cpp)
+  float* ucache = reinterpret_cast<float*>(
+      smem_raw + ((size_t)(scratch - smem_raw) + ((TB + TB / 64) * 4 + 15) / 16 * 16 +
+                  (size_t)(TB / 256) * (2 * a.H + 2) * sizeof(double) + 15) / 16 * 16);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool side = wave >= NWC;
@@ -1623,6 +1640,10 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
           const int ti = min(p + 1, H - 1);
           u1 = clampf(unom_lds[ti] + a.s1 * e1r, a.min_u1, a.max_u1);
           u2 = clampf(unom_lds[H + ti] + a.s2 * e2r, a.min_u2, a.max_u2);
+          if (p < a.ucache_steps) {  // kept for the leaf reduction (uniform branch)
+            ucache[(size_t)p * UCACHE_ROW + tj] = u1;
+            ucache[(size_t)(a.ucache_steps + p) * UCACHE_ROW + tj] = u2;
+          }
         } else {
           const size_t o = (size_t)(valid ? kl : 0) * H + p;
           u1 = a.inj_u1[o];
@@ -1756,7 +1777,8 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 #endif
   __syncthreads();
   if constexpr (MODE == 0)  // rows hold the normals; the leaf recomputes the sampled controls
-    leaf_records<TB, NT, true>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB);
+    leaf_records<TB, NT, true>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB, ucache,
+                               a.ucache_steps);
   else
     leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
   if constexpr (!DUMP) {

@@ -69,6 +69,9 @@ def main():
     side = a[:, 4:].reshape(-1, 2) / phases
     lf = allv[64 * 16 * 6 + 1024 * 2: 64 * 16 * 6 + 1024 * 2 + 64 * 8].reshape(64, 8)[:nb]
     fs = allv[64 * 16 * 6 + 1024 * 2 + 64 * 8:][:16]
+    if lf[:, 4].max() > 0:  # leaf_records stamps (thread 0 of each block, s_memtime cycles)
+        print(f"  leaf records (cyc): weights {np.mean(lf[:, 1] - lf[:, 0]):8.0f}  "
+              f"rows {np.mean(lf[:, 4] - lf[:, 1]):8.0f}  (block 0 total {lf[0, 4] - lf[0, 0]:.0f})")
     us = lambda a, b: (fs[b] - fs[a]) / 100.0  # s_memrealtime: 100 MHz, comparable across CUs
     if fs[13] > 0:
         print(f"  finish level1 (us): scales {us(0, 9):.1f}  apply+store {us(9, 10):.1f}  count {us(10, 13):.1f}; "
