@@ -111,6 +111,13 @@ struct mppi_ctx {
   hipEvent_t eps_ev[kEpsSlots] = {nullptr, nullptr, nullptr};
   bool eps_pending[kEpsSlots] = {false, false, false};
   int noise_ahead = 2;  // steps of normals generated ahead (env MPPI_NOISE_AHEAD=1: the next only)
+  // where the noise stream is handed the steps ahead: 0 = after the rollout launch (beside the
+  // finish), 1 = after the finish launch (env MPPI_NOISE_AT)
+  int noise_at = 0;
+  bool spec_pending = false;
+  Plan spec_plan;
+  uint64_t spec_step = 0;
+  int spec_slot = 0;
   hipStream_t noise_stream = nullptr;
   int prio_least = 0, prio_greatest = 0;
   // tree levels inside the rollout kernel (MPPI_FUSED_FINISH): 0 none (default: measured fastest
@@ -122,6 +129,7 @@ struct mppi_ctx {
   // pair kernel: keep the first steps' sampled controls in spare LDS for the leaf reduction
   // (env MPPI_UCACHE=0: re-read every normals row)
   int ucache = 1;
+  int num_cus = 256;  // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   // host-side step timeline (env MPPI_HOST_TRACE=1, printed by mppi_destroy): microseconds summed
   // over steps of [previous done seen -> entry, entry -> rollout enqueued, -> all enqueued, wait]
   bool trace = false;
@@ -283,7 +291,9 @@ Plan make_plan(const mppi_ctx* c) {
     pl.lds_bytes = pl.pair ? (size_t)(6 * PAIR_RING + 1) * TB * sizeof(float) + 4 * (TB / 64) * sizeof(int) +
                                  (size_t)((2 * H + 3) & ~3) * sizeof(float) + scratch_ws
                            : (size_t)15 * TB * sizeof(float) + scratch_ws;
-    if (pl.pair && c->ucache) {
+    // only at one workgroup per CU: the cache takes the CU's spare LDS, which at larger K
+    // (C5: 4 workgroups per CU) would cost a co-resident rollout workgroup instead
+    if (pl.pair && c->ucache && pl.blocks <= c->num_cus) {
       // the rest of the CU's LDS keeps the sampled controls of the first steps ([2][T][TB]
       // floats, 16-byte aligned after the scratch), so the leaf reduction re-reads only the
       // other steps' normals from HBM (all workgroups reduce at once: a bandwidth burst)
@@ -602,6 +612,17 @@ int speculate_eps(mppi_ctx* c, const Plan& pl, uint64_t step, int used) {
   return MPPI_OK;
 }
 
+// MPPI_NOISE_AT=1: the normals of the steps ahead are generated after the step's finish
+// rather than beside it, so the finish's serial phase (one wave) shares no SIMD with the
+// noise waves; with two steps of look-ahead the noise still has the host round trip and the
+// whole next rollout (at low priority, beside it) before it is needed.
+int flush_speculation(mppi_ctx* c) {
+  if (!c->spec_pending) return MPPI_OK;
+  c->spec_pending = false;
+  HIP_TRY(hipEventRecord(c->ev_prev_roll, c->stream));
+  return speculate_eps(c, c->spec_plan, c->spec_step, c->spec_slot);
+}
+
 // Enqueue the rollout kernel for the current state / nominal sequence.
 int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl,
                     const float* unom, const mppi_state& st, const RolloutArgs* dump_args,
@@ -629,6 +650,8 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     a.noise_ctr = c->noise_ctr;
   }
   int eps_slot = -1, next_slot = -1;
+  rc = flush_speculation(c);  // a speculation no finish has flushed (dump / injected paths)
+  if (rc) return rc;
   if (c->trace) c->tr_mark[0] = now_us();
   if (pl.pair && mode == 0 && pl.blocks > 0) {
     rc = eps_for_step(c, pl, step, &eps_slot);
@@ -679,6 +702,13 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     c->eps_pending[next_slot] = false;  // same stream: ordered before the next rollout
   } else if (eps_slot >= 0 && !dump_args) {
     // no fused epilogue: generate them on the noise stream after this rollout
+    if (c->noise_at == 1) {  // ... after the finish the caller enqueues next (flush_speculation)
+      c->spec_pending = true;
+      c->spec_plan = pl;
+      c->spec_step = step;
+      c->spec_slot = eps_slot;
+      return MPPI_OK;
+    }
     HIP_TRY(hipEventRecord(c->ev_prev_roll, c->stream));
     return speculate_eps(c, pl, step, eps_slot);
   }
@@ -885,6 +915,8 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   remember(c, proj, step, mode, pl);
   rc = enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 1, nullptr, true);
   if (rc) return rc;
+  rc = flush_speculation(c);
+  if (rc) return rc;
   if (!c->trace) return copy_outputs(c, out);
   const double t2 = now_us();
   rc = copy_outputs(c, out);
@@ -1022,11 +1054,17 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   mppi_ctx* c = new mppi_ctx();
   c->p = p;
   c->device = device;
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+      c->num_cus = cus;
+  }
   if (const char* e = std::getenv("MPPI_FUSED_FINISH")) c->fused_level = std::min(std::max(std::atoi(e), 0), 2);
   if (const char* e = std::getenv("MPPI_HOST_TRACE")) c->trace = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_COLFIN")) c->colfin = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_UCACHE")) c->ucache = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_NOISE_AHEAD")) c->noise_ahead = std::atoi(e) == 1 ? 1 : 2;
+  if (const char* e = std::getenv("MPPI_NOISE_AT")) c->noise_at = std::atoi(e) == 1 ? 1 : 0;
   if (const char* e = std::getenv("MPPI_WAVE_PRIO")) c->wave_prio = std::atoi(e) != 0;
   const char* ep = std::getenv("MPPI_STREAM_PRIO");
   const bool use_prio = !(ep && std::atoi(ep) == 0);
@@ -1342,6 +1380,8 @@ int mppi_step_finish(mppi_ctx* c, const double* records_dev, int32_t n, mppi_out
   if (!records_dev || n < 1) return fail(MPPI_EINVAL, "records required");
   const Plan pl = c->have_last ? c->last_plan : make_plan(c);
   rc = enqueue_finish(c, pl, c->st, records_dev, n, 1, nullptr, true);
+  if (rc) return rc;
+  rc = flush_speculation(c);
   if (rc) return rc;
   return copy_outputs(c, out);
 }
