@@ -115,6 +115,7 @@ struct mppi_ctx {
   // finish), 1 = after the finish launch (env MPPI_NOISE_AT)
   int noise_at = 0;
   bool spec_pending = false;
+  bool prev_roll_valid = false;  // MPPI_NOISE_AT=2: ev_prev_roll marks the previous rollout
   Plan spec_plan;
   uint64_t spec_step = 0;
   int spec_slot = 0;
@@ -697,6 +698,21 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     c->ev_roll_pending = true;
   }
+  if (c->noise_at == 2) {
+    // MPPI_NOISE_AT=2: the steps ahead go to the noise stream ordered after the PREVIOUS
+    // rollout only (the last reader of a reused slot; ev_prev_roll still marks it here), so
+    // the noise kernel runs beside this rollout, in its idle issue slots, instead of beside
+    // the finish.  The host calls come after the rollout launch (they are not on its path).
+    bool spec_done = false;
+    if (eps_slot >= 0 && !dump_args && !a.eps_next && c->prev_roll_valid) {
+      rc = speculate_eps(c, pl, step, eps_slot);
+      if (rc) return rc;
+      spec_done = true;
+    }
+    HIP_TRY(hipEventRecord(c->ev_prev_roll, c->stream));  // the last reader for the next call
+    c->prev_roll_valid = true;
+    if (spec_done) return MPPI_OK;
+  }
   if (a.eps_next) {  // the kernel leaves the next step's normals in the other slot
     c->eps_step[next_slot] = (int64_t)(step + 1);
     c->eps_pending[next_slot] = false;  // same stream: ordered before the next rollout
@@ -1064,7 +1080,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   if (const char* e = std::getenv("MPPI_COLFIN")) c->colfin = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_UCACHE")) c->ucache = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_NOISE_AHEAD")) c->noise_ahead = std::atoi(e) == 1 ? 1 : 2;
-  if (const char* e = std::getenv("MPPI_NOISE_AT")) c->noise_at = std::atoi(e) == 1 ? 1 : 0;
+  if (const char* e = std::getenv("MPPI_NOISE_AT")) c->noise_at = std::min(std::max(std::atoi(e), 0), 2);
   if (const char* e = std::getenv("MPPI_WAVE_PRIO")) c->wave_prio = std::atoi(e) != 0;
   const char* ep = std::getenv("MPPI_STREAM_PRIO");
   const bool use_prio = !(ep && std::atoi(ep) == 0);
