@@ -1,0 +1,61 @@
+"""GPU: the engine's scheduling variants are bitwise identical to the default path.
+
+Each toggle below changes only WHERE or WHEN work runs, never the arithmetic:
+  MPPI_COLFIN=0     finish by the record tree (mppi_finish_kernel) instead of the
+                    column-split kernel
+  MPPI_UCACHE=0     leaf reduction re-reads every normals row instead of the LDS-cached controls
+  MPPI_NOISE_AT=1/2 noise of the steps ahead launched after the finish / beside the rollout
+  MPPI_NOISE_AHEAD=1  normals generated one step ahead instead of two
+The toggles are read when a context is created, so each variant gets its own engine.
+Sizes: n = 256 leaf records (C3 K) and n = 1024 (C5 K) at a short horizon.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("u1_opt", "u2_opt", "lin_vel", "ang_vel")
+
+
+def _run(env, K, H, steps=3):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from mppi_amd import _lib, scene
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        eng = _lib.Engine(_lib.make_params(K, H), 0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    Z, hw, cm = scene.scene_c3()
+    eng.set_dem(Z, hw)
+    eng.set_costmap(cm, hw)
+    eng.set_state(_lib.make_state(-60.0, -5.0, (1.0, 0.0, 0.0), goal_x=65.0, goal_y=10.0))
+    outs = []
+    for i in range(steps):
+        o = eng.step("3d", i)
+        outs.append({k: o[k].copy() for k in KEYS})
+    costs = eng.costs()
+    eng.close()
+    return outs, costs
+
+
+@pytest.mark.parametrize("K,H", [(65536, 24), (262144, 16)])
+@pytest.mark.parametrize("env", [{"MPPI_COLFIN": "0"}, {"MPPI_UCACHE": "0"}, {"MPPI_NOISE_AT": "1"},
+                                 {"MPPI_NOISE_AT": "2"}, {"MPPI_NOISE_AHEAD": "1"}],
+                         ids=["record-tree", "no-ucache", "noise-after-finish", "noise-beside-rollout",
+                              "noise-one-ahead"])
+def test_variant_bitwise_equal(K, H, env):
+    ref, ref_costs = _run({}, K, H)
+    got, got_costs = _run(env, K, H)
+    np.testing.assert_array_equal(got_costs, ref_costs)
+    for i, (a, b) in enumerate(zip(got, ref)):
+        for k in KEYS:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=f"step {i} {k} {env}")
