@@ -1420,7 +1420,7 @@ __device__ __forceinline__ void noise_ahead(const RolloutArgs& a, unsigned char*
 // with L = PAIR_LAG; deadlock-free for 0 < L < D (the chain's waits are always
 // satisfied by side iterations that do not wait on it).  Bitwise identical results.
 #ifndef MPPI_PAIR_LAG
-#define MPPI_PAIR_LAG 4
+#define MPPI_PAIR_LAG 6  // measured: 6 beats 2 and 4 at D = 8 (profiles/r01_notes.md)
 #endif
 #ifndef MPPI_FLAG_CACHE
 #define MPPI_FLAG_CACHE 1  // diagnostic builds: 0 = read the partner's counter at every wait
