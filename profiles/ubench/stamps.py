@@ -14,12 +14,12 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 PKG = os.path.join(ROOT, "husky-rover-mppi-isaacsim_amd")
 sys.path[:0] = [ROOT, PKG]
-SO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmppi_hip_stamps.so")
+SO = os.environ.get("MPPI_STAMPS_SO") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmppi_hip_stamps.so")
 
 
 def build():
     csrc = os.path.join(PKG, "csrc")
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
            "-fPIC", "-shared", "-DMPPI_STAMPS", f"-I{ROOT}/include", f"-I{csrc}", "-x", "hip",
            *[os.path.join(csrc, f) for f in ("mppi_kernels.hip", "mppi_costmap.hip", "mppi_python25d.hip",
                                             "mppi_capi.cpp")], "-o", SO]
