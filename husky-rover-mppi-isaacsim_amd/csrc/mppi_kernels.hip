@@ -1,15 +1,18 @@
 // MI355X (gfx950) MPPI rollout-and-cost engine: kernels.
 //
 // One MPPI step (reference: thesis_master/warp_implementation/MPPI_isaac.py:505-720,
-// nine Warp launches) runs here as two kernels:
+// nine Warp launches) runs here as:
 //
-//   mppi_rollout_kernel  (#1-#7 fused)  one lane per sampled trajectory; Philox
-//       noise, wheel filter, 2.5D rollout on the DEM (staged once per workgroup
-//       into LDS), the four critics accumulated online, then the workgroup's
-//       softmax leaf records (min, sum w, sum w*u[t]) -> one float64 record per
-//       workgroup.  Per (k, t) only the sampled controls touch memory.
-//   mppi_finish_kernel   (#7-#9)  one workgroup; binary tree over the records,
-//       u_opt = V/S, optimal-sequence filter and the 3D rollout of it.
+//   mppi_rollout_pair_kernel (#1-#7 fused)  256 trajectories per workgroup: chain waves
+//       run the serial 2.5D projection, side waves the sampling, wheel filter, wheel
+//       contacts and the four critics, paired through LDS rings; then the workgroup's
+//       softmax leaf record (min, sum w, sum w*u[t]) in float64.
+//   mppi_colfin_kernel (#7-#9)  column-split tree over the records, u_opt = V/S, the
+//       optimal-sequence filter and the first optimal-rollout step; outputs to host memory.
+//   mppi_tail_kernel  the rest of the optimal rollout, on a side stream.
+//   mppi_noise_kernel the Philox sampling normals, two steps ahead, on a side stream.
+// The earlier single-role kernels (mppi_rollout_kernel, mppi_rollout_ws_kernel,
+// mppi_finish_kernel) remain selectable (mppi_set_dem_path, MPPI_COLFIN=0) and tested.
 //
 // Numerics: compile with -ffp-contract=off.  Every float op is one IEEE f32
 // operation in the reference's source order; transcendentals come from
