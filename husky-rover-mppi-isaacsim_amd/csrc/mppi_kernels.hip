@@ -2002,12 +2002,25 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
     float L = f.wl, R = f.wr;
     float myL = 0.0f, myR = 0.0f;
     int t = 0;
-    for (; t + 8 <= H; t += 8) {
-      float i1[8], i2[8];
+    // the next block's inputs are read while this block's recurrence runs (one LDS latency
+    // per block would otherwise sit on the serial path)
+    float i1[8], i2[8];
+    if (H >= 8) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        i1[k] = uo[t + k];
-        i2[k] = uo[H + t + k];
+        i1[k] = uo[k];
+        i2[k] = uo[H + k];
+      }
+    }
+    for (; t + 8 <= H; t += 8) {
+      float n1[8], n2[8];
+      const bool more = t + 16 <= H;  // wave-uniform
+      if (more) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          n1[k] = uo[t + 8 + k];
+          n2[k] = uo[H + t + 8 + k];
+        }
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -2020,6 +2033,13 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
       if (((t + 8) & 63) == 0) {
         vb[t + 8 - 64 + lane] = myL;
         wb[t + 8 - 64 + lane] = myR;
+      }
+      if (more) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          i1[k] = n1[k];
+          i2[k] = n2[k];
+        }
       }
     }
     for (; t < H; ++t) {
@@ -2304,7 +2324,7 @@ root_ready:
 // stores before the device-scope counter, and the last workgroup to arrive runs phase 2.
 // One round trip through global memory instead of two (level 1, then the last group) or
 // more (n > 256), and every level but the 4 in registers is an LDS pass.
-// LDS: PairScale[P - 1] | m[P] | m[P / 2] | partial[ncol + 1][P / 16] doubles.
+// LDS: PairScale[P - 1] | node minima m[2P] (all levels) | partial[ncol + 1][P / 16] doubles.
 constexpr int COLFIN_PMAX = 4096;  // leaf records (K <= 1,048,576 per context)
 __device__ __forceinline__ int colfin_level_base(int P, int l) { return P - (P >> l); }
 
@@ -2322,9 +2342,8 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
   const int n = f.n_recs;
   const double* recs = f.recs;
   PairScale* lps = reinterpret_cast<PairScale*>(smem_raw);
-  float* mA = reinterpret_cast<float*>(lps + (P - 1));
-  float* mB = mA + P;
-  double* part = reinterpret_cast<double*>(mB + P / 2);  // [ncol + 1][P / 16], 8-byte aligned (P >= 16)
+  float* mlev = reinterpret_cast<float*>(lps + (P - 1));  // node minima, level l at 2P - (2P >> l)
+  double* part = reinterpret_cast<double*>(mlev + 2 * P);  // [ncol + 1][P / 16], 8-byte aligned (P >= 16)
   // this workgroup's columns: [c0, c1) plus column 1 (S) as slot ncol when c0 > 1
   const int c0 = (int)blockIdx.x * ncol;
   const int c1 = min(E, c0 + ncol);
@@ -2346,24 +2365,26 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
       v[i] = recs[(size_t)r * E + col];
     }
   }
-  for (int i = tid; i < P; i += FIN_THREADS) mA[i] = (i < n) ? (float)recs[(size_t)i * E] : INFINITY;
+  for (int i = tid; i < P; i += FIN_THREADS) mlev[i] = (i < n) ? (float)recs[(size_t)i * E] : INFINITY;
   __syncthreads();
-  // (2) pair scales, level by level (level l has P >> (l + 1) pairs)
-  float* src = mA;
-  float* dst = mB;
-  for (int l = 0; (P >> (l + 1)) >= 1; ++l) {
-    const int w = P >> (l + 1);
-    const int base = colfin_level_base(P, l);
-    for (int i = tid; i < w; i += FIN_THREADS) {
-      const PairScale ps = pair_scale(src[2 * i], src[2 * i + 1], f.T);
-      lps[base + i] = ps;
-      dst[i] = ps.m;
-    }
+  // (2) pair scales: first the node minima level by level (one fminf per node, the m that
+  //     pair_scale forms), then every node's pair scale in one pass, so the exponentials of
+  //     the log2(P) levels run side by side instead of one level after another
+  for (int l = 1; (P >> l) >= 1; ++l) {
+    const float* s = mlev + (2 * P - ((2 * P) >> (l - 1)));
+    float* d = mlev + (2 * P - ((2 * P) >> l));
+    for (int i = tid; i < (P >> l); i += FIN_THREADS) d[i] = fminf(s[2 * i], s[2 * i + 1]);
     __syncthreads();
-    float* t = src;
-    src = dst;
-    dst = t;
   }
+  const int log2P = 31 - __clz(P);
+  for (int g = tid; g < P - 1; g += FIN_THREADS) {
+    const int r = P - g;  // level l holds nodes g with P >> (l + 1) < P - g <= P >> l
+    const int l = log2P - (r <= 1 ? 0 : 32 - __clz(r - 1));
+    const int i = g - colfin_level_base(P, l);
+    const float* s = mlev + (2 * P - ((2 * P) >> l));
+    lps[g] = pair_scale(s[2 * i], s[2 * i + 1], f.T);
+  }
+  __syncthreads();
 #ifdef MPPI_STAMPS
   if (blockIdx.x == 0) FIN_STAMP(9);
 #endif
@@ -2413,7 +2434,7 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
   if (gridDim.x > 1) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    int* flag = reinterpret_cast<int*>(mA);
+    int* flag = reinterpret_cast<int*>(mlev);
     if (tid == 0) {
       const unsigned prev = __hip_atomic_fetch_add(f.level1_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = prev == gridDim.x - 1;
@@ -2819,7 +2840,7 @@ int colfin_shape(int n, int H, int* P_out, int* ncol_out, int* groups_out, size_
   *P_out = P;
   *ncol_out = ncol;
   *groups_out = groups;
-  *lds_tree = (size_t)(P - 1) * sizeof(PairScale) + (size_t)(P + P / 2) * sizeof(float) +
+  *lds_tree = (size_t)(P - 1) * sizeof(PairScale) + (size_t)(2 * P) * sizeof(float) +
               (size_t)(ncol + 1) * (P / 16) * sizeof(double);
   return 1;
 }
