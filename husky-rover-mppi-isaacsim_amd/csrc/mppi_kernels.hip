@@ -2353,8 +2353,8 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
   const int NG = P >> 4;  // register groups of 16 leaves per column
   // (1) leaf values of (column, group) items in registers; loads issued before the scale
   //     table is built so their latency overlaps it
-  const int items = ncols * NG;
-  const int it_c = tid % ncols, it_g = tid / ncols;
+  const int items = ncols * NG;  // <= FIN_THREADS (colfin_shape)
+  const int it_g = tid % NG, it_c = tid / NG;  // a column's groups in consecutive lanes
   const bool has_item = tid < items;
   const int col = (it_c < nc) ? c0 + it_c : 1;
   double v[16];
@@ -2389,6 +2389,7 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
   if (blockIdx.x == 0) FIN_STAMP(9);
 #endif
   // (3) the 4 lowest levels of every item in registers
+  double v0 = 0.0;
   if (has_item) {
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
@@ -2397,12 +2398,21 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
 #pragma unroll
       for (int i = 0; i < w; ++i) v[i] = pair_apply(ps[i], v[2 * i], v[2 * i + 1], col);
     }
-    part[it_c * NG + it_g] = v[0];
+    v0 = v[0];
   }
-  __syncthreads();
-  // (4) the remaining log2(NG) levels in LDS, in place (stride doubling)
+  // (4a) the next levels inside a wave: a column's NG (<= 64 at a time) consecutive lanes
+  //      combine by lane shuffles, left child = the lane with the bit clear (no barrier)
+  const int NGW = min(NG, 64);
   int lvl = 4;
-  for (int stride = 1; stride < NG; stride *= 2, ++lvl) {
+  for (int k = 1; k < NGW; k *= 2, ++lvl) {
+    const double o = __shfl_xor(v0, k, 64);  // every lane: item groups are NG-aligned
+    if (has_item && (it_g & (2 * k - 1)) == 0)
+      v0 = pair_apply(lps[colfin_level_base(P, lvl) + it_g / (2 * k)], v0, o, col);
+  }
+  if (has_item && (it_g & (NGW - 1)) == 0) part[it_c * NG + it_g] = v0;
+  __syncthreads();
+  // (4b) levels above a wave (NG > 64) in LDS, in place (stride doubling)
+  for (int stride = NGW; stride < NG; stride *= 2, ++lvl) {
     const int w = NG / (2 * stride);
     const PairScale* ps = lps + colfin_level_base(P, lvl);
     for (int it = tid; it < ncols * w; it += FIN_THREADS) {
@@ -2836,6 +2846,7 @@ int colfin_shape(int n, int H, int* P_out, int* ncol_out, int* groups_out, size_
   const int E = 2 * H + 2;
   // about 64 workgroups, at least 2 columns each
   const int ncol = std::max(2, (E + 63) / 64);
+  if ((ncol + 1) * (P / 16) > FIN_THREADS) return 0;  // one (column, group) item per thread
   const int groups = (E + ncol - 1) / ncol;
   *P_out = P;
   *ncol_out = ncol;

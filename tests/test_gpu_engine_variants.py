@@ -59,3 +59,15 @@ def test_variant_bitwise_equal(K, H, env):
     for i, (a, b) in enumerate(zip(got, ref)):
         for k in KEYS:
             np.testing.assert_array_equal(a[k], b[k], err_msg=f"step {i} {k} {env}")
+
+
+@pytest.mark.parametrize("K,H", [(1048576, 40), (1048576, 100)])
+def test_column_split_finish_at_4096_records(K, H):
+    """n = 4096 leaf records: the column-split finish's levels above one wave (H=40), and the
+    record-tree fallback where (columns + 1) x (records / 16) exceeds the workgroup (H=100)."""
+    ref, ref_costs = _run({"MPPI_COLFIN": "0"}, K, H, steps=2)
+    got, got_costs = _run({}, K, H, steps=2)
+    np.testing.assert_array_equal(got_costs, ref_costs)
+    for i, (a, b) in enumerate(zip(got, ref)):
+        for k in KEYS:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=f"step {i} {k}")
