@@ -5,18 +5,24 @@ Philox sampling, wheel filter, 2.5D rollout, four critics, softmax-weighted
 update, optimal filter and optimal rollout, with the outputs copied to host
 memory.  Inputs (DEM, costmap, state) are resident in HBM before timing.
 
-Scaling: weak.  Each rank owns K_per_gpu = 65536 trajectories (the headline
-shard); the global sample count is 65536*N, exchanged once per step by one
-RCCL all-gather of the per-rank softmax records.  `value` counts
-K=65536-trajectory MPPI steps per second over the whole job (= N x global
-steps/s).
+Configs (BASELINE.json configs[1..4]):
+  c3  K=65,536   H=100, 1500^2 DEM @0.1 m, 750^2 costmap  (headline, default)
+  c4  K=1,048,576 H=100, same scene
+  c5  K=262,144  H=128, 8192^2 DEM @0.025 m, 1024^2 costmap
+Scaling: STRONG.  The config's K is the global sample count; with N ranks each
+owns a contiguous leaf-aligned shard (distributed.shard_bounds) and the ranks
+exchange one (2H+2)-double softmax record per step with one RCCL all-gather.
+`value` = global MPPI steps/s at the named K.  For N>1 rank 0 also times the
+same config on its own GPU alone (`speedup_vs_1`), and the `c4` leg (K=1,048,576,
+the north-star scaling config) is run beside the headline at every N.
 
-Launch: python bench.py [--steps K --warmup W]  (N=1), or
+Launch: python bench.py [--config c3|c4|c5] [--steps K --warmup W]  (N=1), or
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import platform
@@ -33,8 +39,17 @@ for _p in (ROOT, PKG):
 
 BYTES_PER_ROLLOUT_STEP = 28   # 6 DEM f32 gathers + 1 costmap f32 gather
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
-START = (-60.0, -5.0)
-GOAL = (65.0, 10.0)
+
+# name -> (K global, H, scene function name, start, goal, description)
+CONFIGS = {
+    "c3": (65536, 100, "scene_c3", (-60.0, -5.0), (65.0, 10.0),
+           "C3: K=65536, H=100, 1500^2 DEM @0.1 m, 750^2 costmap @0.2 m"),
+    "c4": (1048576, 100, "scene_c3", (-60.0, -5.0), (65.0, 10.0),
+           "C4: K=1048576, H=100, 1500^2 DEM @0.1 m, 750^2 costmap @0.2 m"),
+    "c5": (262144, 128, "scene_c5", (0.0, 0.0), (80.0, 20.0),
+           "C5: K=262144, H=128, 8192^2 DEM @0.025 m (synthetic craters + fBm), 1024^2 costmap"),
+}
+KERNEL_SOURCES = ("mppi_kernels.hip", "mppi_kernels.h", "mppi_detmath.h", "mppi_capi.cpp", "Makefile")
 
 
 def parse():
@@ -42,19 +57,29 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--k-per-gpu", type=int, default=65536)
-    ap.add_argument("--horizon", type=int, default=100)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--proj", default="3d")
     ap.add_argument("--dem-path", default="auto", choices=["auto", "lds", "global", "ws", "pair"])
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
-                    help="bounded oracle sample on the host (rank 0, N=1); 0 disables")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0,
+                    help="budget of the bounded oracle samples on the host (rank 0, N=1); 0 disables")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     ap.add_argument("--no-bilinear", action="store_true", help="skip the C5 tiled-lookup roofline leg")
-    ap.add_argument("--no-c5", action="store_true", help="skip the C5 full-step leg (K=262144, H=128, 8192^2 DEM)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 (K=1048576) strong-scaling leg")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 full-step leg (N=1)")
     ap.add_argument("--no-costmap", action="store_true", help="skip the obstacle-costmap builder leg")
     ap.add_argument("--sync", action="store_true",
                     help="report the synchronous mode (no deferred optimal rollout) as the headline")
     return ap.parse_args()
+
+
+def source_hash():
+    """sha256 over the kernel sources: ties a committed PMC profile to the code it measured."""
+    h = hashlib.sha256()
+    csrc = os.path.join(PKG, "csrc")
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(csrc, name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
 
 
 def cpu_model():
@@ -68,40 +93,96 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(Z, hw, cm, H, seconds):
-    """Oracle (numpy, float32, one core) on the same workload: whole C3 steps until `seconds` elapse."""
-    os.environ.setdefault("OMP_NUM_THREADS", "1")
+def host_cores():
+    """CPUs this process may use (the GPU box grants a share of a larger machine), at most 16."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(n, cap, 16))
+
+
+# ------------------------------------------------------------------ CPU baseline (oracle, numpy)
+_CPU = {}
+
+
+def _cpu_shard(args):
+    """Worker: one contiguous leaf-aligned slice of K -> its softmax record (oracle.shard_record)."""
     from oracle import mppi_ref as R
-    K = 65536
+    K, H, step, b, c = args
     p = R.Params(K=K, H=H)
-    sc = R.Scene(Z, hw, cm)
-    st = R.State(x=START[0], y=START[1], goal_x=GOAL[0], goal_y=GOAL[1])
-    u1 = np.zeros(H, np.float32)
-    u2 = np.zeros(H, np.float32)
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        out = R.mppi_step(p, sc, st, u1, u2, n)
-        u1, u2 = out["u1_opt"], out["u2_opt"]
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 20:
-            break
-    return {"value": n / el, "unit": "MPPI steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} full C3 steps (K={K}, H={H}) of oracle/mppi_ref.py in {el:.1f} s on 1 core "
-                      f"of {cpu_model()} (os.cpu_count()={os.cpu_count()})"}
+    u0 = np.zeros(H, np.float32)
+    rec, _ = R.shard_record(p, _CPU["sc"], _CPU["st"], u0, u0, step, b, c)
+    return rec
 
 
+def _cpu_step_pool(pool, nw, K, H, step):
+    from oracle import mppi_ref as R
+    bounds = R.shard_bounds(K, nw)
+    recs = pool.map(_cpu_shard, [(K, H, step, b, c) for b, c in bounds])
+    p = R.Params(K=K, H=H)
+    root = R.tree_reduce(np.stack(recs), p.temperature) if len(recs) > 1 else recs[0]
+    return R.finish(p, _CPU["sc"], _CPU["st"], root)  # noqa: the finish is part of the step
+
+
+def cpu_baseline(Z, hw, cm, start, goal, budget_s):
+    """The build's numpy restatement (oracle/mppi_ref.py) timed on this host:
+    C1 (K=256, H=20), C2 (K=4096, H=50) and C3 (K=65536, H=100) on the C3 scene, each on 1 core and
+    on all granted cores (K split into leaf-aligned shards over a fork pool, records combined with
+    the same tree).  C1/C2: 3 warm-up steps then the median of >=10; C3: a few steps."""
+    import multiprocessing as mp
+    from oracle import mppi_ref as R
+    _CPU["sc"] = R.Scene(Z, hw, cm)
+    _CPU["st"] = R.State(x=start[0], y=start[1], goal_x=goal[0], goal_y=goal[1])
+    nw = host_cores()
+    table = {}
+    t_all = time.perf_counter()
+    ctx = mp.get_context("fork")
+    with ctx.Pool(nw) as pool:
+        for name, K, H, reps in (("c1", 256, 20, 10), ("c2", 4096, 50, 10), ("c3", 65536, 100, 3)):
+            u0 = np.zeros(H, np.float32)
+            p = R.Params(K=K, H=H)
+            row = {}
+            for mode in ("1core", "allcores"):
+                warm = 3 if name != "c3" else 1
+                ts = []
+                for i in range(warm + reps):
+                    t0 = time.perf_counter()
+                    if mode == "1core":
+                        R.mppi_step(p, _CPU["sc"], _CPU["st"], u0, u0, i)
+                    else:
+                        _cpu_step_pool(pool, min(nw, (K + 255) // 256), K, H, i)
+                    if i >= warm:
+                        ts.append(time.perf_counter() - t0)
+                    if time.perf_counter() - t_all > budget_s and i >= warm:
+                        break
+                med = float(np.median(ts))
+                row[mode] = {"steps_per_s": round(1.0 / med, 3), "median_ms": round(med * 1e3, 2),
+                             "steps_timed": len(ts),
+                             "workers": 1 if mode == "1core" else min(nw, (K + 255) // 256)}
+            table[name] = row
+    c3 = table["c3"]["allcores"]
+    return {"value": c3["steps_per_s"], "unit": "MPPI steps/s", "cores": c3["workers"], "kind": "port",
+            "sample": (f"oracle/mppi_ref.py (numpy f32), C3 K=65536 H=100 on {c3['workers']} worker "
+                       f"processes (leaf-aligned K shards, same record tree), median of "
+                       f"{c3['steps_timed']} steps; host {cpu_model()}, os.cpu_count()={os.cpu_count()}, "
+                       f"granted cores={nw}"),
+            "table": table, "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(), "granted_cores": nw}
+
+
+# ------------------------------------------------------------------ side legs (N=1)
 def bilinear_bench(torch, device, reps=20):
     """LDS-tiled DEM lookup at C5 size: 8192^2 DEM @0.025 m, N = 262144*128 queries.
 
-    Queries uniform over the tile, binned by 64x64-cell tile once (untimed: inputs resident);
-    `reps` launches of mppi_bilinear_tiled timed with HIP events on the engine's stream.
+    NOT on the MPPI step path (the rollout gathers the DEM through L1/L2): a standalone kernel
+    for the north-star '>=60 % of HBM roofline on the bilinear kernel' figure.  `frac` is the
+    lookup kernel alone with the queries already binned by 64x64-cell tile; `frac_incl_binning`
+    times the binning (count, scan, scatter) and the lookup together on the same stream.
     Algorithmic bytes = the DEM once + 12 B per query (x, y in, h out).
     """
     from mppi_amd import _lib
     G, hw, N = 8192, 102.4, 262144 * 128
-    res = 2 * hw / G
     xs = torch.linspace(-hw, hw, G, device=device)
     Z = (0.8 * torch.sin(0.37 * xs)[None, :] * torch.cos(0.23 * xs)[:, None]).contiguous()   # synthetic terrain
     stream = torch.cuda.Stream(device=device)
@@ -116,72 +197,51 @@ def bilinear_bench(torch, device, reps=20):
     xb, yb = torch.empty_like(x), torch.empty_like(y)
     perm = torch.empty(N, dtype=torch.int64, device=device)
     off = torch.empty(nt + 1, dtype=torch.int32, device=device)
-    eng.bin_queries(x.data_ptr(), y.data_ptr(), N, xb.data_ptr(), yb.data_ptr(), perm.data_ptr(), off.data_ptr())
-    del perm
     h = torch.empty_like(x)
-    with torch.cuda.stream(stream):
-        for _ in range(3):
-            eng.bilinear_tiled(xb.data_ptr(), yb.data_ptr(), off.data_ptr(), h.data_ptr())
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            eng.bilinear_tiled(xb.data_ptr(), yb.data_ptr(), off.data_ptr(), h.data_ptr())
-        e1.record(stream)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+
+    def binned():
+        eng.bin_queries(x.data_ptr(), y.data_ptr(), N, xb.data_ptr(), yb.data_ptr(), perm.data_ptr(),
+                        off.data_ptr())
+
+    def lookup():
+        eng.bilinear_tiled(xb.data_ptr(), yb.data_ptr(), off.data_ptr(), h.data_ptr())
+
+    def timed(fn):
+        with torch.cuda.stream(stream):
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    binned()
+    torch.cuda.synchronize()
+    ms = timed(lookup)
+    ms_all = timed(lambda: (binned(), lookup()))
     alg = G * G * 4 + 12 * N
-    # scattered lookup (no binning, corners through L1/L2) on the same unsorted points, for reference
+    # scattered lookup (no binning, corners through L1/L2) on the same unsorted points
     hq = torch.empty_like(x)
     eng.bilinear_query(x.data_ptr(), y.data_ptr(), hq.data_ptr(), N)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     eng.bilinear_query(x.data_ptr(), y.data_ptr(), hq.data_ptr(), N)
+    torch.cuda.synchronize()
     scat_ms = (time.perf_counter() - t0) * 1e3
     eng.close()
     achieved = alg / (ms * 1e-3) / 1e9
-    return {"bound": "hbm", "kernel": "mppi_bilinear_tiled_kernel", "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "kernel_avg_ms": round(ms, 4), "algorithmic_bytes_per_launch": alg,
+    achieved_all = alg / (ms_all * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": "mppi_bilinear_tiled_kernel", "on_step_path": False,
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel_avg_ms": round(ms, 4),
+            "incl_binning_ms": round(ms_all, 4), "frac_incl_binning": round(achieved_all / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes_per_launch": alg,
             "workload": f"C5 tile {G}^2 DEM (synthetic), N={N} uniform queries binned by 64x64 tile",
-            "scattered_query_ms": round(scat_ms, 3)}
-
-
-def c5_bench(device_index, steps=50, warmup=10):
-    """Config C5 (BASELINE.json configs[4]) on one GPU: K=262144, H=128 on the 8192^2 DEM @0.025 m.
-
-    Same step and timing as the headline (inputs resident, outputs in host memory every step,
-    deferred optimal rollout); reported beside the headline, not as `value`.
-    """
-    from mppi_amd import _lib, scene
-    Z, hw, cm = scene.scene_c5()
-    K, H = 262144, 128
-    eng = _lib.Engine(_lib.make_params(K, H), device_index)
-    eng.set_dem(Z, hw)
-    eng.set_costmap(cm, hw)
-    eng.set_state(_lib.make_state(0.0, 0.0, (1.0, 0.0, 0.0), goal_x=80.0, goal_y=20.0))
-    eng.set_async_tail(True)
-    for i in range(warmup):
-        eng.step("3d", i, copy=False)
-    eng.sync()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        eng.step("3d", warmup + i, copy=False)
-    eng.outputs()
-    eng.sync()
-    el = time.perf_counter() - t0
-    eng.set_timing(True)
-    for i in range(10):
-        eng.step("3d", warmup + steps + i, copy=False)
-    eng.outputs()
-    roll_ms, fin_ms, n = eng.timing()
-    eng.close()
-    k_ms = roll_ms / max(n, 1)
-    alg = BYTES_PER_ROLLOUT_STEP * K * H
-    return {"workload": "C5: K=262144, H=128, 8192^2 DEM @0.025 m (synthetic craters + fBm), 1024^2 costmap",
-            "steps_per_s": round(steps / el, 3), "ms_per_step": round(el / steps * 1e3, 4),
-            "rollout_kernel_avg_ms": round(k_ms, 4), "finish_kernel_avg_ms": round(fin_ms / max(n, 1), 4),
-            "rollout_achieved_GBs": round(alg / (k_ms * 1e-3) / 1e9, 1),
-            "rollout_frac_of_hbm_peak": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            "scattered_query_ms": round(scat_ms, 3),
+            "scattered_frac": round(alg / (scat_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 COSTMAP_BYTES_PER_CELL = 23   # occ 1+1+1, g2 4+4, d2 4+4, out 4 (csrc/mppi_costmap.hip)
@@ -190,7 +250,7 @@ COSTMAP_BYTES_PER_CELL = 23   # occ 1+1+1, g2 4+4, d2 4+4, out 4 (csrc/mppi_cost
 def costmap_bench(device_index, reps=20, cpu=True):
     """Surface.create_obstacles_costmap (MPPI_isaac.py:361-378) on the GPU: a 1024^2 costmap (the C5
     map, grid 8192 / 8) from 750 rocks, HIP-event device time per build; the oracle (numpy raster +
-    scipy exact EDT, 1 core) on the same input once for reference."""
+    distance transform, 1 core) on the same input once for reference."""
     from mppi_amd import _lib
     rng = np.random.RandomState(99)
     rocks = [[rng.uniform(-95, 95), rng.uniform(-95, 95), rng.uniform(0.0, 0.8)] for _ in range(750)]
@@ -205,7 +265,7 @@ def costmap_bench(device_index, reps=20, cpu=True):
     call_ms = (time.perf_counter() - t0) / reps * 1e3
     b.close()
     dev_ms /= reps
-    rec = {"workload": "1024^2 costmap @0.2 m from 750 rocks (exact EDT, power 20)",
+    rec = {"workload": "1024^2 costmap @0.2 m from 750 rocks (power 20)",
            "kernel_ms": round(dev_ms, 4), "call_ms_incl_d2h": round(call_ms, 3),
            "achieved_GBs": round(COSTMAP_BYTES_PER_CELL * size * size / (dev_ms * 1e-3) / 1e9, 1)}
     if cpu:
@@ -216,14 +276,112 @@ def costmap_bench(device_index, reps=20, cpu=True):
     return rec
 
 
+# ------------------------------------------------------------------ the MPPI step runs
+_SCENES = {}
+
+
+def get_scene(fn):
+    if fn not in _SCENES:
+        from mppi_amd import scene
+        _SCENES[fn] = getattr(scene, fn)()
+    return _SCENES[fn]
+
+
+class Runner:
+    """One rank's controller for one config: the sharded engine (N>1) or a single-GPU engine."""
+
+    def __init__(self, cfg, device, world, dem_path="auto", solo=False):
+        from mppi_amd import _lib
+        from mppi_amd.distributed import ShardedMPPI
+        K, H, scene_fn, start, goal, desc = CONFIGS[cfg]
+        self.K, self.H, self.desc = K, H, desc
+        self.world = 1 if solo else world
+        Z, hw, cm = get_scene(scene_fn)
+        if self.world > 1:
+            self.sharded = ShardedMPPI(K, H, device)
+            self.eng = self.sharded.engine
+            self.k_local = self.sharded.k_count
+        else:
+            self.sharded = None
+            self.eng = _lib.Engine(_lib.make_params(K, H), device)
+            self.k_local = K
+        self.eng.set_dem_path(dem_path)
+        self.eng.set_dem(Z, hw)
+        self.eng.set_costmap(cm, hw)
+        self.eng.set_state(_lib.make_state(start[0], start[1], (1.0, 0.0, 0.0), goal_x=goal[0],
+                                           goal_y=goal[1]))
+
+    def step(self, proj, i):
+        if self.sharded is not None:
+            self.sharded.step(proj, i, copy=False)
+        else:
+            self.eng.step(proj, i, copy=False)
+
+    def close(self):
+        if self.sharded is not None:
+            self.sharded.close()
+        else:
+            self.eng.close()
+
+
+def timed_run(torch, dist, run, proj, warmup, steps, step0, async_tail, kernel_timing=False):
+    """`warmup` untimed + `steps` timed MPPI steps, barrier + synchronize on both sides; returns
+    the max-over-ranks wall time of the timed steps."""
+    eng = run.eng
+    eng.set_async_tail(async_tail)
+    eng.set_timing(False)
+    for i in range(warmup):
+        run.step(proj, step0 + i)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None and run.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    eng.set_timing(kernel_timing)
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        run.step(proj, step0 + warmup + i)
+    eng.outputs()          # the last step's deferred optimal rollout is in host memory too
+    barrier()
+    el = time.perf_counter() - t0
+    if dist is not None and run.world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def pmc_traffic(path, kernel, K_local, H):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary, only if it was
+    measured on the current kernel sources (src_sha256) at the same K and H; else None."""
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return None, "no PMC summary"
+    if pm.get("src_sha256") != source_hash():
+        return None, f"PMC summary is for other kernel sources ({pm.get('src_sha256')})"
+    if pm.get("K") != K_local or pm.get("H") != H:
+        return None, f"PMC summary is for K={pm.get('K')} H={pm.get('H')}"
+    k = pm.get("kernels", {}).get(kernel, {})
+    return k.get("hbm_bytes_per_launch"), f"profiles PMC at git {pm.get('git_head')}, src {pm.get('src_sha256')}"
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    if world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    cpu = None
+    if world == 1 and args.cpu_baseline_seconds > 0:
+        # before anything touches the GPU: the fork pool's workers must not inherit a HIP context
+        Z, hw, cm = get_scene("scene_c3")
+        cpu = cpu_baseline(Z, hw, cm, CONFIGS["c3"][3], CONFIGS["c3"][4], args.cpu_baseline_seconds)
     import torch
     dist = None
     if world > 1:
@@ -231,106 +389,95 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    from mppi_amd import _lib, scene
-    from mppi_amd.distributed import ShardedMPPI
-    Z, hw, cm = scene.scene_c3()
-    H = args.horizon
-    Kl = args.k_per_gpu
-    if Kl % 256:
-        raise SystemExit("--k-per-gpu must be a multiple of 256 (reduction leaf)")
-    # rank r owns trajectories [r*Kl, (r+1)*Kl) of the global K = Kl*world (shard_bounds)
-    sharded = ShardedMPPI(Kl * world, H, local_rank) if world > 1 else None
-    eng = sharded.engine if sharded is not None else _lib.Engine(_lib.make_params(Kl, H), local_rank)
-    eng.set_dem_path(args.dem_path)
-    eng.set_dem(Z, hw)
-    eng.set_costmap(cm, hw)
-    eng.set_state(_lib.make_state(START[0], START[1], (1.0, 0.0, 0.0), goal_x=GOAL[0], goal_y=GOAL[1]))
-
-    if sharded is not None:
-        def one_step(i):
-            sharded.step(args.proj, i, copy=False)
-    else:
-        def one_step(i):
-            eng.step(args.proj, i, copy=False)
-
-    def barrier():
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    def timed_run(async_tail, step0, steps, kernel_timing=False):
-        """W warmup + `steps` timed MPPI steps; returns the max-over-ranks wall time."""
-        eng.set_async_tail(async_tail)
-        eng.set_timing(False)
-        for i in range(args.warmup):
-            one_step(step0 + i)
-        eng.set_timing(kernel_timing)
-        barrier()
-        t0 = time.perf_counter()
-        for i in range(steps):
-            one_step(step0 + args.warmup + i)
-        eng.outputs()         # the last step's deferred optimal rollout is in host memory too
-        barrier()
-        el = time.perf_counter() - t0
-        if dist is not None:
-            t = torch.tensor([el], dtype=torch.float64, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el
-
+    run = Runner(args.config, local_rank, world, args.dem_path)
+    K, H = run.K, run.H
     # synchronous MPPI_step semantics first (every output in host memory when step() returns)
-    el_sync = timed_run(False, 0, args.steps)
+    el_sync = timed_run(torch, dist, run, args.proj, args.warmup, args.steps, 0, False)
     # headline: the optimal rollout of step i (it only feeds trajectories_sim) overlaps step i+1;
     # every step's outputs still reach pinned host memory inside the timed region
-    el = timed_run(not args.sync, args.warmup + args.steps, args.steps)
+    s0 = args.warmup + args.steps
+    el = timed_run(torch, dist, run, args.proj, args.warmup, args.steps, s0, not args.sync)
     # per-kernel HIP-event times in a separate pass (events add stream work of their own)
-    timed_run(not args.sync, 2 * (args.warmup + args.steps), max(args.steps // 4, 10), kernel_timing=True)
-    roll_ms, fin_ms, n_roll = eng.timing()
-    tail_ms, n_tail = eng.tail_timing()
-    info = eng.launch_info()
+    timed_run(torch, dist, run, args.proj, args.warmup, max(args.steps // 4, 10), 2 * s0, not args.sync,
+              kernel_timing=True)
+    roll_ms, fin_ms, n_roll = run.eng.timing()
+    tail_ms, n_tail = run.eng.tail_timing()
+    info = run.eng.launch_info()
+    record_bytes = run.eng.record_len() * 8
+    k_local = run.k_local
+    run.close()
+
+    def solo_rate(cfg, steps):
+        """rank 0 alone, the whole config on its GPU (the N=1 reference of this job)."""
+        r = Runner(cfg, local_rank, 1, args.dem_path, solo=True)
+        t = timed_run(torch, None, r, args.proj, args.warmup, steps, 0, not args.sync)
+        r.close()
+        return steps / t
+
+    speedup = None
+    if world > 1:
+        dist.barrier()
+        if rank == 0:
+            speedup = (args.steps / el) / solo_rate(args.config, args.steps)
+        dist.barrier()
+
+    c4 = None
+    if not args.no_c4 and args.config != "c4":
+        r4 = Runner("c4", local_rank, world, args.dem_path)
+        c4_steps = max(10, args.steps // 8)
+        t4 = timed_run(torch, dist, r4, args.proj, min(args.warmup, 5), c4_steps, 0, not args.sync)
+        r4.eng.set_timing(False)
+        kl4 = r4.k_local
+        r4.close()
+        if world > 1:
+            dist.barrier()
+        c4 = {"workload": CONFIGS["c4"][5] + f", K-sharded over {world} GPU(s)", "global_K": CONFIGS["c4"][0],
+              "k_per_gpu": kl4, "steps": c4_steps, "steps_per_s": round(c4_steps / t4, 3),
+              "ms_per_step": round(t4 / c4_steps * 1e3, 4)}
+        if world > 1:
+            sp = None
+            if rank == 0:
+                sp = (c4_steps / t4) / solo_rate("c4", c4_steps)
+                c4["speedup_vs_1"] = round(sp, 3)
+            dist.barrier()
 
     if rank == 0:
         steps_per_s = args.steps / el
-        value = steps_per_s * world * Kl / 65536.0
         k_avg_ms = roll_ms / max(n_roll, 1)
-        alg_bytes = BYTES_PER_ROLLOUT_STEP * Kl * H
+        alg_bytes = BYTES_PER_ROLLOUT_STEP * k_local * H
         achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(args.pmc_json):
-            try:
-                with open(args.pmc_json) as f:
-                    pm = json.load(f)
-                if pm.get("K") == Kl and pm.get("H") == H:
-                    traffic = pm.get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
+        kernel = {"auto": "mppi_rollout_pair_kernel", "pair": "mppi_rollout_pair_kernel",
+                  "ws": "mppi_rollout_ws_kernel"}.get(args.dem_path, "mppi_rollout_kernel")
+        traffic, traffic_src = pmc_traffic(args.pmc_json, kernel, k_local, H)
         rec = {
             "metric": "MPPI steps/sec at K=65536 H=100 on 750x750 costmap; 1/2/4/8-GPU scaling",
-            "value": round(value, 3),
-            "unit": "MPPI steps/s (K=65536-trajectory steps)",
+            "value": round(steps_per_s, 3),
+            "unit": "MPPI steps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (reference crater + obstacle recipes; reference .npy blobs are absent)",
             "config": {
-                "workload": f"C3: K={Kl} per GPU (global K={Kl * world}), H={H}, 1500^2 DEM @0.1 m, "
-                            f"750^2 costmap @0.2 m, proj={args.proj}, outputs in host memory each step",
-                "global_K": Kl * world,
+                "workload": f"{run.desc}, proj={args.proj}, outputs in host memory each step",
+                "global_K": K,
+                "k_per_gpu": k_local,
                 "H": H,
-                "parallelism": f"K-sharded dp{world}, one RCCL all_gather per step" if world > 1 else "single GPU",
+                "parallelism": (f"K-sharded dp{world}, one RCCL all_gather of a {record_bytes}-byte record "
+                                f"per rank per step") if world > 1 else "single GPU",
+                "record_bytes_per_rank": record_bytes,
+                "speedup_vs_1": round(speedup, 3) if speedup is not None else None,
                 "rollout_kernel": info,
-                "global_steps_per_s": round(steps_per_s, 3),
                 "pipelined_tail": not args.sync,
                 "sync_steps_per_s": round(args.steps / el_sync, 3),
                 "sync_ms_per_step": round(el_sync / args.steps * 1e3, 4),
                 "finish_kernel_avg_ms": round(fin_ms / max(n_roll, 1), 5),
                 "tail_kernel_avg_ms": round(tail_ms / n_tail, 5) if n_tail else None,
+                "src_sha256": source_hash(),
             },
             "roofline": {
                 "bound": "hbm",
@@ -339,22 +486,34 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": {"auto": "mppi_rollout_pair_kernel", "pair": "mppi_rollout_pair_kernel",
-                           "ws": "mppi_rollout_ws_kernel"}.get(args.dem_path, "mppi_rollout_kernel"),
+                "traffic_source": traffic_src,
+                "kernel": kernel,
                 "kernel_avg_ms": round(k_avg_ms, 5),
                 "algorithmic_bytes_per_launch": alg_bytes,
             },
         }
+        if c4 is not None:
+            rec["c4"] = c4
         if world == 1 and not args.no_bilinear:
             rec["bilinear_roofline"] = bilinear_bench(torch, torch.device("cuda", local_rank))
-        if world == 1 and not args.no_c5:
-            rec["c5"] = c5_bench(local_rank)
+        if world == 1 and not args.no_c5 and args.config != "c5":
+            r5 = Runner("c5", local_rank, 1, args.dem_path, solo=True)
+            t5 = timed_run(torch, None, r5, args.proj, 10, 50, 0, not args.sync)
+            timed_run(torch, None, r5, args.proj, 2, 10, 100, not args.sync, kernel_timing=True)
+            roll5, fin5, n5 = r5.eng.timing()
+            r5.close()
+            k5 = roll5 / max(n5, 1)
+            alg5 = BYTES_PER_ROLLOUT_STEP * CONFIGS["c5"][0] * CONFIGS["c5"][1]
+            rec["c5"] = {"workload": CONFIGS["c5"][5], "steps_per_s": round(50 / t5, 3),
+                         "ms_per_step": round(t5 / 50 * 1e3, 4), "rollout_kernel_avg_ms": round(k5, 4),
+                         "finish_kernel_avg_ms": round(fin5 / max(n5, 1), 4),
+                         "rollout_achieved_GBs": round(alg5 / (k5 * 1e-3) / 1e9, 1),
+                         "rollout_frac_of_hbm_peak": round(alg5 / (k5 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         if world == 1 and not args.no_costmap:
             rec["costmap_builder"] = costmap_bench(local_rank, cpu=args.cpu_baseline_seconds > 0)
-        if world == 1 and args.cpu_baseline_seconds > 0:
-            rec["cpu_baseline"] = cpu_baseline(Z, hw, cm, H, args.cpu_baseline_seconds)
+        if cpu is not None:
+            rec["cpu_baseline"] = cpu
         print(json.dumps(rec), flush=True)
-    eng.close()
     if dist is not None:
         dist.destroy_process_group()
 

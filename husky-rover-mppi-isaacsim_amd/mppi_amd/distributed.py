@@ -57,10 +57,14 @@ class ShardedMPPI:
     with no host synchronisation in between.
     """
 
-    def __init__(self, K_global: int, H: int, device: int, group=None, **params_kw):
+    def __init__(self, K_global: int, H: int, device, group=None, engine_factory=None, **params_kw):
+        """``engine_factory(K, H, k_offset, device)`` replaces the HIP engine (CPU protocol tests
+        drive the same exchange with an oracle-backed stand-in); ``device="cpu"`` then skips the
+        HIP stream and keeps the exchange buffers in host memory (gloo)."""
+        import contextlib
+
         import torch
         import torch.distributed as dist
-        from . import _lib
 
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -68,23 +72,40 @@ class ShardedMPPI:
         self.K_global = int(K_global)
         self.H = int(H)
         self.k_begin, self.k_count = shard_bounds(self.K_global, self.world)[self.rank]
-        if self.k_count <= 0:
-            raise ValueError(f"rank {self.rank} has no trajectories (K={K_global}, world={self.world})")
-        self.engine = _lib.Engine(_lib.make_params(self.k_count, H, k_offset=self.k_begin, **params_kw),
-                                  device)
-        self.stream = torch.cuda.Stream(device=device)
-        self.engine.set_stream(self.stream.cuda_stream)
+        # a rank left without trajectories (K < world * LEAF) still takes part in every exchange:
+        # it contributes the empty record (m = +inf, S = V = 0), which the combine tree passes
+        # through, and runs the finish like every other rank.  Its engine only serves the finish.
+        self.empty = self.k_count <= 0
+        k_eng = LEAF if self.empty else self.k_count
+        k_off = min(self.k_begin, self.K_global)
+        if engine_factory is None:
+            from . import _lib
+            self.engine = _lib.Engine(_lib.make_params(k_eng, H, k_offset=k_off, **params_kw), device)
+        else:
+            self.engine = engine_factory(k_eng, H, k_off, device)
+        if device == "cpu":
+            self.stream = None
+            self._ctx = contextlib.nullcontext
+            tdev = "cpu"
+        else:
+            self.stream = torch.cuda.Stream(device=device)
+            self.engine.set_stream(self.stream.cuda_stream)
+            self._ctx = lambda: torch.cuda.stream(self.stream)
+            tdev = f"cuda:{device}"
         E = self.engine.record_len()
-        self.record = torch.empty(E, dtype=torch.float64, device=f"cuda:{device}")
-        self.gathered = torch.empty(self.world * E, dtype=torch.float64, device=f"cuda:{device}")
+        self.record = torch.empty(E, dtype=torch.float64, device=tdev)
+        self.gathered = torch.empty(self.world * E, dtype=torch.float64, device=tdev)
 
     def step(self, proj="3d", step=0, copy=True):
         """One MPPI_step over K_global trajectories; outputs (identical on all ranks) in host memory."""
-        import torch
-        with torch.cuda.stream(self.stream):
+        with self._ctx():
             if self.world == 1:
                 return self.engine.step(proj, step, copy)
-            self.engine.step_partial(self.record.data_ptr(), proj, step)
+            if self.empty:
+                self.record.zero_()
+                self.record[0] = float("inf")
+            else:
+                self.engine.step_partial(self.record.data_ptr(), proj, step)
             exchange_records(self.record, self.gathered, self.group)
             return self.engine.step_finish(self.gathered.data_ptr(), self.world, copy)
 

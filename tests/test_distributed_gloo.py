@@ -109,3 +109,97 @@ def test_gloo_ragged_shards_agree_across_ranks():
     one = R.mppi_step(p, R.Scene(Z, hw, cm), st, u, u, 2)
     rel = np.abs(sharded["u1_opt"] - one["u1_opt"]) / np.maximum(np.abs(one["u1_opt"]), 1e-3)
     assert rel.max() <= 1e-5
+
+
+class _OracleEngine:
+    """CPU stand-in for the HIP engine behind ShardedMPPI: the same three calls, computed by the
+    oracle (record of this rank's slice; finish over the gathered records)."""
+
+    def __init__(self, K, H, k_offset, K_global, sharded_ref):
+        self.K, self.H, self.k0, self.K_global = K, H, k_offset, K_global
+        self.sh = sharded_ref
+        self.partial_calls = 0
+
+    def record_len(self):
+        return 2 * self.H + 2
+
+    def _setup(self):
+        Z, hw, cm = _scene()
+        p = R.Params(K=self.K_global, H=self.H, seed=7)
+        return p, R.Scene(Z, hw, cm), R.State(x=-5.0, y=1.0, goal_x=6.0, goal_y=-2.0)
+
+    def step_partial(self, ptr, proj, step):
+        import torch
+        self.partial_calls += 1
+        p, sc, st = self._setup()
+        u = np.zeros(self.H, np.float32)
+        rec, _ = R.shard_record(p, sc, st, u, u, step, self.k0, self.K)
+        sh = self.sh[0]
+        assert ptr == sh.record.data_ptr()
+        sh.record.copy_(torch.from_numpy(rec))
+
+    def step_finish(self, ptr, n, copy=True):
+        sh = self.sh[0]
+        assert ptr == sh.gathered.data_ptr() and n == sh.world
+        p, sc, st = self._setup()
+        recs = sh.gathered.numpy().reshape(n, -1)
+        root = R.tree_reduce(recs, p.temperature)
+        out = R.finish(p, sc, st, root)
+        out["root"] = root
+        return out
+
+    def close(self):
+        pass
+
+
+def _sharded_worker(rank, world, port, K, H, q):
+    import torch.distributed as dist
+    from mppi_amd.distributed import ShardedMPPI
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        holder = []
+        eng = []
+
+        def factory(k, h, k0, device):
+            e = _OracleEngine(k, h, k0, K, holder)
+            eng.append(e)
+            return e
+
+        sh = ShardedMPPI(K, H, "cpu", engine_factory=factory)
+        holder.append(sh)
+        out = sh.step("3d", 2)
+        q.put((rank, sh.empty, eng[0].partial_calls, out["root"], out["u1_opt"], out["v_opt"]))
+        sh.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_sharded_mppi_with_empty_shard():
+    """ShardedMPPI's own exchange (world 4, K=1280: rank 3 owns no trajectory).  The empty rank
+    contributes the empty record and no rank blocks; every rank emits the one-rank result's
+    controls, and the root equals the oracle's 4-shard combine."""
+    world, K, H = 4, 1280, 6
+    assert shard_bounds(K, world)[3] == (1280, 0)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, K, H, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    Z, hw, cm = _scene()
+    p = R.Params(K=K, H=H, seed=7)
+    st = R.State(x=-5.0, y=1.0, goal_x=6.0, goal_y=-2.0)
+    u = np.zeros(H, np.float32)
+    sharded = R.mppi_step(p, R.Scene(Z, hw, cm), st, u, u, 2, world=world)
+    for rank, empty, calls, root, u1, v in res:
+        assert empty == (rank == 3)
+        assert calls == (0 if rank == 3 else 1)
+        np.testing.assert_array_equal(root, sharded["root"])
+        np.testing.assert_array_equal(u1, sharded["u1_opt"])
+        np.testing.assert_array_equal(v, sharded["v_opt"])
