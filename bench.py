@@ -59,7 +59,6 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--proj", default="3d")
-    ap.add_argument("--dem-path", default="auto", choices=["auto", "lds", "global", "ws", "pair"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0,
                     help="budget of the bounded oracle samples on the host (rank 0, N=1); 0 disables")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
@@ -290,7 +289,7 @@ def get_scene(fn):
 class Runner:
     """One rank's controller for one config: the sharded engine (N>1) or a single-GPU engine."""
 
-    def __init__(self, cfg, device, world, dem_path="auto", solo=False):
+    def __init__(self, cfg, device, world, solo=False):
         from mppi_amd import _lib
         from mppi_amd.distributed import ShardedMPPI
         K, H, scene_fn, start, goal, desc = CONFIGS[cfg]
@@ -305,7 +304,6 @@ class Runner:
             self.sharded = None
             self.eng = _lib.Engine(_lib.make_params(K, H), device)
             self.k_local = K
-        self.eng.set_dem_path(dem_path)
         self.eng.set_dem(Z, hw)
         self.eng.set_costmap(cm, hw)
         self.eng.set_state(_lib.make_state(start[0], start[1], (1.0, 0.0, 0.0), goal_x=goal[0],
@@ -389,7 +387,7 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    run = Runner(args.config, local_rank, world, args.dem_path)
+    run = Runner(args.config, local_rank, world)
     K, H = run.K, run.H
     # synchronous MPPI_step semantics first (every output in host memory when step() returns)
     el_sync = timed_run(torch, dist, run, args.proj, args.warmup, args.steps, 0, False)
@@ -409,7 +407,7 @@ def main():
 
     def solo_rate(cfg, steps):
         """rank 0 alone, the whole config on its GPU (the N=1 reference of this job)."""
-        r = Runner(cfg, local_rank, 1, args.dem_path, solo=True)
+        r = Runner(cfg, local_rank, 1, solo=True)
         t = timed_run(torch, None, r, args.proj, args.warmup, steps, 0, not args.sync)
         r.close()
         return steps / t
@@ -423,7 +421,7 @@ def main():
 
     c4 = None
     if not args.no_c4 and args.config != "c4":
-        r4 = Runner("c4", local_rank, world, args.dem_path)
+        r4 = Runner("c4", local_rank, world)
         c4_steps = max(10, args.steps // 8)
         t4 = timed_run(torch, dist, r4, args.proj, min(args.warmup, 5), c4_steps, 0, not args.sync)
         r4.eng.set_timing(False)
@@ -446,8 +444,7 @@ def main():
         k_avg_ms = roll_ms / max(n_roll, 1)
         alg_bytes = BYTES_PER_ROLLOUT_STEP * k_local * H
         achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9
-        kernel = {"auto": "mppi_rollout_pair_kernel", "pair": "mppi_rollout_pair_kernel",
-                  "ws": "mppi_rollout_ws_kernel"}.get(args.dem_path, "mppi_rollout_kernel")
+        kernel = "mppi_rollout_pair_kernel"
         traffic, traffic_src = pmc_traffic(args.pmc_json, kernel, k_local, H)
         rec = {
             "metric": "MPPI steps/sec at K=65536 H=100 on 750x750 costmap; 1/2/4/8-GPU scaling",
@@ -497,7 +494,7 @@ def main():
         if world == 1 and not args.no_bilinear:
             rec["bilinear_roofline"] = bilinear_bench(torch, torch.device("cuda", local_rank))
         if world == 1 and not args.no_c5 and args.config != "c5":
-            r5 = Runner("c5", local_rank, 1, args.dem_path, solo=True)
+            r5 = Runner("c5", local_rank, 1, solo=True)
             t5 = timed_run(torch, None, r5, args.proj, 10, 50, 0, not args.sync)
             timed_run(torch, None, r5, args.proj, 2, 10, 100, not args.sync, kernel_timing=True)
             roll5, fin5, n5 = r5.eng.timing()

@@ -42,11 +42,7 @@ constexpr size_t kLdsBytes = 160 * 1024;
 constexpr int kEpsSlots = 3;
 
 struct Plan {
-  bool lds = false;       // rollout kernel DEM path
-  bool ws = false;        // warp-specialised rollout kernel (chain + side waves)
-  bool pair = false;      // ... synchronised per chain/side pair (default)
   int traj_per_block = 256;
-  bool fin_lds = false;   // finish kernel DEM path
   int block = 256, blocks = 0;
   int wx0 = 0, wy0 = 0, W = 1, Wr = 1;
   size_t lds_bytes = 0, fin_lds_bytes = 0, fin_tree_bytes = 0;
@@ -121,9 +117,6 @@ struct mppi_ctx {
   int spec_slot = 0;
   hipStream_t noise_stream = nullptr;
   int prio_least = 0, prio_greatest = 0;
-  // tree levels inside the rollout kernel (MPPI_FUSED_FINISH): 0 none (default: measured fastest
-  // with the deferred optimal rollout, profiles/r01_notes.md), 1 the first level, 2 all + the finish
-  int fused_level = 0;
   // finish: 1 = column-split kernel (mppi_colfin_kernel) where it applies, 0 = the record tree
   // (env MPPI_COLFIN=0)
   int colfin = 1;
@@ -140,21 +133,18 @@ struct mppi_ctx {
   int wave_prio = 1;  // rollout waves raise their issue priority (env MPPI_WAVE_PRIO=0: off)
   hipEvent_t ev_roll_done = nullptr;
   hipEvent_t ev_prev_roll = nullptr;  // recorded after the last rollout that read an eps slot
-  // fused finish: cross-workgroup tree counters / level records
-  unsigned* tree_cnt = nullptr;
-  unsigned* noise_ctr = nullptr;  // [2] in-kernel noise work / exit counters
+  // finish: column-split u_opt slice records / first tree level, arrival counter
   double* level1 = nullptr;       // finish kernel first-level records
   size_t level1_cap = 0;
   unsigned* level1_cnt = nullptr;
-  double* tree_nodes = nullptr;
-  size_t tree_cap = 0;
   // tiled bilinear binning scratch
   int* bin_tile_of = nullptr;
   size_t bin_n_cap = 0;
   int* bin_counts = nullptr;
   int* bin_cursor = nullptr;
   size_t bin_t_cap = 0;
-  int dem_path = 0;
+  // the finish the last step ran (mppi_get_launch_info): 1 column-split, 0 record tree
+  int fin_kind = -1, fin_P = 0, fin_ncol = 0, fin_groups = 0;
   // last step (for dump)
   bool have_last = false;
   int last_proj = 3, last_mode = 0;
@@ -252,69 +242,40 @@ Plan make_plan(const mppi_ctx* c) {
   int i0, j0;
   host_cell(c, c->st.x, c->st.y, i0, j0);
   const int64_t span = 2 * (int64_t)Rc + 2;
+  // the square DEM window every lane of the step can touch (reported by mppi_get_launch_info)
   pl.W = (int)std::min<int64_t>(span, c->cols);
   pl.Wr = (int)std::min<int64_t>(span, c->rows);
   pl.wx0 = std::min(std::max(i0 - Rc, 0), c->cols - pl.W);
   pl.wy0 = std::min(std::max(j0 - Rc, 0), c->rows - pl.Wr);
-  const size_t win = (size_t)pl.W * pl.Wr * sizeof(float);
   const int64_t K = c->p.num_trajectories;
-
-  bool lds_fits = win <= kLdsBytes;
-  pl.lds = (c->dem_path == 1) || (c->dem_path == 0 && lds_fits);
-  if (c->dem_path == 2) pl.lds = false;
-  if (pl.lds) {
-    // one workgroup per CU holds the window: size the workgroup so ~256 of them cover K
-    pl.block = K <= 256 * 256 ? 256 : (K <= 512 * 256 ? 512 : 1024);
-  } else {
-    pl.block = 256;
-  }
-  pl.traj_per_block = pl.block;
-  pl.blocks = (int)((K + pl.block - 1) / pl.block);
-  const int NW = pl.block / 64;
-  // reduction scratch (mppi_rollout_kernel): costs[block], w[block] + wave minima, [leaves][2H+2] doubles
-  const size_t scratch = (size_t)pl.block * sizeof(float) +
-                         ((size_t)(pl.block + NW) * sizeof(float) + 15) / 16 * 16 +
-                         (size_t)(NW / 4) * (2 * H + 2) * sizeof(double);
-  pl.lds_bytes = std::max(pl.lds ? win : (size_t)0, scratch);
-  if (c->dem_path == 3 || c->dem_path == 0 || c->dem_path == 4) {
-    // warp-specialised kernels (chain + side waves, DEM via L1/L2).  Default: the
-    // pair-synchronised one (rings [D][6][TB] + cost[TB] + flags + scratch in LDS);
-    // 3: one workgroup barrier per step (rings [2][7][TB]).  profiles/r01_notes.md
-    const int TB = WS_TRAJ;
-    pl.ws = true;
-    pl.pair = c->dem_path != 3;
-    pl.lds = false;
-    pl.traj_per_block = TB;
-    pl.block = 2 * TB;
-    pl.blocks = (int)((K + TB - 1) / TB);
-    const size_t scratch_ws = ((size_t)(TB + TB / 64) * 4 + 15) / 16 * 16 +
-                              (size_t)(TB / 256) * (2 * H + 2) * sizeof(double);
-    pl.lds_bytes = pl.pair ? (size_t)(6 * PAIR_RING + 1) * TB * sizeof(float) + 4 * (TB / 64) * sizeof(int) +
-                                 (size_t)((2 * H + 3) & ~3) * sizeof(float) + scratch_ws
-                           : (size_t)15 * TB * sizeof(float) + scratch_ws;
-    // only at one workgroup per CU: the cache takes the CU's spare LDS, which at larger K
-    // (C5: 4 workgroups per CU) would cost a co-resident rollout workgroup instead
-    if (pl.pair && c->ucache && pl.blocks <= c->num_cus) {
-      // the rest of the CU's LDS keeps the sampled controls of the first steps ([2][T][TB]
-      // floats, 16-byte aligned after the scratch), so the leaf reduction re-reads only the
-      // other steps' normals from HBM (all workgroups reduce at once: a bandwidth burst)
-      // room is left for the deferred optimal rollout of the previous step (mppi_tail_kernel,
-      // 15H floats), which runs beside a rollout workgroup on one CU
-      const size_t base = (pl.lds_bytes + 15) / 16 * 16;
-      const size_t row2 = (size_t)2 * (TB + 4) * sizeof(float);  // UCACHE_ROW: one float4 of bank skew
-      const size_t budget = kLdsBytes - ((size_t)15 * H * sizeof(float) + 2047) / 1024 * 1024;
-      pl.ucache_steps = base < budget ? (int)std::min<size_t>((size_t)H, (budget - base) / row2) : 0;
-      if (pl.ucache_steps > 0) pl.lds_bytes = base + (size_t)pl.ucache_steps * row2;
-    }
+  // rollout kernel: chain + side waves per 64 trajectories, DEM and normals through L1/L2,
+  // rings [D][6][TB] + cost[TB] + flags + nominal + leaf scratch in LDS (profiles/r01_notes.md)
+  const int TB = PAIR_TRAJ;
+  pl.traj_per_block = TB;
+  pl.block = 2 * TB;
+  pl.blocks = (int)((K + TB - 1) / TB);
+  const size_t scratch = ((size_t)(TB + TB / 64) * 4 + 15) / 16 * 16 + (size_t)(TB / 256) * (2 * H + 2) * sizeof(double);
+  pl.lds_bytes = (size_t)(6 * PAIR_RING + 1) * TB * sizeof(float) + 4 * (TB / 64) * sizeof(int) +
+                 (size_t)((2 * H + 3) & ~3) * sizeof(float) + scratch;
+  // only at one workgroup per CU: the cache takes the CU's spare LDS, which at larger K
+  // (C5: 4 workgroups per CU) would cost a co-resident rollout workgroup instead
+  if (c->ucache && pl.blocks <= c->num_cus) {
+    // the rest of the CU's LDS keeps the sampled controls of the first steps ([2][T][TB]
+    // floats, 16-byte aligned after the scratch), so the leaf reduction re-reads only the
+    // other steps' normals from HBM (all workgroups reduce at once: a bandwidth burst)
+    // room is left for the deferred optimal rollout of the previous step (mppi_tail_kernel,
+    // 15H floats), which runs beside a rollout workgroup on one CU
+    const size_t base = (pl.lds_bytes + 15) / 16 * 16;
+    const size_t row2 = (size_t)2 * (TB + 4) * sizeof(float);  // UCACHE_ROW: one float4 of bank skew
+    const size_t budget = kLdsBytes - ((size_t)15 * H * sizeof(float) + 2047) / 1024 * 1024;
+    pl.ucache_steps = base < budget ? (int)std::min<size_t>((size_t)H, (budget - base) / row2) : 0;
+    if (pl.ucache_steps > 0) pl.lds_bytes = base + (size_t)pl.ucache_steps * row2;
   }
   // finish kernel: tree phase [16][2H+2] doubles + 64 x (15 PairScale + 16 m); phase 2
-  // uo[2H] v[H] w[H] sin[H] cos[H] chain[12H] out[16H] floats, then the DEM window
+  // uo[2H] v[H] w[H] sin[H] cos[H] chain[12H] out[16H] floats
   pl.fin_tree_bytes = (size_t)16 * (2 * H + 2) * sizeof(double) + (size_t)64 * (15 * 16 + 16 * 4);
   pl.fin_win_offset = (int)(((size_t)34 * H * sizeof(float) + 15) / 16 * 16);
-  // the optimal rollout stages the window only on request: one workgroup loading 150 KB costs
-  // more than the L2 latency it saves on 100 serial steps (measured, profiles/r01_notes.md)
-  pl.fin_lds = lds_fits && c->dem_path == 1 && (pl.fin_win_offset + win) <= kLdsBytes;
-  pl.fin_lds_bytes = std::max(pl.fin_tree_bytes, (size_t)pl.fin_win_offset + (pl.fin_lds ? win : 0));
+  pl.fin_lds_bytes = std::max(pl.fin_tree_bytes, (size_t)pl.fin_win_offset);
   return pl;
 }
 
@@ -330,24 +291,6 @@ int ensure_nodes(mppi_ctx* c, int blocks) {
   HIP_TRY(hipMalloc(&c->scratch0, half * sizeof(double)));
   HIP_TRY(hipMalloc(&c->scratch1, half * sizeof(double)));
   c->nodes_cap = need;
-  return MPPI_OK;
-}
-
-// Counters and level records of the in-kernel cross-workgroup tree (fused finish).
-int ensure_tree(mppi_ctx* c, int blocks) {
-  size_t groups = 0;
-  for (int n = blocks; n > 1; n = (n + 15) / 16) groups += (size_t)(n + 15) / 16;  // groups of 16
-  groups = std::max<size_t>(groups, 1);
-  if (groups <= c->tree_cap) return MPPI_OK;
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  if (c->tree_cnt) HIP_TRY(hipFree(c->tree_cnt));
-  if (c->tree_nodes) HIP_TRY(hipFree(c->tree_nodes));
-  c->tree_cnt = nullptr;
-  c->tree_nodes = nullptr;
-  HIP_TRY(hipMalloc(&c->tree_cnt, groups * sizeof(unsigned)));
-  HIP_TRY(hipMemset(c->tree_cnt, 0, groups * sizeof(unsigned)));
-  HIP_TRY(hipMalloc(&c->tree_nodes, groups * E_of(c) * sizeof(double)));
-  c->tree_cap = groups;
   return MPPI_OK;
 }
 
@@ -367,10 +310,6 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   a.x_min = c->x_min;
   a.y_min = c->y_min;
   a.res = c->res;
-  a.wx0 = pl.wx0;
-  a.wy0 = pl.wy0;
-  a.W = pl.W;
-  a.Wr = pl.Wr;
   a.cm = c->cm;
   a.cm_size = c->cm_size;
   a.hw = c->cm_hw;
@@ -626,8 +565,7 @@ int flush_speculation(mppi_ctx* c) {
 
 // Enqueue the rollout kernel for the current state / nominal sequence.
 int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl,
-                    const float* unom, const mppi_state& st, const RolloutArgs* dump_args,
-                    const FinishArgs* fused = nullptr, int fused_level = 0) {
+                    const float* unom, const mppi_state& st, const RolloutArgs* dump_args) {
   if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
   int rc = ensure_nodes(c, pl.blocks);
   if (rc) return rc;
@@ -641,36 +579,14 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   RolloutArgs a;
   fill_rollout(c, pl, st, step, unom, a);
   a.wave_prio = c->wave_prio;
-  if (fused) {
-    rc = ensure_tree(c, pl.blocks);
-    if (rc) return rc;
-    a.fused = fused_level;
-    a.fin = *fused;
-    a.tree_cnt = c->tree_cnt;
-    a.tree_nodes = c->tree_nodes;
-    a.noise_ctr = c->noise_ctr;
-  }
-  int eps_slot = -1, next_slot = -1;
+  int eps_slot = -1;
   rc = flush_speculation(c);  // a speculation no finish has flushed (dump / injected paths)
   if (rc) return rc;
   if (c->trace) c->tr_mark[0] = now_us();
-  if (pl.pair && mode == 0 && pl.blocks > 0) {
+  if (mode == 0 && pl.blocks > 0) {
     rc = eps_for_step(c, pl, step, &eps_slot);
     if (rc) return rc;
     a.eps = c->eps[eps_slot];
-    if (fused && fused_level == 2 && !dump_args) {  // generated by the workgroups that finish early
-      next_slot = eps_victim(c, eps_slot, step, 0);
-      if (next_slot < 0) return fail(MPPI_ESTATE, "no free noise slot");
-      a.eps_next = c->eps[next_slot];
-      a.n_base_next = (step + 1) * (uint64_t)((H_of(c) + 1) / 2);
-      for (int i = 0; i < kEpsSlots; ++i)  // the next step's normals come from this kernel only
-        if (c->eps_step[i] == (int64_t)(step + 1)) c->eps_step[i] = -1;
-      c->eps_step[next_slot] = -1;  // being overwritten
-      if (c->eps_pending[next_slot]) {  // an earlier noise-stream fill of that slot
-        HIP_TRY(hipStreamWaitEvent(c->stream, c->eps_ev[next_slot], 0));
-        c->eps_pending[next_slot] = false;
-      }
-    }
   }
   if (dump_args) {
     a.d_traj = dump_args->d_traj;
@@ -685,14 +601,7 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   if (pl.blocks == 0) return MPPI_OK;
   if (c->timing && !dump_args) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   if (c->trace) c->tr_mark[1] = now_us();
-  if (pl.pair) {
-    HIP_TRY(launch_rollout_pair(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr));
-  } else if (pl.ws) {
-    HIP_TRY(launch_rollout_ws(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr));
-  } else {
-    HIP_TRY(launch_rollout(a, pl.block, pl.blocks, pl.lds_bytes, c->stream, pl.lds, proj, mode,
-                           dump_args != nullptr));
-  }
+  HIP_TRY(launch_rollout_pair(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr));
   if (c->trace) c->tr_mark[2] = now_us();
   if (c->timing && !dump_args) {
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
@@ -704,7 +613,7 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     // the noise kernel runs beside this rollout, in its idle issue slots, instead of beside
     // the finish.  The host calls come after the rollout launch (they are not on its path).
     bool spec_done = false;
-    if (eps_slot >= 0 && !dump_args && !a.eps_next && c->prev_roll_valid) {
+    if (eps_slot >= 0 && !dump_args && c->prev_roll_valid) {
       rc = speculate_eps(c, pl, step, eps_slot);
       if (rc) return rc;
       spec_done = true;
@@ -713,11 +622,8 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     c->prev_roll_valid = true;
     if (spec_done) return MPPI_OK;
   }
-  if (a.eps_next) {  // the kernel leaves the next step's normals in the other slot
-    c->eps_step[next_slot] = (int64_t)(step + 1);
-    c->eps_pending[next_slot] = false;  // same stream: ordered before the next rollout
-  } else if (eps_slot >= 0 && !dump_args) {
-    // no fused epilogue: generate them on the noise stream after this rollout
+  if (eps_slot >= 0 && !dump_args) {
+    // the next steps' normals on the noise stream after this rollout
     if (c->noise_at == 1) {  // ... after the finish the caller enqueues next (flush_speculation)
       c->spec_pending = true;
       c->spec_plan = pl;
@@ -797,7 +703,7 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
   // column-split finish (default): one launch, no partial-tree handoff between workgroups
   int cf_P = 0, cf_ncol = 0, cf_groups = 0;
   size_t cf_lds = 0;
-  if (c->colfin && !(f.mode == 1 && pl.fin_lds) && colfin_shape(n, H_of(c), &cf_P, &cf_ncol, &cf_groups, &cf_lds)) {
+  if (c->colfin && colfin_shape(n, H_of(c), &cf_P, &cf_ncol, &cf_groups, &cf_lds)) {
     const size_t need = (size_t)E_of(c);  // f.level1 carries the 2H u_opt floats
     if (c->level1_cap < 1 || c->level1_cap * (size_t)E_of(c) < need) {
       HIP_TRY(hipStreamSynchronize(c->stream));
@@ -808,6 +714,10 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
     }
     f.level1 = c->level1;
     f.level1_cnt = c->level1_cnt;
+    c->fin_kind = 1;
+    c->fin_P = cf_P;
+    c->fin_ncol = cf_ncol;
+    c->fin_groups = cf_groups;
     const size_t lds = std::max(cf_lds, f.mode == 0 ? (size_t)0 : pl.fin_lds_bytes);
     if (timed && c->timing) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     HIP_TRY(launch_colfin(f, lds, c->stream, cf_P, cf_ncol, cf_groups));
@@ -831,9 +741,12 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
     f.level1 = c->level1;
     f.level1_cnt = c->level1_cnt;
   }
+  c->fin_kind = 0;
+  c->fin_P = n;
+  c->fin_ncol = 0;
+  c->fin_groups = groups;
   if (timed && c->timing) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-  HIP_TRY(launch_finish(f, f.mode == 0 ? pl.fin_tree_bytes : pl.fin_lds_bytes, c->stream,
-                        f.mode == 1 && pl.fin_lds, groups));
+  HIP_TRY(launch_finish(f, f.mode == 0 ? pl.fin_tree_bytes : pl.fin_lds_bytes, c->stream, groups));
   if (timed && c->timing) {
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     c->ev_fin_pending = true;
@@ -899,32 +812,6 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   int rc = check_ready(c);
   if (rc) return rc;
   const Plan pl = make_plan(c);
-  if (c->dem_path == 1 && (size_t)pl.W * pl.Wr * sizeof(float) > kLdsBytes)
-    return fail(MPPI_EINVAL, "DEM window does not fit in LDS");
-  if (pl.pair && pl.blocks > 0 && c->fused_level == 2) {  // whole finish in the rollout kernel
-    FinishArgs f;
-    int par = 0;
-    rc = prepare_finish(c, pl, c->st, 1, nullptr, f, par);
-    if (rc) return rc;
-    rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr, &f, 2);
-    if (rc) return rc;
-    remember(c, proj, step, mode, pl);
-    if (f.mode == 2) {
-      rc = enqueue_tail(c, f, par);
-      if (rc) return rc;
-    }
-    return copy_outputs(c, out);
-  }
-  if (pl.pair && pl.blocks > 1 && c->fused_level == 1) {  // first tree level in the rollout kernel
-    FinishArgs unused;
-    std::memset(&unused, 0, sizeof(unused));
-    rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr, &unused, 1);
-    if (rc) return rc;
-    remember(c, proj, step, mode, pl);
-    rc = enqueue_finish(c, pl, c->st, c->tree_nodes, (pl.blocks + 15) / 16, 1, nullptr, true);
-    if (rc) return rc;
-    return copy_outputs(c, out);
-  }
   rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr);
   if (rc) return rc;
   if (c->trace) c->tr_t1 = now_us();
@@ -1075,7 +962,6 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
       c->num_cus = cus;
   }
-  if (const char* e = std::getenv("MPPI_FUSED_FINISH")) c->fused_level = std::min(std::max(std::atoi(e), 0), 2);
   if (const char* e = std::getenv("MPPI_HOST_TRACE")) c->trace = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_COLFIN")) c->colfin = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_UCACHE")) c->ucache = std::atoi(e) != 0;
@@ -1102,7 +988,6 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipHostMalloc(&c->stage, 16 * H * sizeof(float), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&c->done, 64, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->cdiv_bad, sizeof(unsigned)) != hipSuccess ||
-      hipMalloc(&c->noise_ctr, 2 * sizeof(unsigned)) != hipSuccess ||
       hipMalloc(&c->level1_cnt, sizeof(unsigned)) != hipSuccess ||
       hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
@@ -1130,8 +1015,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   c->out_host = new float[16 * H]();
   std::memset(c->stage, 0, 16 * H * sizeof(float));
   *c->done = 0;
-  if (hipMemset(c->noise_ctr, 0, 2 * sizeof(unsigned)) != hipSuccess ||
-      hipMemset(c->level1_cnt, 0, sizeof(unsigned)) != hipSuccess)
+  if (hipMemset(c->level1_cnt, 0, sizeof(unsigned)) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
   if (hipDeviceSynchronize() != hipSuccess) return cleanup(fail(MPPI_EHIP, "device sync failed"));
   *out = c;
@@ -1181,11 +1065,8 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->ev_roll_done) hipEventDestroy(c->ev_roll_done);
   if (c->ev_prev_roll) hipEventDestroy(c->ev_prev_roll);
   if (c->bin_tile_of) hipFree(c->bin_tile_of);
-  if (c->tree_cnt) hipFree(c->tree_cnt);
-  if (c->noise_ctr) hipFree(c->noise_ctr);
   if (c->level1) hipFree(c->level1);
   if (c->level1_cnt) hipFree(c->level1_cnt);
-  if (c->tree_nodes) hipFree(c->tree_nodes);
   if (c->bin_counts) hipFree(c->bin_counts);
   if (c->bin_cursor) hipFree(c->bin_cursor);
   if (c->noise_stream) hipStreamDestroy(c->noise_stream);
@@ -1366,24 +1247,6 @@ int mppi_step_partial(mppi_ctx* c, int32_t proj, uint64_t step, double* record_d
   if (rc) return rc;
   if (!record_dev) return fail(MPPI_EINVAL, "null record buffer");
   const Plan pl = make_plan(c);
-  if (pl.pair && pl.blocks > 0 && c->fused_level == 2) {  // the rank record straight out of the rollout
-    FinishArgs f;
-    int par = 0;
-    rc = prepare_finish(c, pl, c->st, 0, record_dev, f, par);
-    if (rc) return rc;
-    rc = enqueue_rollout(c, proj, step, 0, pl, c->u_nom[c->cur], c->st, nullptr, &f, 2);
-    if (rc) return rc;
-    remember(c, proj, step, 0, pl);
-    return MPPI_OK;
-  }
-  if (pl.pair && pl.blocks > 1 && c->fused_level == 1) {
-    FinishArgs unused;
-    std::memset(&unused, 0, sizeof(unused));
-    rc = enqueue_rollout(c, proj, step, 0, pl, c->u_nom[c->cur], c->st, nullptr, &unused, 1);
-    if (rc) return rc;
-    remember(c, proj, step, 0, pl);
-    return enqueue_finish(c, pl, c->st, c->tree_nodes, (pl.blocks + 15) / 16, 0, record_dev, false);
-  }
   rc = enqueue_rollout(c, proj, step, 0, pl, c->u_nom[c->cur], c->st, nullptr);
   if (rc) return rc;
   remember(c, proj, step, 0, pl);
@@ -1497,19 +1360,12 @@ int mppi_get_timing(mppi_ctx* c, double* roll, double* fin, int64_t* n) {
   return MPPI_OK;
 }
 
-int mppi_set_dem_path(mppi_ctx* c, int32_t mode) {
-  if (!c) return fail(MPPI_EINVAL, "null context");
-  if (mode < 0 || mode > 4) return fail(MPPI_EINVAL, "dem path must be 0, 1, 2, 3 or 4");
-  c->dem_path = mode;
-  return MPPI_OK;
-}
-
 int mppi_get_launch_info(mppi_ctx* c, int64_t* info, int32_t n) {
   if (!c || !info) return fail(MPPI_EINVAL, "null argument");
   const Plan& pl = c->last_plan;
-  const int64_t v[6] = {pl.pair ? 4 : (pl.ws ? 3 : (pl.lds ? 1 : 0)), pl.block, pl.blocks, pl.W, pl.Wr,
-                        (int64_t)pl.lds_bytes};
-  for (int i = 0; i < n && i < 6; ++i) info[i] = v[i];
+  const int64_t v[11] = {0, pl.block, pl.blocks, pl.W, pl.Wr, (int64_t)pl.lds_bytes, c->fin_kind,
+                         c->fin_P, c->fin_ncol, c->fin_groups, pl.ucache_steps};
+  for (int i = 0; i < n && i < 11; ++i) info[i] = v[i];
   return MPPI_OK;
 }
 

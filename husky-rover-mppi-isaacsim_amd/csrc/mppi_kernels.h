@@ -52,7 +52,6 @@ struct RolloutArgs {
   const float4* ntab;  // per-cell normals [(rows+1) x (grid+1)] (mppi_normal_table_kernel)
   int rows, grid;
   float x_min, y_min, res;
-  int wx0, wy0, W, Wr;  // LDS window (cols x rows)
   // costmap
   const float* cm;
   int cm_size;
@@ -85,38 +84,24 @@ struct RolloutArgs {
   const float* inj_u2;
   // dump (DUMP)
   float *d_traj, *d_hv, *d_lw, *d_rw, *d_v, *d_w, *d_u1, *d_u2;
-  // fused tree (pair kernel): the last-arriving workgroup of each aligned group of 16
-  // combines the group's records.  fused 1: that first level only, into tree_nodes, for
-  // mppi_finish_kernel to finish; fused 2: level by level up to the root, whose workgroup
-  // then runs the finish itself (fin.mode 1/2) or stores the rank record (fin.mode 0)
-  int fused;
-  unsigned* tree_cnt;   // zero-initialised counters, one per group of every level (re-armed in-kernel)
-  double* tree_nodes;   // records of the levels above the leaves
-  FinishArgs fin;
-  // the next step's normals, generated by workgroups whose own work is done (null: none)
-  float* eps_next;
-  uint64_t n_base_next;
-  unsigned* noise_ctr;  // [2] work / exit counters, zero-initialised, re-armed in-kernel
   int wave_prio;        // pair kernel: raise the waves' issue priority (s_setprio 2)
   int ucache_steps;     // pair kernel, MODE 0: steps [0, n) keep their sampled controls in LDS
                         // ([2][n][TB] floats after the scratch) for leaf_records
 };
 
 
-hipError_t launch_rollout(const RolloutArgs& a, int block, int blocks, size_t lds, hipStream_t st,
-                          bool use_lds, int proj, int mode, bool dump);
-// warp-specialised rollout: 256 trajectories per 512-thread workgroup
-constexpr int WS_TRAJ = 256;
-hipError_t launch_rollout_ws(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
-                             int mode, bool dump);
-// pair-synchronised variant (LDS progress counters per chain/side pair instead of barriers)
+// The rollout kernel (mppi_rollout_pair_kernel): 256 trajectories per 512-thread workgroup, a
+// chain wave and a side wave per 64 trajectories, synchronised through LDS progress counters
+// over PAIR_RING-deep rings.
+constexpr int PAIR_TRAJ = 256;
 #ifndef MPPI_PAIR_D
 #define MPPI_PAIR_D 8
 #endif
 constexpr int PAIR_RING = MPPI_PAIR_D;  // = PAIR_D in mppi_kernels.hip
 hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
                                int mode, bool dump);
-hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool use_lds, int groups = 1);
+// record tree finish (mppi_finish_kernel): the fallback where the column-split shape does not fit
+hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, int groups = 1);
 // column-split finish: every workgroup builds the pair-scale table and reduces ncol columns
 // over all n records; the last to arrive runs phase 2 (f.level1 holds >= 2H floats, f.level1_cnt
 // a zeroed counter).  colfin_shape returns 0 when n is outside the kernel's range.

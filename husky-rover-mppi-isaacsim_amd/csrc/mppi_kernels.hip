@@ -11,8 +11,8 @@
 //       optimal-sequence filter and the first optimal-rollout step; outputs to host memory.
 //   mppi_tail_kernel  the rest of the optimal rollout, on a side stream.
 //   mppi_noise_kernel the Philox sampling normals, two steps ahead, on a side stream.
-// The earlier single-role kernels (mppi_rollout_kernel, mppi_rollout_ws_kernel,
-// mppi_finish_kernel) remain selectable (mppi_set_dem_path, MPPI_COLFIN=0) and tested.
+// mppi_finish_kernel (the record tree) is the finish where the column split does not fit
+// (MPPI_COLFIN=0 selects it everywhere).
 //
 // Numerics: compile with -ffp-contract=off.  Every float op is one IEEE f32
 // operation in the reference's source order; transcendentals come from
@@ -630,225 +630,6 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
                                              unsigned char* scratch, const float* ub_block,
                                              const float* ucache = nullptr, int uc_steps = 0);
 
-// =====================================================================  rollout kernel
-// Everything one trajectory carries from step to step.
-struct Lane {
-  Traj s;
-  float L, R;                                  // wheel filter state
-  float pf_sum, sw, sp, ob, last_x, last_y;    // critic accumulators
-  float lwx, lwy, lwz, rwx, rwy, rwz;          // wheel points of the last even step
-  float cm_pend;                               // costmap value gathered in the previous step
-};
-
-// Constants of one rollout launch that every step reads.
-template <bool LDS>
-struct StepCtx {
-  const RolloutArgs* a;
-  Dem<LDS> dem;
-  Recip rres_c, rwheel, rT;  // fast-path reciprocals (operands validated on the host)
-  float res_half_neg, res_sq, one_m_fa;
-};
-
-// One rollout-step of one trajectory: filter (sampling_warp.py:120-138), the
-// 3D/2D projection step, and the online critics (critics_warp.py:85-300).
-// Returns the costmap index this step gathers (the value is accumulated next step).
-template <bool F, bool LDS, int PROJ>
-__device__ __forceinline__ int rollout_step(const StepCtx<LDS>& k, int t, float u1, float u2,
-                                            Lane& l, StepOut& o, float& v, float& w, bool& bad) {
-  const RolloutArgs& a = *k.a;
-  Recip rw = k.rwheel, rcm = k.rres_c;
-  if constexpr (!F) {
-    rw.b = a.rwheel;
-    rcm.b = a.res_c;
-  }
-  l.L = l.L * a.fa + (u1 * a.fk) * k.one_m_fa;
-  l.R = l.R * a.fa + (u2 * a.fk) * k.one_m_fa;
-  v = clampf((l.L + l.R) / 2.0f, a.vmin, a.vmax);
-  w = clampf(dv<F>((-l.L) + l.R, rw, bad), a.wmin, a.wmax);
-  float sn, cs;
-  dm_sincosf(w * a.dt, &sn, &cs);
-  if constexpr (PROJ == 3) {
-    float q[4], nx, ny, nz;
-    chain3d<F, LDS>(k.dem, k.res_half_neg, k.res_sq, a.dt, v, sn, cs, l.s, q, nx, ny, nz, bad);
-    wheels3d<F, LDS>(k.dem, a.off, l.s.x, l.s.y, q, nx, ny, nz, l.s.hx, l.s.hy, l.s.hz, o, bad);
-  } else {
-    step2d<F, LDS>(k.dem, a.dt, v, sn, cs, l.s, o, bad);
-  }
-  // _path_follow_critic sum branch (:125-126) over t < H-1; last point (:116)
-  if (t < a.H - 1) l.pf_sum = l.pf_sum + 10.0f * (fabsf(l.s.x - a.gx) + fabsf(l.s.y - a.gy));
-  l.last_x = l.s.x;
-  l.last_y = l.s.y;
-  // _avoid_slope_wheels (:190-216): terms (i, i+2) for even i < H-3
-  if ((t & 1) == 0) {
-    if (t >= 2 && t - 2 < a.H - 3)
-      l.sw = l.sw + slope_term<F>(l.lwx, l.lwy, l.lwz, o.lx, o.ly, o.lz, l.rwx, l.rwy, l.rwz, o.rx,
-                                  o.ry, o.rz, bad);
-    l.lwx = o.lx; l.lwy = o.ly; l.lwz = o.lz;
-    l.rwx = o.rx; l.rwy = o.ry; l.rwz = o.rz;
-  }
-  // _maximise_speed (:296-297)
-  if (a.speed_on) l.sp = l.sp + dv1<F>(a.vmax - v, v + 0.0001f, bad);
-  return costmap_index<F>(a.cm_size, a.hw, rcm, l.s.x, l.s.y, bad, a.rinv_res_c, a.cdiv_res_c);
-}
-
-__device__ __forceinline__ void add_obstacle(const RolloutArgs& a, Lane& l, float cm) {
-  // _avoid_obstacle (critics_warp.py:251-253)
-  if (cm > a.thr) l.ob = l.ob + a.pen;
-  l.ob = l.ob + cm;
-}
-
-template <int BLOCK, bool LDS, int PROJ, int MODE, bool DUMP>
-__global__ __launch_bounds__(BLOCK) void mppi_rollout_kernel(const RolloutArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  float* win = reinterpret_cast<float*>(smem_raw);
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  constexpr int NW = BLOCK / 64;
-
-  // ---- stage the DEM window [wy0, wy0+Wr) x [wx0, wx0+W) into LDS (coalesced rows)
-  if constexpr (LDS) {
-    for (int r = wave; r < a.Wr; r += NW) {
-      const float* src = a.Z + (size_t)(a.wy0 + r) * a.grid + a.wx0;
-      float* dst = win + r * a.W;
-      for (int c = lane; c < a.W; c += 64) dst[c] = src[c];
-    }
-    __syncthreads();
-  }
-  StepCtx<LDS> k;
-  k.a = &a;
-  k.dem.init(a.Z, win, a.rows, a.grid, a.wx0, a.wy0, a.W, a.Wr, a.x_min, a.y_min, a.res, a.rinv_res,
-             a.cdiv_res);
-  {
-    bool unused = false;
-    k.rres_c = rc<true>(a.res_c, unused);
-    k.rwheel = rc<true>(a.rwheel, unused);
-    k.rT = rc<true>(a.T, unused);
-  }
-  k.res_half_neg = (-a.res) / 2.0f;
-  k.res_sq = a.res * a.res;
-  k.one_m_fa = 1.0f - a.fa;
-
-  const int64_t kl = (int64_t)blockIdx.x * BLOCK + tid;  // shard-local trajectory
-  const bool valid = kl < a.K;
-  const uint64_t kg = (uint64_t)(a.k_offset + kl);         // global trajectory (Philox subsequence)
-  const int H = a.H;
-
-  // ---- initial projection at the robot pose (projection_warp.py:306-310), IEEE operators
-  Lane l;
-  l.s.x = a.x0;
-  l.s.y = a.y0;
-  {
-    bool unused = false;
-    float q[4];
-    k.dem.template corners<false>(l.s.x, l.s.y, q, unused);
-    const float vx = k.res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
-    const float vy = k.res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
-    const float nn = sqrtf((vx * vx + vy * vy) + k.res_sq * k.res_sq);
-    const float nx = vx / nn, ny = vy / nn, nz = k.res_sq / nn;
-    if constexpr (PROJ == 3) {
-      const float d = (a.h0x * nx + a.h0y * ny) + a.h0z * nz;
-      const float tx = a.h0x - d * nx, ty = a.h0y - d * ny, tz = a.h0z - d * nz;
-      const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
-      l.s.hx = tx / tn;
-      l.s.hy = ty / tn;
-      l.s.hz = tz / tn;
-    } else {
-      l.s.hx = a.h0x;
-      l.s.hy = a.h0y;
-      l.s.hz = a.h0z;
-    }
-  }
-  l.L = a.wl;
-  l.R = a.wr;
-  l.pf_sum = l.sw = l.sp = l.ob = 0.0f;
-  l.last_x = l.s.x;
-  l.last_y = l.s.y;
-  l.lwx = l.lwy = l.lwz = l.rwx = l.rwy = l.rwz = 0.0f;
-  l.cm_pend = 0.0f;
-
-  // sampled controls are kept for the weighted sum: [ch][t][BLOCK] per workgroup (coalesced)
-  float* ust = a.ustore + (size_t)blockIdx.x * (2 * H) * BLOCK + tid;
-
-  auto one_step = [&](int t, float u1, float u2) {
-    ust[(size_t)t * BLOCK] = u1;
-    ust[(size_t)(H + t) * BLOCK] = u2;
-    const Lane saved = l;
-    StepOut o;
-    float v, w;
-    bool bad = false;
-    int cidx = rollout_step<kFastMath, LDS, PROJ>(k, t, u1, u2, l, o, v, w, bad);
-    if (kFastMath && __builtin_expect(bad, 0)) {  // an operand left the fast-path range: redo with IEEE ops
-      l = saved;
-      cidx = rollout_step<false, LDS, PROJ>(k, t, u1, u2, l, o, v, w, bad);
-    }
-    // the costmap value gathered in step t is accumulated in step t+1 (latency hiding)
-    if (t > 0) add_obstacle(a, l, l.cm_pend);
-    l.cm_pend = a.cm[cidx];
-    if constexpr (DUMP) {
-      if (valid) {
-        const size_t o3 = ((size_t)kl * H + t) * 3;
-        if (a.d_traj) { a.d_traj[o3] = l.s.x; a.d_traj[o3 + 1] = l.s.y; a.d_traj[o3 + 2] = o.z; }
-        if (a.d_hv) { a.d_hv[o3] = l.s.hx; a.d_hv[o3 + 1] = l.s.hy; a.d_hv[o3 + 2] = l.s.hz; }
-        if (a.d_lw) { a.d_lw[o3] = o.lx; a.d_lw[o3 + 1] = o.ly; a.d_lw[o3 + 2] = o.lz; }
-        if (a.d_rw) { a.d_rw[o3] = o.rx; a.d_rw[o3 + 1] = o.ry; a.d_rw[o3 + 2] = o.rz; }
-        const size_t o1 = (size_t)kl * H + t;
-        if (a.d_v) a.d_v[o1] = v;
-        if (a.d_w) a.d_w[o1] = w;
-        if (a.d_u1) a.d_u1[o1] = u1;
-        if (a.d_u2) a.d_u2[o1] = u2;
-      }
-    }
-  };
-
-  // sampled control u[k,t] (sampling_warp.py:71-92, noise DEFINED as Philox + Box-Muller)
-  auto sample = [&](int t, float e1, float e2, float& u1, float& u2) {
-    const int ti = min(t + 1, H - 1);
-    u1 = clampf(a.u_nom1[ti] + a.s1 * e1, a.min_u1, a.max_u1);
-    u2 = clampf(a.u_nom2[ti] + a.s2 * e2, a.min_u2, a.max_u2);
-  };
-
-  for (int t = 0; t < H; t += 2) {
-    float u1a, u2a, u1b, u2b;
-    if constexpr (MODE == 0) {
-      float e1a, e2a, e1b, e2b;
-      noise_block(a.seed, a.n_base + (uint64_t)(t >> 1), kg, &e1a, &e2a, &e1b, &e2b);
-      sample(t, e1a, e2a, u1a, u2a);
-      sample(t + 1, e1b, e2b, u1b, u2b);
-    } else {
-      const size_t o = (size_t)(valid ? kl : 0) * H + t;
-      u1a = a.inj_u1[o];
-      u2a = a.inj_u2[o];
-      u1b = (t + 1 < H) ? a.inj_u1[o + 1] : 0.0f;
-      u2b = (t + 1 < H) ? a.inj_u2[o + 1] : 0.0f;
-    }
-    one_step(t, u1a, u2a);
-    if (t + 1 < H) one_step(t + 1, u1b, u2b);
-  }
-  add_obstacle(a, l, l.cm_pend);
-
-  // ---- _evaluate_trajectories_kernel (critics_warp.py:325-329), costs[] zeroed by reset
-  float pf;
-  if (a.pf_far) {
-    const float dx = l.last_x - a.igx, dy = l.last_y - a.igy;
-    pf = (dx * dx + dy * dy) * a.pf_scale;
-  } else {
-    pf = l.pf_sum;
-  }
-  float cost = a.w_path * pf;
-  cost = cost + a.w_slope * l.sw;
-  cost = cost + a.w_speed * l.sp;
-  cost = cost + a.w_obs * l.ob;
-  if (valid) a.cost_out[kl] = cost;
-
-  // ---- softmax leaf records (DEFINED replacement of critics_warp.py:338-376), shared code
-  __syncthreads();  // LDS window no longer needed: reuse it for the leaf records
-  float* cost_l = reinterpret_cast<float*>(smem_raw);  // [BLOCK]
-  cost_l[tid] = valid ? cost : INFINITY;
-  __syncthreads();
-  leaf_records<BLOCK, BLOCK>(a, cost_l, smem_raw + BLOCK * 4, a.ustore + (size_t)blockIdx.x * (2 * H) * BLOCK);
-}
-
 // =====================================================================  leaf records (shared)
 // Softmax leaf records (DEFINED replacement of critics_warp.py:338-376) for the
 // TB trajectories of a workgroup, whose costs are in cost_lds[TB] and sampled
@@ -979,444 +760,11 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
   }
 }
 
-// =====================================================================  warp-specialised rollout kernel
-// A workgroup of 2*TB threads serves TB trajectories.  Waves [0, TB/64) are
-// CHAIN waves: lane l of chain wave w runs the serial projection
-// (projection_warp.py:314-326) of trajectory 64w + l.  Waves [TB/64, TB/32)
-// are SIDE waves for the same trajectories: Philox noise, sampling, wheel
-// filter and sin/cos ahead of the chain (sampling_warp.py:54-138), wheel
-// contacts and the four critics behind it (projection_warp.py:333-348,
-// critics_warp.py:85-300).  Each SIMD then runs one chain and one side wave,
-// which doubles its issue rate over one wave per SIMD.  Per-step values go
-// through double-buffered LDS rings, one workgroup barrier per phase p:
-//   side : produce step p  (v, sin, cos)       -> in [p & 1]
-//   chain: consume in[(p-1) & 1], run step p-1 -> out[(p-1) & 1] (x, y, right.x, right.y)
-//   side : consume out[(p-2) & 1]: wheels + critics of step p-2
-template <int TB, int PROJ, int MODE, bool DUMP>
-__global__ __launch_bounds__(2 * TB) void mppi_rollout_ws_kernel(const RolloutArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  constexpr int NT = 2 * TB;
-  constexpr int NWC = TB / 64;
-  float* ring_in = reinterpret_cast<float*>(smem_raw);   // [2][3][TB]: v, sin, cos
-  float* ring_out = ring_in + 6 * TB;                    // [2][4][TB]: x, y, cx, cy
-  float* cost_lds = ring_out + 8 * TB;                   // [TB]
-  unsigned char* scratch = reinterpret_cast<unsigned char*>(cost_lds + TB);
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool side = wave >= NWC;
-  const int tj = side ? tid - TB : tid;  // trajectory within the workgroup
-#ifdef MPPI_STAMPS
-  const uint64_t k_t0 = dbg_stamp(), k_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
-  const int64_t kl = (int64_t)blockIdx.x * TB + tj;
-  const bool valid = kl < a.K;
-  const uint64_t kg = (uint64_t)(a.k_offset + kl);
-  const int H = a.H;
-  Dem<false> dem;
-  dem.init(a.Z, nullptr, a.rows, a.grid, 0, 0, 1, 1, a.x_min, a.y_min, a.res, a.rinv_res, a.cdiv_res);
-  const float res_half_neg = (-a.res) / 2.0f;
-  const float res_sq = a.res * a.res;
-  bool nobad = false;
-
-  // ---------------- per-role state
-  Traj s;                       // chain
-  float L = a.wl, R = a.wr;     // side: filter
-  float e1b = 0.f, e2b = 0.f;   // side: noise of the odd step of the current Philox block
-  float vq0 = 0.f, vq1 = 0.f, wq0 = 0.f, wq1 = 0.f;  // side: v, w of steps p-2, p-1
-  float pf_sum = 0.f, sw = 0.f, sp = 0.f, ob = 0.f, last_x = a.x0, last_y = a.y0;
-  float lwx = 0.f, lwy = 0.f, lwz = 0.f, rwx = 0.f, rwy = 0.f, rwz = 0.f;
-  float cm_pend = 0.f;
-  float* ust = a.ustore + (size_t)blockIdx.x * (2 * H) * TB + tj;
-
-  if (!side) {  // initial projection at the robot pose (projection_warp.py:306-310)
-    s.x = a.x0;
-    s.y = a.y0;
-    float q[4];
-    dem.template corners<false>(s.x, s.y, q, nobad);
-    const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
-    const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
-    const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
-    const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
-    if constexpr (PROJ == 3) {
-      const float d = (a.h0x * nx + a.h0y * ny) + a.h0z * nz;
-      const float tx = a.h0x - d * nx, ty = a.h0y - d * ny, tz = a.h0z - d * nz;
-      const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
-      s.hx = tx / tn;
-      s.hy = ty / tn;
-      s.hz = tz / tn;
-    } else {
-      s.hx = a.h0x;
-      s.hy = a.h0y;
-      s.hz = a.h0z;
-    }
-  }
-
-  // ---- side: wheels + critics of step sc (branch-free: conditions become selects)
-  auto consume = [&](int sc, bool even) __attribute__((always_inline)) {
-    const float* ro = ring_out + (sc & 1) * 4 * TB + tj;
-    const float x = ro[0], y = ro[TB], cx = ro[2 * TB], cy = ro[3 * TB];
-    float lx = 0.f, ly = 0.f, lz = 0.f, rx = 0.f, ry = 0.f, rz = 0.f;
-    if constexpr (PROJ == 3) {
-      lx = x + cx;
-      ly = y + cy;
-      lz = dem.template point<false>(lx, ly, nobad);
-      rx = x - cx;
-      ry = y - cy;
-      rz = dem.template point<false>(rx, ry, nobad);
-    }
-    Recip rcm;
-    rcm.b = a.res_c;
-    const float cm_now = a.cm[costmap_index<false>(a.cm_size, a.hw, rcm, x, y, nobad, a.rinv_res_c, a.cdiv_res_c)];
-    const float pft = pf_sum + 10.0f * (fabsf(x - a.gx) + fabsf(y - a.gy));
-    pf_sum = (sc < H - 1) ? pft : pf_sum;   // _path_follow_critic sum over t < H-1
-    last_x = x;
-    last_y = y;
-    if (even) {  // _avoid_slope_wheels terms (i, i+2), even i < H-3
-      const float term = slope_term<false>(lwx, lwy, lwz, lx, ly, lz, rwx, rwy, rwz, rx, ry, rz, nobad);
-      sw = (sc >= 2 && sc - 2 < H - 3) ? sw + term : sw;
-      lwx = lx; lwy = ly; lwz = lz;
-      rwx = rx; rwy = ry; rwz = rz;
-    }
-    const float spt = sp + (a.vmax - vq0) / (vq0 + 0.0001f);  // _maximise_speed
-    sp = a.speed_on ? spt : sp;
-    // _avoid_obstacle: the costmap value gathered in the previous consume
-    const float ob1 = (cm_pend > a.thr) ? ob + a.pen : ob;
-    ob = (sc > 0) ? ob1 + cm_pend : ob;
-    cm_pend = cm_now;
-    if constexpr (DUMP) {
-      if (valid) {
-        const size_t o3 = ((size_t)kl * H + sc) * 3;
-        if (a.d_lw) { a.d_lw[o3] = lx; a.d_lw[o3 + 1] = ly; a.d_lw[o3 + 2] = lz; }
-        if (a.d_rw) { a.d_rw[o3] = rx; a.d_rw[o3 + 1] = ry; a.d_rw[o3 + 2] = rz; }
-        const size_t o1 = (size_t)kl * H + sc;
-        if (a.d_v) a.d_v[o1] = vq0;
-        if (a.d_w) a.d_w[o1] = wq0;
-      }
-    }
-  };
-  // ---- side: noise, sampling, filter, sin/cos of step p
-  auto produce = [&](int p, bool even, float& vp, float& wp) __attribute__((always_inline)) {
-    float u1, u2;
-    if constexpr (MODE == 0) {
-      float e1, e2;
-      if (even) {
-        noise_block(a.seed, a.n_base + (uint64_t)(p >> 1), kg, &e1, &e2, &e1b, &e2b);
-      } else {
-        e1 = e1b;
-        e2 = e2b;
-      }
-      const int ti = min(p + 1, H - 1);
-      u1 = clampf(a.u_nom1[ti] + a.s1 * e1, a.min_u1, a.max_u1);
-      u2 = clampf(a.u_nom2[ti] + a.s2 * e2, a.min_u2, a.max_u2);
-    } else {
-      const size_t o = (size_t)(valid ? kl : 0) * H + p;
-      u1 = a.inj_u1[o];
-      u2 = a.inj_u2[o];
-    }
-    ust[(size_t)p * TB] = u1;
-    ust[(size_t)(H + p) * TB] = u2;
-    L = L * a.fa + (u1 * a.fk) * (1.0f - a.fa);
-    R = R * a.fa + (u2 * a.fk) * (1.0f - a.fa);
-    vp = clampf((L + R) / 2.0f, a.vmin, a.vmax);
-    wp = clampf(((-L) + R) / a.rwheel, a.wmin, a.wmax);
-    float* ri = ring_in + (p & 1) * 3 * TB + tj;
-    ri[0] = vp;
-    ri[TB] = wp;
-    if constexpr (DUMP) {
-      if (valid) {
-        const size_t o1 = (size_t)kl * H + p;
-        if (a.d_u1) a.d_u1[o1] = u1;
-        if (a.d_u2) a.d_u2[o1] = u2;
-      }
-    }
-  };
-  // ---- chain: step sc (sin/cos of w*dt evaluated here: it overlaps the position update)
-  auto chain_step = [&](int sc) __attribute__((always_inline)) {
-    const float* ri = ring_in + (sc & 1) * 3 * TB + tj;
-    const float v = ri[0], wv = ri[TB];
-    float sn, cs;
-    dm_sincosf(wv * a.dt, &sn, &cs);
-    float cx = 0.f, cy = 0.f, z = 0.f;
-    float q[4];
-    if constexpr (PROJ == 3) {
-      float nx, ny, nz;
-      bool bad = false;
-      const Traj saved = s;
-      chain3d<kChainFast, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-      if (kChainFast && __builtin_expect(bad, 0)) {  // operand outside the fast range: IEEE redo
-        s = saved;
-        chain3d<false, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-      }
-      cx = a.off * (ny * s.hz - nz * s.hy);
-      cy = a.off * (nz * s.hx - nx * s.hz);
-      if constexpr (DUMP) z = bilinear<false>(s.x, s.y, q, dem.template rr<false>(), nobad);
-    } else {
-      StepOut o;
-      step2d<false, false>(dem, a.dt, v, sn, cs, s, o, nobad);
-      z = o.z;
-    }
-    float* ro = ring_out + (sc & 1) * 4 * TB + tj;
-    ro[0] = s.x;
-    ro[TB] = s.y;
-    ro[2 * TB] = cx;
-    ro[3 * TB] = cy;
-    if constexpr (DUMP) {
-      if (valid) {
-        const size_t o3 = ((size_t)kl * H + sc) * 3;
-        if (a.d_traj) { a.d_traj[o3] = s.x; a.d_traj[o3 + 1] = s.y; a.d_traj[o3 + 2] = z; }
-        if (a.d_hv) { a.d_hv[o3] = s.hx; a.d_hv[o3 + 1] = s.hy; a.d_hv[o3 + 2] = s.hz; }
-      }
-    }
-  };
-#ifdef MPPI_STAMPS
-  uint64_t st_work = 0, st_wait = 0;
-#endif
-  // one phase: flags are compile-time constants at the peeled call sites below
-  auto phase = [&](int p, bool prod, bool cons, bool chain, bool even) __attribute__((always_inline)) {
-#ifdef MPPI_STAMPS
-    const uint64_t t0 = dbg_stamp();
-#endif
-    if (side) {
-      if (cons) consume(p - 2, even);
-      float vp = 0.f, wp = 0.f;
-      if (prod) produce(p, even, vp, wp);
-      vq0 = vq1;
-      vq1 = vp;
-      wq0 = wq1;
-      wq1 = wp;
-    } else if (chain) {
-      chain_step(p - 1);
-    }
-#ifdef MPPI_STAMPS
-    const uint64_t t1 = dbg_stamp();
-#endif
-    __syncthreads();
-#ifdef MPPI_STAMPS
-    const uint64_t t2 = dbg_stamp();
-    st_work += t1 - t0;
-    st_wait += t2 - t1;
-#endif
-  };
-
-  if (H >= 4) {
-    phase(0, true, false, false, true);
-    phase(1, true, false, true, false);
-    int p = 2;
-    for (; p + 1 < H; p += 2) {
-      phase(p, true, true, true, true);
-      phase(p + 1, true, true, true, false);
-    }
-    if (p < H) {  // odd H: one more producing (even) phase
-      phase(p, true, true, true, true);
-      ++p;
-    }
-    if ((H & 1) == 0) {
-      phase(H, false, true, true, true);
-      phase(H + 1, false, true, false, false);
-    } else {
-      phase(H, false, true, true, false);
-      phase(H + 1, false, true, false, true);
-    }
-  } else {
-    for (int p = 0; p < H + 2; ++p) phase(p, p < H, p >= 2, p >= 1 && p <= H, (p & 1) == 0);
-  }
-#ifdef MPPI_STAMPS
-  if ((tid & 63) == 0 && blockIdx.x < 64) {
-    g_dbg_stamps[(blockIdx.x * (NT / 64) + wave) * 2] = st_work;
-    g_dbg_stamps[(blockIdx.x * (NT / 64) + wave) * 2 + 1] = st_wait;
-  }
-#endif
-  if (side) {
-    if (cm_pend > a.thr) ob = ob + a.pen;  // last step's obstacle term
-    ob = ob + cm_pend;
-    // _evaluate_trajectories_kernel (critics_warp.py:325-329)
-    float pf;
-    if (a.pf_far) {
-      const float dx = last_x - a.igx, dy = last_y - a.igy;
-      pf = (dx * dx + dy * dy) * a.pf_scale;
-    } else {
-      pf = pf_sum;
-    }
-    float cost = a.w_path * pf;
-    cost = cost + a.w_slope * sw;
-    cost = cost + a.w_speed * sp;
-    cost = cost + a.w_obs * ob;
-    if (valid) a.cost_out[kl] = cost;
-    cost_lds[tj] = valid ? cost : INFINITY;
-  }
-  __syncthreads();
-#ifdef MPPI_STAMPS
-  const uint64_t k_t1 = dbg_stamp();
-#endif
-  leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
-#ifdef MPPI_STAMPS
-  const uint64_t k_t2 = dbg_stamp(), k_r2 = __builtin_amdgcn_s_memrealtime();
-  if ((tid & 63) == 0 && blockIdx.x < 64) {
-    uint64_t* g = g_dbg_stamps + 64 * 16 * 2 + (blockIdx.x * (NT / 64) + wave) * 4;
-    g[0] = k_t1 - k_t0;   // start .. end of phase loop + cost
-    g[1] = k_t2 - k_t1;   // leaf records
-    g[2] = k_r2 - k_r0;   // wall (100 MHz ticks)
-    g[3] = k_t2 - k_t0;   // total shader cycles
-  }
-  if (tid == 0 && blockIdx.x < 1024) {
-    uint64_t* g = g_dbg_stamps + 64 * 16 * 6 + blockIdx.x * 2;
-    g[0] = k_r0;
-    g[1] = k_r2;
-  }
-#endif
-}
-
-template <bool LDS>
-__device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, unsigned char* smem, int tid,
-                                              int nthreads);
-
-// Cross-workgroup softmax tree without a second kernel: the last workgroup of each
-// aligned group of 16 to arrive combines the group's records (four levels of the
-// binary tree, as mppi_finish_kernel / oracle tree_reduce), level by level, until
-// one record remains; that workgroup then stores the rank record (fin.mode 0) or
-// runs the finish (fin.mode 1/2).  Release/acquire fences at device scope make the
-// records written on other XCDs visible; each counter is re-armed by its last
-// arriver for the next launch.
-template <int NT>
-__device__ __forceinline__ bool fused_tree_finish(const RolloutArgs& a, unsigned char* smem, int tid) {
-  const int H = a.H, E = 2 * H + 2;
-  int* flag = reinterpret_cast<int*>(smem);
-  int idx = blockIdx.x, count = gridDim.x;
-  const double* src = a.nodes;
-  double* dst = a.tree_nodes;
-  unsigned* cnt = a.tree_cnt;
-#ifdef MPPI_STAMPS
-  int lvl_dbg = 0;
-  FIN_STAMP(6);
-#endif
-  constexpr int G = 16;  // aligned groups of 16 records: 256 workgroups -> 16 -> 1
-  int levels = (a.fused == 1) ? 1 : 64;  // fused 1: the first level only, mppi_finish_kernel does the rest
-  while (count > 1 && levels-- > 0) {
-    const int g = idx / G;
-    const int gsize = min(G, count - G * g);
-    const int groups = (count + G - 1) / G;
-    __syncthreads();  // this workgroup's record is complete
-    if (tid == 0) {
-      __threadfence();  // release it device-wide
-      const unsigned prev = atomicAdd(&cnt[g], 1u);
-      const int last = prev == (unsigned)(gsize - 1);
-      if (last) cnt[g] = 0u;
-      flag[0] = last;
-    }
-    __syncthreads();
-    if (!flag[0]) return false;
-    __threadfence();  // acquire the other members' records
-#ifdef MPPI_STAMPS
-    FIN_STAMP(7 + 2 * lvl_dbg);
-#endif
-    // the group's G-1 pair scales once, level by level, into LDS; then every element
-    float* lm = reinterpret_cast<float*>(smem + 16);                      // [G]
-    PairScale* lps = reinterpret_cast<PairScale*>(smem + 16 + 4 * G);      // [G-1]
-    if (tid < G) lm[tid] = (tid < gsize) ? (float)src[(size_t)(G * g + tid) * E] : INFINITY;
-    __syncthreads();
-    int base = 0;
-#pragma unroll
-    for (int w = G / 2; w >= 1; w >>= 1) {
-      PairScale p;
-      if (tid < w) {
-        p = pair_scale(lm[2 * tid], lm[2 * tid + 1], a.T);
-        lps[base + tid] = p;
-      }
-      __syncthreads();
-      if (tid < w) lm[tid] = p.m;
-      __syncthreads();
-      base += w;
-    }
-    for (int j = tid; j < E; j += NT) {
-      double v[G];
-#pragma unroll
-      for (int i = 0; i < G; ++i) v[i] = (i < gsize) ? src[(size_t)(G * g + i) * E + j] : 0.0;
-      dst[(size_t)g * E + j] = group_apply<G>(lps, v, j);
-    }
-    src = dst;
-    dst += (size_t)groups * E;
-    cnt += groups;
-    idx = g;
-    count = groups;
-#ifdef MPPI_STAMPS
-    FIN_STAMP(8 + 2 * lvl_dbg);
-    ++lvl_dbg;
-#endif
-  }
-  __syncthreads();  // src[idx * E ..] is the root (written by this workgroup)
-  if (a.fused == 1) return true;  // first level only: the group records go to mppi_finish_kernel
-  const double* root = src + (size_t)idx * E;
-  if (a.fin.mode == 0) {
-    for (int j = tid; j < E; j += NT) a.fin.record_out[j] = root[j];
-    return true;
-  }
-  const double S = root[1];
-  const float ures = (tid < 2 * H && S > 0.0) ? (float)(root[2 + tid] / S) : 0.0f;
-  __syncthreads();
-  finish_phase2<false>(a.fin, ures, smem, tid, NT);
-  return true;
-}
-
-// The next step's sampling normals (mppi_noise_kernel's work), shared out in chunks of
-// 4 Philox rows x 256 trajectories among the workgroups whose own work is done: they
-// finish at different times (the last one runs the finish), so the generation fills
-// the CUs the kernel would otherwise leave idle.  The last workgroup to leave re-arms
-// the counters.
-template <int NT>
-__device__ __forceinline__ void noise_ahead(const RolloutArgs& a, unsigned char* smem, int tid) {
-  int* sh = reinterpret_cast<int*>(smem);
-  if (a.eps_next) {
-    const int H = a.H;
-    const int NB = (H + 1) >> 1, NB4 = (NB + 3) >> 2;
-    const int total = (int)gridDim.x * NB4;
-    const int tj = tid & 255;
-    __syncthreads();
-    if (tid == 0) sh[0] = (int)atomicAdd(&a.noise_ctr[0], 1u);
-    __syncthreads();
-    int c = sh[0];
-    while (c < total) {
-      __syncthreads();
-      if (tid == 0) sh[0] = (int)atomicAdd(&a.noise_ctr[0], 1u);  // the next chunk, fetched ahead
-      const int blk = c / NB4, n0 = (c - blk * NB4) * 4;
-      const uint64_t kg = (uint64_t)(a.k_offset + (int64_t)blk * 256 + tj);
-#pragma unroll
-      for (int r = 0; r < 4; r += NT / 256) {
-        const int n = n0 + r + (tid >> 8);
-        if (n < NB) {
-          float a1, a2, b1, b2;
-          noise_block(a.seed, a.n_base_next + (uint64_t)n, kg, &a1, &a2, &b1, &b2);
-          const int t = 2 * n;
-          float* e1 = a.eps_next + ((size_t)blk * 2 * H + t) * 256 + tj;
-          float* e2 = e1 + (size_t)H * 256;
-          e1[0] = a1;
-          e2[0] = a2;
-          if (t + 1 < H) {
-            e1[256] = b1;
-            e2[256] = b2;
-          }
-        }
-      }
-      __syncthreads();
-      c = sh[0];
-    }
-  }
-  if (tid == 0 && a.noise_ctr) {
-    __threadfence();
-    const unsigned left = atomicAdd(&a.noise_ctr[1], 1u);
-    if (left == gridDim.x - 1) {  // every workgroup is past its last atomicAdd on [0]
-      a.noise_ctr[0] = 0u;
-      a.noise_ctr[1] = 0u;
-    }
-  }
-}
-
 // =====================================================================  pair-synchronised rollout kernel
-// Same roles as mppi_rollout_ws_kernel (chain wave c and side wave c serve the
-// trajectories 64c..64c+63), but each chain/side PAIR synchronises only with
-// itself, through three LDS progress counters, instead of all eight waves
-// meeting at a workgroup barrier every step.  Deeper rings (PAIR_D steps) let
-// a pair absorb step-to-step jitter (DEM gather latency) instead of paying the
-// slowest of eight waves every step:
+// Chain wave c and side wave c serve the trajectories 64c..64c+63 (lane = trajectory).
+// Each chain/side PAIR synchronises only with itself, through LDS progress
+// counters, never at a workgroup barrier.  Rings PAIR_D steps deep let a pair
+// absorb step-to-step jitter (DEM gather latency):
 //   chain step s : needs produced > s and consumed > s - D        -> chained = s + 1
 //   side  iter p : produce p   (needs chained > p - D)           -> produced = p + 1
 //                  consume p-L (needs chained > p - L)           -> consumed = p - L + 1
@@ -1784,12 +1132,6 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
                                a.ucache_steps);
   else
     leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
-  if constexpr (!DUMP) {
-    if (a.fused) {
-      fused_tree_finish<NT>(a, smem_raw, tid);  // the rings are dead: reuse their LDS
-      if (a.fused == 2) noise_ahead<NT>(a, smem_raw, tid);
-    }
-  }
 #ifdef MPPI_STAMPS
   const uint64_t k_t2 = dbg_stamp(), k_r2 = __builtin_amdgcn_s_memrealtime();
   if ((tid & 63) == 0 && blockIdx.x < 64) {
@@ -2744,62 +2086,6 @@ __global__ __launch_bounds__(256) void mppi_selftest_kernel(int what, int64_t n,
 }
 
 // =====================================================================  launchers
-template <int BLOCK, bool LDS, int PROJ, int MODE, bool DUMP>
-static hipError_t launch_rollout_t(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((mppi_rollout_kernel<BLOCK, LDS, PROJ, MODE, DUMP>), dim3(blocks), dim3(BLOCK),
-                     lds, st, a);
-  return hipGetLastError();
-}
-
-template <int BLOCK, bool LDS, int PROJ>
-static hipError_t launch_rollout_m(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st,
-                                   int mode, bool dump) {
-  if (mode == 0) {
-    if (dump) return launch_rollout_t<BLOCK, LDS, PROJ, 0, true>(a, blocks, lds, st);
-    return launch_rollout_t<BLOCK, LDS, PROJ, 0, false>(a, blocks, lds, st);
-  }
-  if (dump) return launch_rollout_t<BLOCK, LDS, PROJ, 1, true>(a, blocks, lds, st);
-  return launch_rollout_t<BLOCK, LDS, PROJ, 1, false>(a, blocks, lds, st);
-}
-
-template <int BLOCK>
-static hipError_t launch_rollout_b(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st,
-                                   bool use_lds, int proj, int mode, bool dump) {
-  if (use_lds) {
-    if (proj == 3) return launch_rollout_m<BLOCK, true, 3>(a, blocks, lds, st, mode, dump);
-    return launch_rollout_m<BLOCK, true, 2>(a, blocks, lds, st, mode, dump);
-  }
-  if (proj == 3) return launch_rollout_m<BLOCK, false, 3>(a, blocks, lds, st, mode, dump);
-  return launch_rollout_m<BLOCK, false, 2>(a, blocks, lds, st, mode, dump);
-}
-
-hipError_t launch_rollout(const RolloutArgs& a, int block, int blocks, size_t lds, hipStream_t st,
-                          bool use_lds, int proj, int mode, bool dump) {
-  switch (block) {
-    case 256: return launch_rollout_b<256>(a, blocks, lds, st, use_lds, proj, mode, dump);
-    case 512: return launch_rollout_b<512>(a, blocks, lds, st, use_lds, proj, mode, dump);
-    case 1024: return launch_rollout_b<1024>(a, blocks, lds, st, use_lds, proj, mode, dump);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-template <int TB, int PROJ>
-static hipError_t launch_ws_m(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int mode,
-                              bool dump) {
-  if (mode == 0) {
-    if (dump)
-      hipLaunchKernelGGL((mppi_rollout_ws_kernel<TB, PROJ, 0, true>), dim3(blocks), dim3(2 * TB), lds, st, a);
-    else
-      hipLaunchKernelGGL((mppi_rollout_ws_kernel<TB, PROJ, 0, false>), dim3(blocks), dim3(2 * TB), lds, st, a);
-  } else {
-    if (dump)
-      hipLaunchKernelGGL((mppi_rollout_ws_kernel<TB, PROJ, 1, true>), dim3(blocks), dim3(2 * TB), lds, st, a);
-    else
-      hipLaunchKernelGGL((mppi_rollout_ws_kernel<TB, PROJ, 1, false>), dim3(blocks), dim3(2 * TB), lds, st, a);
-  }
-  return hipGetLastError();
-}
-
 template <int TB, int PROJ>
 static hipError_t launch_pair_m(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int mode,
                                 bool dump) {
@@ -2823,17 +2109,8 @@ hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hip
   return launch_pair_m<256, 2>(a, blocks, lds, st, mode, dump);
 }
 
-hipError_t launch_rollout_ws(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
-                             int mode, bool dump) {
-  if (proj == 3) return launch_ws_m<256, 3>(a, blocks, lds, st, mode, dump);
-  return launch_ws_m<256, 2>(a, blocks, lds, st, mode, dump);
-}
-
-hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, bool use_lds, int groups) {
-  if (use_lds)
-    hipLaunchKernelGGL(mppi_finish_kernel<true>, dim3(groups), dim3(FIN_THREADS), lds, st, f);
-  else
-    hipLaunchKernelGGL(mppi_finish_kernel<false>, dim3(groups), dim3(FIN_THREADS), lds, st, f);
+hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, int groups) {
+  hipLaunchKernelGGL(mppi_finish_kernel<false>, dim3(groups), dim3(FIN_THREADS), lds, st, f);
   return hipGetLastError();
 }
 

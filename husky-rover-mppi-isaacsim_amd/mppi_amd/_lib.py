@@ -89,7 +89,6 @@ _PROTOS = {
     "mppi_get_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_int64)]),
     "mppi_get_tail_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
-    "mppi_set_dem_path": (C.c_int, [C.c_void_p, C.c_int32]),
     "mppi_get_launch_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]),
     "mppi_bilinear_query": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
     "mppi_selftest": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.POINTER(C.c_int64)]),
@@ -346,11 +345,6 @@ class Engine:
         self._c(self.lib.mppi_get_nominal(self.ctx, _fp(u1), _fp(u2)), "mppi_get_nominal")
         return u1, u2
 
-    def set_dem_path(self, mode):
-        self._c(self.lib.mppi_set_dem_path(self.ctx, {"auto": 0, "lds": 1, "global": 2, "ws": 3, "pair": 4}.get(mode, mode)),
-                "mppi_set_dem_path")
-
-    # ------------------------------------------------------------ steps
     def _outputs(self):
         H = self.H
         b = self._buf
@@ -429,9 +423,10 @@ class Engine:
         return t.value, n.value
 
     def launch_info(self):
-        info = (C.c_int64 * 6)()
-        self._c(self.lib.mppi_get_launch_info(self.ctx, info, 6), "mppi_get_launch_info")
-        keys = ("dem_in_lds", "block", "blocks", "window_cols", "window_rows", "lds_bytes")
+        info = (C.c_int64 * 11)()
+        self._c(self.lib.mppi_get_launch_info(self.ctx, info, 11), "mppi_get_launch_info")
+        keys = ("reserved", "block", "blocks", "window_cols", "window_rows", "lds_bytes", "finish_kind",
+                "finish_records", "finish_ncol", "finish_groups", "ucache_steps")
         return dict(zip(keys, [int(v) for v in info]))
 
     def selftest(self, what, n=1 << 24, seed=1):

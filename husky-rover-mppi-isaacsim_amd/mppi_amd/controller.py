@@ -177,8 +177,7 @@ class MPPI_Controller:
 
     Extra (optional) config section ``engine:`` — ``seed`` (Philox key, default
     42 as default_rng(42) at :409), ``device`` (HIP device, default 0),
-    ``kernel`` ("default" | "ws" | "lds" | "global"), ``max_loops`` (run(),
-    default 3500 as :763).
+    ``max_loops`` (run(), default 3500 as :763), ``async_tail``.
     """
 
     def __init__(self, surface, robot, config_path, goal_x, goal_y, goal_orientation):
@@ -211,7 +210,6 @@ class MPPI_Controller:
         eng = config.get("engine", {}) or {}
         self.seed = int(eng.get("seed", 42))
         self.device = int(eng.get("device", 0))
-        self.kernel = eng.get("kernel", "default")
         self.max_loops = int(eng.get("max_loops", 3500))
         # deferred optimal rollout: MPPI_step returns with the controls and row 0 of the
         # *_sim arrays; the other rows are fetched on first access (bitwise identical)
@@ -235,7 +233,6 @@ class MPPI_Controller:
         if self.engine is not None:
             self.engine.close()
         self.engine = _lib.Engine(self._params(), self.device)
-        self.engine.set_dem_path({"default": "auto"}.get(self.kernel, self.kernel))
         self.engine.set_async_tail(self.async_tail)
         self._tail_fresh = True
         self._upload_dem(self.surface.Z)

@@ -212,17 +212,12 @@ int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_
 /* HIP-event time of the deferred optimal-rollout kernels (side stream). */
 int mppi_get_tail_timing(mppi_ctx* ctx, double* tail_ms, int64_t* launches);
 
-/* Rollout kernel variant: 0 = default (= 4); 1 = one wave per trajectory group
- * with the DEM window staged in LDS (error if it does not fit); 2 = one wave per
- * trajectory group, DEM read through L1/L2; 3 = warp-specialised (a chain wave
- * and a side wave per 64 trajectories, DEM through L1/L2, one workgroup barrier
- * per step); 4 = warp-specialised, each chain/side pair synchronised through LDS
- * progress counters.  All variants give bitwise identical results. */
-int mppi_set_dem_path(mppi_ctx* ctx, int32_t mode);
-
-/* Layout/launch facts for the last step (for tests and the bench):
- * info[0]=dem_in_lds, [1]=block threads, [2]=blocks, [3]=window cols,
- * [4]=window rows, [5]=lds bytes. */
+/* Layout/launch facts for the last step (for tests and the bench), up to 11 values:
+ * info[0]=0 (reserved), [1]=rollout block threads, [2]=rollout blocks, [3]/[4]=cols/rows of
+ * the DEM window the step's lanes can touch, [5]=rollout LDS bytes, [6]=finish kind (1 =
+ * column-split mppi_colfin_kernel, 0 = record tree mppi_finish_kernel), [7]=records padded
+ * (column-split) or records (tree), [8]=columns per finish workgroup, [9]=finish workgroups,
+ * [10]=steps whose sampled controls the rollout keeps in LDS. */
 int mppi_get_launch_info(mppi_ctx* ctx, int64_t* info, int32_t n);
 
 /* Standalone DEM bilinear kernel: for n query points

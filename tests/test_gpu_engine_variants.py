@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 KEYS = ("u1_opt", "u2_opt", "lin_vel", "ang_vel")
 
 
-def _run(env, K, H, steps=3):
+def _run(env, K, H, steps=3, info=None):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
@@ -43,6 +43,8 @@ def _run(env, K, H, steps=3):
         o = eng.step("3d", i)
         outs.append({k: o[k].copy() for k in KEYS})
     costs = eng.costs()
+    if info is not None:
+        info.update(eng.launch_info())
     eng.close()
     return outs, costs
 
@@ -64,9 +66,15 @@ def test_variant_bitwise_equal(K, H, env):
 @pytest.mark.parametrize("K,H", [(1048576, 40), (1048576, 100)])
 def test_column_split_finish_at_4096_records(K, H):
     """n = 4096 leaf records: the column-split finish's levels above one wave (H=40), and the
-    record-tree fallback where (columns + 1) x (records / 16) exceeds the workgroup (H=100)."""
-    ref, ref_costs = _run({"MPPI_COLFIN": "0"}, K, H, steps=2)
-    got, got_costs = _run({}, K, H, steps=2)
+    record-tree fallback where (columns + 1) x (records / 16) exceeds the workgroup (H=100).
+    launch_info names the finish that ran; the oracle pins H=100 in test_gpu_headline.py."""
+    i_ref, i_got = {}, {}
+    ref, ref_costs = _run({"MPPI_COLFIN": "0"}, K, H, steps=2, info=i_ref)
+    got, got_costs = _run({}, K, H, steps=2, info=i_got)
+    assert i_ref["finish_kind"] == 0 and i_ref["finish_records"] == 4096
+    assert i_got["finish_kind"] == (1 if H == 40 else 0), i_got
+    if H == 40:
+        assert i_got["finish_records"] == 4096 and i_got["finish_ncol"] >= 2
     np.testing.assert_array_equal(got_costs, ref_costs)
     for i, (a, b) in enumerate(zip(got, ref)):
         for k in KEYS:

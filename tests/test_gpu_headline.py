@@ -86,6 +86,8 @@ def test_c4_full_size_step():
     eng = hp.engine_for(K4, H3, Z, hw, cm, st, seed=7)
     out = eng.step("3d", 0)
     _assert_outputs(out, ref, eng.costs())
+    info = eng.launch_info()   # 4096 records at H=100: the record-tree finish (column split does not fit)
+    assert info["finish_kind"] == 0 and info["finish_records"] == 4096 and info["blocks"] == 4096
     eng.close()
 
 
