@@ -48,6 +48,7 @@ struct Plan {
   size_t lds_bytes = 0, fin_lds_bytes = 0, fin_tree_bytes = 0;
   int fin_win_offset = 0;
   int ucache_steps = 0;   // pair kernel: steps whose sampled controls stay in LDS for the leaf
+  bool roles = false;     // the role-split rollout kernel (mppi_rollout_roles_kernel)
 };
 
 }  // namespace
@@ -131,6 +132,8 @@ struct mppi_ctx {
   double tr_msum[4] = {0, 0, 0, 0};
   long tr_n = 0;
   int wave_prio = 1;  // rollout waves raise their issue priority (env MPPI_WAVE_PRIO=0: off)
+  int roles = -1;     // rollout kernel: -1 auto (role split at <= 1 workgroup per CU), 0 pair, 1 roles (MPPI_ROLES)
+  int noise_gpc = 0;  // noise kernel workgroups per CU: 0 auto (2 beside the role split, else 4) (MPPI_NOISE_GPC)
   hipEvent_t ev_roll_done = nullptr;
   hipEvent_t ev_prev_roll = nullptr;  // recorded after the last rollout that read an eps slot
   // finish: column-split u_opt slice records / first tree level, arrival counter
@@ -249,13 +252,17 @@ Plan make_plan(const mppi_ctx* c) {
   pl.wy0 = std::min(std::max(j0 - Rc, 0), c->rows - pl.Wr);
   const int64_t K = c->p.num_trajectories;
   // rollout kernel: chain + side waves per 64 trajectories, DEM and normals through L1/L2,
-  // rings [D][6][TB] + cost[TB] + flags + nominal + leaf scratch in LDS (profiles/r01_notes.md)
+  // rings [D][PAIR_RING_IN + 4][TB] + cost[TB] + flags + nominal + leaf scratch in LDS (profiles/r01_notes.md)
   const int TB = PAIR_TRAJ;
   pl.traj_per_block = TB;
-  pl.block = 2 * TB;
   pl.blocks = (int)((K + TB - 1) / TB);
+  // role split where the rollout is latency-bound (at most one workgroup per CU); the pair
+  // kernel's 8 waves per workgroup pack 4 workgroups per CU at larger K (MPPI_ROLES=0/1 forces)
+  pl.roles = c->roles < 0 ? pl.blocks <= c->num_cus : c->roles != 0;
+  pl.block = (pl.roles ? ROLES_WAVES_PER_TRAJ_WAVE : 2) * TB;
   const size_t scratch = ((size_t)(TB + TB / 64) * 4 + 15) / 16 * 16 + (size_t)(TB / 256) * (2 * H + 2) * sizeof(double);
-  pl.lds_bytes = (size_t)(6 * PAIR_RING + 1) * TB * sizeof(float) + 4 * (TB / 64) * sizeof(int) +
+  const size_t ring_rows = pl.roles ? (size_t)(4 + 4) * PAIR_RING + 2 : (size_t)(PAIR_RING_IN + 4) * PAIR_RING + 1;
+  pl.lds_bytes = ring_rows * TB * sizeof(float) + 4 * (TB / 64) * sizeof(int) +
                  (size_t)((2 * H + 3) & ~3) * sizeof(float) + scratch;
   // only at one workgroup per CU: the cache takes the CU's spare LDS, which at larger K
   // (C5: 4 workgroups per CU) would cost a co-resident rollout workgroup instead
@@ -277,6 +284,14 @@ Plan make_plan(const mppi_ctx* c) {
   pl.fin_win_offset = (int)(((size_t)34 * H * sizeof(float) + 15) / 16 * 16);
   pl.fin_lds_bytes = std::max(pl.fin_tree_bytes, (size_t)pl.fin_win_offset);
   return pl;
+}
+
+// Noise grid: a few 4-wave workgroups per CU.  The noise of step i+2 runs beside the finish of
+// step i and the start of rollout i+1; beside the role-split rollout (16 waves) and the deferred
+// optimal rollout (4 waves) only 2 per CU leave the rollout's wave slots free.
+int noise_groups(const mppi_ctx* c, const Plan& pl) {
+  const int gpc = c->noise_gpc > 0 ? c->noise_gpc : (pl.roles ? 2 : 4);
+  return std::max(c->num_cus, 1) * gpc;
 }
 
 int ensure_nodes(mppi_ctx* c, int blocks) {
@@ -503,7 +518,8 @@ int eps_for_step(mppi_ctx* c, const Plan& pl, uint64_t step, int* slot_out) {
       c->eps_pending[i] = false;
     }
   const int slot = 0;
-  HIP_TRY(launch_noise(c->p.seed, step * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[slot], c->stream));
+  HIP_TRY(launch_noise(c->p.seed, step * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[slot], c->stream,
+                       noise_groups(c, pl)));
   for (int i = 0; i < kEpsSlots; ++i) c->eps_step[i] = -1;
   c->eps_step[slot] = (int64_t)step;
   *slot_out = slot;
@@ -544,7 +560,7 @@ int speculate_eps(mppi_ctx* c, const Plan& pl, uint64_t step, int used) {
       waited = true;
     }
     HIP_TRY(launch_noise(c->p.seed, target * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[slot],
-                         c->noise_stream));
+                         c->noise_stream, noise_groups(c, pl)));
     HIP_TRY(hipEventRecord(c->eps_ev[slot], c->noise_stream));
     c->eps_step[slot] = (int64_t)target;
     c->eps_pending[slot] = true;
@@ -601,7 +617,7 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   if (pl.blocks == 0) return MPPI_OK;
   if (c->timing && !dump_args) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   if (c->trace) c->tr_mark[1] = now_us();
-  HIP_TRY(launch_rollout_pair(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr));
+  HIP_TRY(launch_rollout_pair(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr, pl.roles));
   if (c->trace) c->tr_mark[2] = now_us();
   if (c->timing && !dump_args) {
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
@@ -968,6 +984,8 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   if (const char* e = std::getenv("MPPI_NOISE_AHEAD")) c->noise_ahead = std::atoi(e) == 1 ? 1 : 2;
   if (const char* e = std::getenv("MPPI_NOISE_AT")) c->noise_at = std::min(std::max(std::atoi(e), 0), 2);
   if (const char* e = std::getenv("MPPI_WAVE_PRIO")) c->wave_prio = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MPPI_ROLES")) c->roles = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MPPI_NOISE_GPC")) c->noise_gpc = std::max(std::atoi(e), 0);
   const char* ep = std::getenv("MPPI_STREAM_PRIO");
   const bool use_prio = !(ep && std::atoi(ep) == 0);
   const int H = p.num_iterations;

@@ -98,8 +98,18 @@ constexpr int PAIR_TRAJ = 256;
 #define MPPI_PAIR_D 8
 #endif
 constexpr int PAIR_RING = MPPI_PAIR_D;  // = PAIR_D in mppi_kernels.hip
+// sin / cos of the Rodrigues angle computed by the side wave at production and handed to the
+// chain through the ring (v, sin, cos), off the chain's serial path; 0 = the chain computes them
+#ifndef MPPI_SC_SIDE
+#define MPPI_SC_SIDE 0
+#endif
+constexpr int PAIR_RING_IN = MPPI_SC_SIDE ? 3 : 2;  // floats per trajectory and step, side -> chain
 hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
-                               int mode, bool dump);
+                               int mode, bool dump, bool roles = false);
+// The role-split rollout kernel (mppi_rollout_roles_kernel): the same 256 trajectories per
+// workgroup over 1024 threads, one wave per role (chain, producer, wheel, cost) and 64
+// trajectories; rings [D][4 + 4][TB] + cost[TB] + slope[TB] in LDS.
+constexpr int ROLES_WAVES_PER_TRAJ_WAVE = 4;
 // record tree finish (mppi_finish_kernel): the fallback where the column-split shape does not fit
 hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, int groups = 1);
 // column-split finish: every workgroup builds the pair-scale table and reduces ncol columns
@@ -118,7 +128,7 @@ hipError_t launch_cdiv_verify(float b, float y, unsigned* bad, hipStream_t st);
 // The sampling normals of one step (Philox block n_base + t/2 of global trajectory k_offset + k),
 // laid out [blocks][2][H][256]: eps1 rows then eps2 rows, 256 trajectories per row.
 hipError_t launch_noise(uint64_t seed, uint64_t n_base, int64_t k_offset, int blocks, int H, float* eps,
-                        hipStream_t st);
+                        hipStream_t st, int max_groups);
 hipError_t launch_bilinear(const float* Z, int rows, int grid, float x_min, float y_min, float res,
                            const float* xs, const float* ys, float* hs, int64_t n, hipStream_t st);
 // LDS-tiled lookup over queries binned by 64x64-cell DEM tile (tile count = ceil(rows/64)*ceil(cols/64))

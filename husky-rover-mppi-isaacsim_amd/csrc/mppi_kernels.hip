@@ -218,7 +218,13 @@ struct Dem {
   // column), so the table has (rows + 1) x (grid + 1) entries
   __device__ __forceinline__ float4 normal_cell(int i, int j) const {
     const int ii = min(i, grid - 1) + 1, jj = min(j, rows - 1) + 1;
+#if defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 1  // diagnostic builds only: one cell (L1 hits)
+    return N[(uint32_t)((jj * (grid + 1) + ii) & 0)];
+#elif defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 2  // diagnostic: no load
+    return make_float4(__builtin_bit_cast(float, jj) * 1e-30f, __builtin_bit_cast(float, ii) * 1e-30f, 1.0f, 0.f);
+#else
     return N[(uint32_t)(jj * (grid + 1) + ii)];
+#endif
   }
   template <bool F>
   __device__ __forceinline__ float point(float x, float y, bool& bad) const {
@@ -444,6 +450,126 @@ __device__ __forceinline__ void chain3d_lean(const Dem<false>& dem, float res_ha
     s.hz = lean_div(rz, r, l);
   }
   bad |= lean_bad(l);
+}
+
+// ---------------------------------------------------------------------  packed chain (roles kernel)
+// The role-split kernel's chain wave is bound by its own instruction issue (one wave issues
+// about one instruction per 5 cycles, whatever its type), so the serial step is written with
+// packed-FP32 instructions (v_pk_mul / v_pk_add / v_pk_fma: the x and y components in one
+// instruction, each lane an ordinary IEEE f32 operation, results unchanged) wherever the
+// reference computes the same operation on x and y.  Range guards and the IEEE redo as
+// chain3d_lean.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 bc2(float s) { return f2{s, s}; }
+
+// sqrt_cr with the two neighbour residuals in one packed fma:
+// sqrt_cr = sdn + [rdn > 0] + [rup > 0] (rdn <= 0 < rup is impossible: sdn < sup).
+// The tests stay float compares: with the residual lanes bit-cast to integers, this
+// compiler (ROCm 7.2 LLVM) folded lane 1's test onto lane 0's (sdn + 2 [rdn > 0]).
+__device__ __forceinline__ float sqrt_cr2(float n) {
+  const float s = __builtin_amdgcn_sqrtf(n);
+  const int si = __builtin_bit_cast(int, s);
+  const f2 nb = {__builtin_bit_cast(float, si - 1), __builtin_bit_cast(float, si + 1)};
+  const f2 r = pk_fma(-nb, bc2(s), bc2(n));
+  const int inc_dn = r.x > 0.0f ? 1 : 0;
+  const int inc_up = r.y > 0.0f ? 1 : 0;
+  return __builtin_bit_cast(float, (si - 1) + inc_dn + inc_up);
+}
+__device__ __forceinline__ Recip lean_norm2(float n, Lean& l) {
+  const int nb = __builtin_bit_cast(int, n);
+  l.nlo = min(l.nlo, nb);
+  l.nhi = max(l.nhi, nb);
+  Recip r;
+  r.b = sqrt_cr2(n);
+  const float y0 = __builtin_amdgcn_rcpf(r.b);
+  r.y = __builtin_fmaf(__builtin_fmaf(-r.b, y0, 1.0f), y0, y0);
+  return r;
+}
+// (a.x, a.y) / r.b, each lane lean_div
+__device__ __forceinline__ f2 lean_div2(f2 a, const Recip& r, Lean& l) {
+  l.emin = min(l.emin, min(__builtin_amdgcn_frexp_expf(a.x), __builtin_amdgcn_frexp_expf(a.y)));
+  const f2 b = bc2(r.b), y = bc2(r.y);
+  const f2 q0 = a * y;
+  const f2 e0 = pk_fma(-b, q0, a);
+  const f2 q1 = pk_fma(e0, y, q0);
+  const f2 e1 = pk_fma(-b, q1, a);
+  const f2 q2 = pk_fma(e1, y, q1);
+  return f2{__builtin_copysignf(q2.x, a.x), __builtin_copysignf(q2.y, a.y)};
+}
+// cross(n, o).xy = (ny oz - nz oy, nz ox - nx oz), as (ny oz, -nx oz) + (-nz oy, nz ox)
+__device__ __forceinline__ f2 cross_xy(f2 nxy, float nz, f2 oxy, float oz) {
+  const f2 p1 = nxy.yx * f2{oz, -oz};
+  const f2 p2 = f2{-nz, nz} * oxy.yx;
+  return p1 + p2;
+}
+
+struct Head {  // heading vector (x, y packed)
+  f2 xy;
+  float z;
+};
+
+// _get_heading_tangent_vector + _update_orientation (projection_warp.py:168-248): the new heading
+// from the previous one, the surface normal n and sin / cos / (1 - cos) of w dt.
+template <bool F>
+__device__ __forceinline__ Head orient_step(f2 nxy, float nz, const Head& h, float sn, float cs, float omc,
+                                           Lean& l) {
+  const f2 hn = h.xy * nxy;
+  const float d = (hn.x + hn.y) + h.z * nz;
+  const f2 pxy = h.xy - bc2(d) * nxy;
+  const float pz = h.z - d * nz;
+  f2 txy, oxy;
+  float tz, oz;
+  if constexpr (F) {
+    const f2 p2 = pxy * pxy;
+    const Recip r = lean_norm2((p2.x + p2.y) + pz * pz, l);
+    txy = lean_div2(pxy, r, l);
+    tz = lean_div(pz, r, l);
+    const f2 t2 = txy * txy;
+    const Recip ro = lean_norm2((t2.x + t2.y) + tz * tz, l);
+    oxy = lean_div2(txy, ro, l);
+    oz = lean_div(tz, ro, l);
+  } else {
+    const float pn = sqrtf((pxy.x * pxy.x + pxy.y * pxy.y) + pz * pz);
+    txy = f2{pxy.x / pn, pxy.y / pn};
+    tz = pz / pn;
+    const float tn = sqrtf((txy.x * txy.x + txy.y * txy.y) + tz * tz);
+    oxy = f2{txy.x / tn, txy.y / tn};
+    oz = tz / tn;
+  }
+  const f2 cxy = cross_xy(nxy, nz, oxy, oz);
+  const f2 cz2 = nxy * oxy.yx;
+  const float crz = cz2.x - cz2.y;
+  const f2 no = nxy * oxy;
+  const float dn = (no.x + no.y) + nz * oz;
+  const f2 rxy = (oxy * bc2(cs) + cxy * bc2(sn)) + (nxy * bc2(dn)) * bc2(omc);
+  const float rz = (oz * cs + crz * sn) + (nz * dn) * omc;
+  Head o;
+  if constexpr (F) {
+    const f2 r2 = rxy * rxy;
+    const Recip r = lean_norm2((r2.x + r2.y) + rz * rz, l);
+    o.xy = lean_div2(rxy, r, l);
+    o.z = lean_div(rz, r, l);
+  } else {
+    const float rn = sqrtf((rxy.x * rxy.x + rxy.y * rxy.y) + rz * rz);
+    o.xy = f2{rxy.x / rn, rxy.y / rn};
+    o.z = rz / rn;
+  }
+  return o;
+}
+// _update_position (projection_warp.py:207-223): pos + normalize(h).xy * v * dt
+template <bool F>
+__device__ __forceinline__ f2 advance_step(const Head& h, float v, float dt, f2 pos, Lean& l) {
+  f2 u;
+  if constexpr (F) {
+    const f2 h2 = h.xy * h.xy;
+    const Recip r = lean_norm2((h2.x + h2.y) + h.z * h.z, l);
+    u = lean_div2(h.xy, r, l);
+  } else {
+    const float hn = sqrtf((h.xy.x * h.xy.x + h.xy.y * h.xy.y) + h.z * h.z);
+    u = f2{h.xy.x / hn, h.xy.y / hn};
+  }
+  return pos + (u * bc2(v)) * bc2(dt);
 }
 
 // Height and wheel contacts of a rollout-step (projection_warp.py:318, :333-348),
@@ -801,8 +927,9 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   constexpr int NT = 2 * TB;
   constexpr int NWC = TB / 64;
   constexpr int D = PAIR_D;
-  float* ring_in = reinterpret_cast<float*>(smem_raw);   // [D][2][TB]: v, w
-  float* ring_out = ring_in + D * 2 * TB;                // [D][4][TB]: x, y, cx, cy
+  constexpr int RI = PAIR_RING_IN;
+  float* ring_in = reinterpret_cast<float*>(smem_raw);   // [D][RI][TB]: v, w or v, sin, cos
+  float* ring_out = ring_in + D * RI * TB;               // [D][4][TB]: x, y, cx, cy
   float* cost_lds = ring_out + D * 4 * TB;               // [TB]
   int* flags = reinterpret_cast<int*>(cost_lds + TB);    // [4][NWC]: produced, chained, consumed, -
   float* unom_lds = reinterpret_cast<float*>(flags + 4 * NWC);  // [2H] u_nom1 | u_nom2 (padded to 4)
@@ -914,10 +1041,15 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
     for (int sc = 0; sc < H; ++sc) {
       wait_ge(f_prod, sc + 1, seen_prod);
       wait_ge(f_cons, sc - D + 1, seen_cons);
-      const float* ri = ring_in + (sc % D) * 2 * TB + tj;
-      const float v = ri[0], wv = ri[TB];
-      float sn, cs;  // sin/cos of the Rodrigues angle: independent of the chain state, so it
-      dm_sincosf(wv * a.dt, &sn, &cs);  // overlaps the position update (measured cheaper here than in the side)
+      const float* ri = ring_in + (sc % D) * RI * TB + tj;
+      const float v = ri[0];
+      float sn, cs;  // sin/cos of the Rodrigues angle: independent of the chain state
+#if MPPI_SC_SIDE
+      sn = ri[TB];
+      cs = ri[2 * TB];
+#else
+      dm_sincosf(ri[TB] * a.dt, &sn, &cs);
+#endif
       float cx = 0.f, cy = 0.f, z = 0.f;
       float q[4];
       if constexpr (PROJ == 3) {
@@ -1007,9 +1139,18 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
         R = R * a.fa + (u2 * a.fk) * (1.0f - a.fa);
         const float vp = clampf((L + R) / 2.0f, a.vmin, a.vmax);
         const float wp = clampf(((-L) + R) / a.rwheel, a.wmin, a.wmax);
-        float* ri = ring_in + (p % D) * 2 * TB + tj;
+        float* ri = ring_in + (p % D) * RI * TB + tj;
         ri[0] = vp;
+#if MPPI_SC_SIDE
+        {
+          float sn, cs;
+          dm_sincosf(wp * a.dt, &sn, &cs);
+          ri[TB] = sn;
+          ri[2 * TB] = cs;
+        }
+#else
         ri[TB] = wp;
+#endif
         if constexpr (DUMP) {
           if (valid) {
             const size_t o1 = (size_t)kl * H + p;
@@ -1025,7 +1166,7 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
         wait_ge(f_chain, sc + 1, seen_chain);
         const float* ro = ring_out + (sc % D) * 4 * TB + tj;
         const float x = ro[0], y = ro[TB], cx = ro[2 * TB], cy = ro[3 * TB];
-        const float vq = ring_in[(sc % D) * 2 * TB + tj];  // v of step sc (slot not reused yet)
+        const float vq = ring_in[(sc % D) * RI * TB + tj];  // v of step sc (slot not reused yet)
         if constexpr (!ODD) {  // contacts of an even step: heights in flight until the odd half
           if constexpr (PROJ == 3) {
             elx = x + cx;
@@ -1147,6 +1288,467 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
     g[1] = k_r2;
   }
 #endif
+}
+
+// =====================================================================  role-split rollout kernel
+// Four waves per 64 trajectories (lane = trajectory), one per role, wave = role * NG + group,
+// so the four roles of a group share one SIMD:
+//   CHAIN  the serial projection (projection_warp.py:314-326), as the pair kernel's chain wave;
+//   PROD   sampling, wheel filter (sampling_warp.py:54-138) and sin / cos of the Rodrigues angle
+//          -> ring_in (v, sin, cos);
+//   WHEEL  wheel contacts and heights of the even steps and the slope critic
+//          (projection_warp.py:333-348, critics_warp.py:220-267);
+//   COST   costmap gather, obstacle, path-follow and speed critics (critics_warp.py:85-300).
+// One wave issues at most one instruction per ~4 cycles whatever its type, and the SIMD takes
+// up to ~2 waves' worth of VALU issue (profiles/ubench/issue.hip): the chain wave's
+// instruction count per step bounds the kernel, so everything off its recurrence runs in the
+// other three waves, whose own streams are then shorter than the chain's.
+// Progress counters per group (LDS), each wave caching the last value it acquired:
+//   CHAIN step s : produced > s, wheel > s - D, cost > s - D   (ring_out slot s % D free)
+//   PROD  step p : cost > p - D   (ring_in slot p % D read by CHAIN and COST; COST waited on CHAIN)
+//   WHEEL / COST step s : chained > s
+// Deadlock-free: no wave waits on a later step of a wave that waits on it.
+constexpr int ROLE_CHAIN = 0, ROLE_PROD = 1, ROLE_WHEEL = 2, ROLE_COST = 3, NROLES = 4;
+
+template <int TB, int PROJ, int MODE, bool DUMP>
+__global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const RolloutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  constexpr int NT = NROLES * TB;
+  constexpr int NG = TB / 64;  // trajectory groups (waves per role)
+  constexpr int D = PAIR_D;
+  constexpr int RI = 4;
+  static_assert(TB == 256, "UCACHE_ROW assumes 256 trajectories per workgroup");
+  float* ring_in = reinterpret_cast<float*>(smem_raw);   // [D][4][TB]: v, sin, cos, 1 - cos
+  float* ring_out = ring_in + D * RI * TB;               // [D][4][TB]: x, y, cx, cy
+  float* cost_lds = ring_out + D * 4 * TB;               // [TB]
+  float* sw_lds = cost_lds + TB;                         // [TB] slope critic (WHEEL -> COST)
+  int* flags = reinterpret_cast<int*>(sw_lds + TB);      // [4][NG]: produced, chained, wheel, cost
+  float* unom_lds = reinterpret_cast<float*>(flags + 4 * NG);  // [2H] u_nom1 | u_nom2 (padded to 4)
+  unsigned char* scratch = reinterpret_cast<unsigned char*>(unom_lds + ((2 * a.H + 3) & ~3));
+  float* ucache = reinterpret_cast<float*>(
+      smem_raw + ((size_t)(scratch - smem_raw) + ((TB + TB / 64) * 4 + 15) / 16 * 16 +
+                  (size_t)(TB / 256) * (2 * a.H + 2) * sizeof(double) + 15) / 16 * 16);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int role = wave / NG;
+  const int grp = wave - role * NG;
+  const int tj = grp * 64 + (tid & 63);  // trajectory within the workgroup
+  if (a.wave_prio) {  // above the deferred optimal rollout (priority 0); the chain above all
+    if (role == ROLE_CHAIN) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(2);
+  }
+  int* f_prod = flags + grp;
+  int* f_chain = flags + NG + grp;
+  int* f_wheel = flags + 2 * NG + grp;
+  int* f_cost = flags + 3 * NG + grp;
+  const int64_t kl = (int64_t)blockIdx.x * TB + tj;
+  const bool valid = kl < a.K;
+  const int H = a.H;
+  Dem<false> dem;
+  dem.init(a.Z, nullptr, a.rows, a.grid, 0, 0, 1, 1, a.x_min, a.y_min, a.res, a.rinv_res, a.cdiv_res);
+  dem.N = a.ntab;
+  const float res_half_neg = (-a.res) / 2.0f;
+  const float res_sq = a.res * a.res;
+  bool nobad = false;
+  if (tid < 4 * NG) flags[tid] = 0;
+  if constexpr (MODE == 0)
+    for (int i = tid; i < 2 * H; i += NT) unom_lds[i] = i < H ? a.u_nom1[i] : a.u_nom2[i - H];
+  __syncthreads();  // flags and nominal sequence initialised
+
+#ifdef MPPI_STAMPS
+  const uint64_t k_t0 = dbg_stamp();
+  uint64_t st_wait = 0, st_n = 0;
+#endif
+  auto wait_ge = [&](const int* f, int target, int& seen) __attribute__((always_inline)) {
+    if (seen >= target) return;
+#ifdef MPPI_STAMPS
+    const uint64_t t0 = dbg_stamp();
+#endif
+    int v;
+    while ((v = lds_load_acquire(f)) < target) __builtin_amdgcn_s_sleep(1);
+    seen = v;
+#ifdef MPPI_STAMPS
+    st_wait += dbg_stamp() - t0;
+    st_n += 1;
+#endif
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  float c_pf = 0.f, c_sp = 0.f, c_ob = 0.f;  // COST: the critic sums, kept across the barrier
+
+  if (role == ROLE_CHAIN) {
+    // ---------------- the serial projection, one step per iteration
+    Traj s;
+    s.x = a.x0;
+    s.y = a.y0;
+    {  // initial projection at the robot pose (projection_warp.py:306-310)
+      float q[4];
+      dem.template corners<false>(s.x, s.y, q, nobad);
+      const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
+      const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
+      const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
+      const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
+      if constexpr (PROJ == 3) {
+        const float d = (a.h0x * nx + a.h0y * ny) + a.h0z * nz;
+        const float tx = a.h0x - d * nx, ty = a.h0y - d * ny, tz = a.h0z - d * nz;
+        const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
+        s.hx = tx / tn;
+        s.hy = ty / tn;
+        s.hz = tz / tn;
+      } else {
+        s.hx = a.h0x;
+        s.hy = a.h0y;
+        s.hz = a.h0z;
+      }
+    }
+    int seen_prod = 0, seen_wheel = 0, seen_cost = 0;
+    if constexpr (PROJ == 3) {
+      // Software-pipelined: iteration t orients step t (its normal gathered during iteration
+      // t - 1), then advances the position of step t + 1 and issues that step's normal gather,
+      // which stays in flight while step t's outputs are published.  Register sets A / B
+      // alternate between steps (no loop-carried copy of a load in flight).
+      Head hd{f2{s.hx, s.hy}, s.hz};
+      f2 posA = f2{s.x, s.y}, posB = posA;
+      float4 nvA = make_float4(0.f, 0.f, 0.f, 0.f), nvB = nvA;
+      float snA = 0.f, csA = 0.f, omA = 0.f, snB = 0.f, csB = 0.f, omB = 0.f;
+      const f2 cell_off = f2{-a.x_min, a.y_min};
+      const float fi_hi = (float)(a.grid - 1), fj_lo = (float)(1 - a.rows);
+      const float4* ntab0 = dem.N + (a.grid + 2);  // entry (jj, ii) = (1 - tjj, ti + 1): offset ti - tjj * (grid + 1)
+      const int nrow = a.grid + 1;
+      // normal-table entry of the cell holding pos (Dem::cell + Dem::normal_cell)
+      auto gather = [&](f2 pos, float4& nv) __attribute__((always_inline)) {
+        f2 f;
+        if (dem.cdiv) {  // uniform: division by the verified reciprocal (cdiv_f), both axes at once
+          const f2 aa = pos + cell_off;
+          const f2 q0 = aa * bc2(dem.rinv);
+          const f2 r = pk_fma(-q0, bc2(dem.res), aa);
+          f = pk_fma(r, bc2(dem.rinv), q0);
+        } else {
+          f = f2{(pos.x - a.x_min) / a.res, (pos.y + a.y_min) / a.res};
+        }
+        const int ti = (int)__builtin_amdgcn_fmed3f(f.x, -1.0f, fi_hi);  // min(i, grid - 1)
+        const int tjj = (int)__builtin_amdgcn_fmed3f(f.y, fj_lo, 1.0f);  // -min(j, rows - 1)
+        nv = ntab0[ti - tjj * nrow];
+      };
+      auto read_in = [&](int t, float& v, float& sn, float& cs, float& om) __attribute__((always_inline)) {
+        wait_ge(f_prod, t + 1, seen_prod);
+        const float* ri = ring_in + (t % D) * RI * TB + tj;
+        v = ri[0];
+        sn = ri[TB];
+        cs = ri[2 * TB];
+        om = ri[3 * TB];
+      };
+      {  // step 0's position and normal
+        float v0;
+        read_in(0, v0, snA, csA, omA);
+        Lean l;
+        lean_init(l);
+        f2 p = advance_step<true>(hd, v0, a.dt, posA, l);
+        if (__builtin_expect(lean_bad(l), 0)) p = advance_step<false>(hd, v0, a.dt, posA, l);
+        posA = p;
+        gather(posA, nvA);
+      }
+      // step t in set X (pos, normal in flight, sin / cos / 1 - cos); step t + 1 into set Y
+      auto it = [&](int t, f2& pX, float4& nX, float& snX, float& csX, float& omX, f2& pY, float4& nY,
+                    float& snY, float& csY, float& omY) __attribute__((always_inline)) {
+        const bool more = t + 1 < H;  // uniform
+        float v1 = 0.f;
+        if (more) read_in(t + 1, v1, snY, csY, omY);
+        const f2 nxy = f2{nX.x, nX.y};
+        const float nz = nX.z;
+        Lean l;
+        lean_init(l);
+        Head ho = orient_step<true>(nxy, nz, hd, snX, csX, omX, l);
+        f2 p1 = pX;
+        if (more) p1 = advance_step<true>(ho, v1, a.dt, pX, l);
+        if (__builtin_expect(lean_bad(l), 0)) {  // operand outside the fast range: IEEE redo
+          ho = orient_step<false>(nxy, nz, hd, snX, csX, omX, l);
+          if (more) p1 = advance_step<false>(ho, v1, a.dt, pX, l);
+        }
+        if (more) {
+          pY = p1;
+          gather(pY, nY);
+        }
+        // wheel offset right = 0.2 * cross(normal, current_hv) (projection_warp.py:333)
+        const f2 cxy = bc2(a.off) * cross_xy(nxy, nz, ho.xy, ho.z);
+        wait_ge(f_wheel, t - D + 1, seen_wheel);
+        wait_ge(f_cost, t - D + 1, seen_cost);
+        float* ro = ring_out + (t % D) * 4 * TB + tj;
+        ro[0] = pX.x;
+        ro[TB] = pX.y;
+        ro[2 * TB] = cxy.x;
+        ro[3 * TB] = cxy.y;
+        if constexpr (DUMP) {
+          if (valid) {
+            float q[4];
+            dem.template corners<false>(pX.x, pX.y, q, nobad);
+            const float z = bilinear<false>(pX.x, pX.y, q, dem.template rr<false>(), nobad);
+            const size_t o3 = ((size_t)kl * H + t) * 3;
+            if (a.d_traj) { a.d_traj[o3] = pX.x; a.d_traj[o3 + 1] = pX.y; a.d_traj[o3 + 2] = z; }
+            if (a.d_hv) { a.d_hv[o3] = ho.xy.x; a.d_hv[o3 + 1] = ho.xy.y; a.d_hv[o3 + 2] = ho.z; }
+          }
+        }
+        lds_store_release(f_chain, t + 1);
+        hd = ho;
+      };
+      int t = 0;
+      for (; t + 1 < H; t += 2) {
+        it(t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
+        it(t + 1, posB, nvB, snB, csB, omB, posA, nvA, snA, csA, omA);
+      }
+      if (t < H) it(t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
+    } else
+    for (int sc = 0; sc < H; ++sc) {
+      wait_ge(f_prod, sc + 1, seen_prod);
+      wait_ge(f_wheel, sc - D + 1, seen_wheel);
+      wait_ge(f_cost, sc - D + 1, seen_cost);
+      const float* ri = ring_in + (sc % D) * RI * TB + tj;
+      const float v = ri[0], sn = ri[TB], cs = ri[2 * TB];
+      float cx = 0.f, cy = 0.f, z = 0.f;
+      float q[4];
+      if constexpr (PROJ == 3) {
+        float nx, ny, nz;
+        bool bad = false;
+        const Traj saved = s;
+        chain3d_lean<true>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+        if constexpr (DUMP) dem.template corners<false>(s.x, s.y, q, nobad);  // heights: dump only
+        if (__builtin_expect(bad, 0)) {  // operand outside the fast range: IEEE redo
+          s = saved;
+          chain3d<false, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+        }
+        cx = a.off * (ny * s.hz - nz * s.hy);
+        cy = a.off * (nz * s.hx - nx * s.hz);
+        if constexpr (DUMP) z = bilinear<false>(s.x, s.y, q, dem.template rr<false>(), nobad);
+      } else {
+        StepOut o;
+        step2d<false, false>(dem, a.dt, v, sn, cs, s, o, nobad);
+        z = o.z;
+      }
+      float* ro = ring_out + (sc % D) * 4 * TB + tj;
+      ro[0] = s.x;
+      ro[TB] = s.y;
+      ro[2 * TB] = cx;
+      ro[3 * TB] = cy;
+      if constexpr (DUMP) {
+        if (valid) {
+          const size_t o3 = ((size_t)kl * H + sc) * 3;
+          if (a.d_traj) { a.d_traj[o3] = s.x; a.d_traj[o3 + 1] = s.y; a.d_traj[o3 + 2] = z; }
+          if (a.d_hv) { a.d_hv[o3] = s.hx; a.d_hv[o3 + 1] = s.hy; a.d_hv[o3 + 2] = s.hz; }
+        }
+      }
+      lds_store_release(f_chain, sc + 1);
+    }
+  } else if (role == ROLE_PROD) {
+    // ---------------- sampling + wheel filter + sin/cos, normals prefetched two steps ahead
+    // (even / odd steps in their own registers: no loop-carried copy of a load in flight)
+    const float* eps_row = (MODE == 0) ? a.eps + (size_t)blockIdx.x * (2 * H) * TB + tj : nullptr;
+    float* ust = a.ustore + (size_t)blockIdx.x * (2 * H) * TB + tj;
+    float L = a.wl, R = a.wr;
+    int seen_cost = 0;
+    float eA1 = 0.f, eA2 = 0.f, eB1 = 0.f, eB2 = 0.f;
+    if constexpr (MODE == 0) {
+      eA1 = eps_row[0];
+      eA2 = eps_row[(size_t)H * TB];
+      const int t1 = min(1, H - 1);
+      eB1 = eps_row[(size_t)t1 * TB];
+      eB2 = eps_row[(size_t)(H + t1) * TB];
+    }
+    auto prod = [&](int p, float& e1r, float& e2r) __attribute__((always_inline)) {
+      float u1, u2;
+      if constexpr (MODE == 0) {
+        const int ti = min(p + 1, H - 1);
+        u1 = clampf(unom_lds[ti] + a.s1 * e1r, a.min_u1, a.max_u1);
+        u2 = clampf(unom_lds[H + ti] + a.s2 * e2r, a.min_u2, a.max_u2);
+        if (p < a.ucache_steps) {  // kept for the leaf reduction (uniform branch)
+          ucache[(size_t)p * UCACHE_ROW + tj] = u1;
+          ucache[(size_t)(a.ucache_steps + p) * UCACHE_ROW + tj] = u2;
+        }
+      } else {
+        const size_t o = (size_t)(valid ? kl : 0) * H + p;
+        u1 = a.inj_u1[o];
+        u2 = a.inj_u2[o];
+        ust[(size_t)p * TB] = u1;  // MODE 1: the leaf records read the injected controls back
+        ust[(size_t)(H + p) * TB] = u2;
+      }
+      L = L * a.fa + (u1 * a.fk) * (1.0f - a.fa);
+      R = R * a.fa + (u2 * a.fk) * (1.0f - a.fa);
+      const float vp = clampf((L + R) / 2.0f, a.vmin, a.vmax);
+      const float wp = clampf(((-L) + R) / a.rwheel, a.wmin, a.wmax);
+      float sn, cs;
+      dm_sincosf(wp * a.dt, &sn, &cs);
+      wait_ge(f_cost, p - D + 1, seen_cost);
+      float* ri = ring_in + (p % D) * RI * TB + tj;
+      ri[0] = vp;
+      ri[TB] = sn;
+      ri[2 * TB] = cs;
+      ri[3 * TB] = 1.0f - cs;
+      if constexpr (DUMP) {
+        if (valid) {
+          const size_t o1 = (size_t)kl * H + p;
+          if (a.d_u1) a.d_u1[o1] = u1;
+          if (a.d_u2) a.d_u2[o1] = u2;
+          if (a.d_w) a.d_w[o1] = wp;
+        }
+      }
+      lds_store_release(f_prod, p + 1);
+      if constexpr (MODE == 0) {  // the normals of step p + 2 into the registers just freed
+        const int tn = min(p + 2, H - 1);
+        e1r = eps_row[(size_t)tn * TB];
+        e2r = eps_row[(size_t)(H + tn) * TB];
+      }
+    };
+    int p = 0;
+    for (; p + 1 < H; p += 2) {
+      prod(p, eA1, eA2);
+      prod(p + 1, eB1, eB2);
+    }
+    if (p < H) prod(p, eA1, eA2);
+  } else if (role == ROLE_WHEEL) {
+    // ---------------- wheel contacts of the even steps (the slope critic reads lw / rw at i,
+    // i + 2 for even i, critics_warp.py:220-267) and the slope critic.  Contact sets A / B
+    // alternate (steps 0, 4, 8, ... / 2, 6, 10, ...); the term of (i, i + 2) = (sc - 4, sc - 2)
+    // is added at even step sc, before sc's contacts replace those of sc - 4, so every height
+    // gathered has two chain steps to arrive and no register holding a load in flight is copied.
+    int seen_chain = 0;
+    float sw = 0.f;
+    float Alx = 0.f, Aly = 0.f, Alz = 0.f, Arx = 0.f, Ary = 0.f, Arz = 0.f;
+    float Blx = 0.f, Bly = 0.f, Blz = 0.f, Brx = 0.f, Bry = 0.f, Brz = 0.f;
+    auto contacts = [&](int sc, float& lx, float& ly, float& lz, float& rx, float& ry, float& rz)
+        __attribute__((always_inline)) {
+      wait_ge(f_chain, sc + 1, seen_chain);
+      const float* ro = ring_out + (sc % D) * 4 * TB + tj;
+      const float x = ro[0], y = ro[TB], cx = ro[2 * TB], cy = ro[3 * TB];
+      lx = ly = lz = rx = ry = rz = 0.f;
+      if constexpr (PROJ == 3) {
+        lx = x + cx;
+        ly = y + cy;
+        lz = dem.template point<false>(lx, ly, nobad);
+        rx = x - cx;
+        ry = y - cy;
+        rz = dem.template point<false>(rx, ry, nobad);
+      }
+      if constexpr (DUMP) {
+        if (valid) {
+          const size_t o3 = ((size_t)kl * H + sc) * 3;
+          if (a.d_lw) { a.d_lw[o3] = lx; a.d_lw[o3 + 1] = ly; a.d_lw[o3 + 2] = lz; }
+          if (a.d_rw) { a.d_rw[o3] = rx; a.d_rw[o3 + 1] = ry; a.d_rw[o3 + 2] = rz; }
+        }
+      }
+    };
+    // even step sc in set X (other set Y): the term of (sc - 4, sc - 2) = (X, Y), then X = sc
+    auto wstep = [&](auto x_is_a, int sc) __attribute__((always_inline)) {
+      constexpr bool XA = decltype(x_is_a)::value;
+      float& Xlx = XA ? Alx : Blx; float& Xly = XA ? Aly : Bly; float& Xlz = XA ? Alz : Blz;
+      float& Xrx = XA ? Arx : Brx; float& Xry = XA ? Ary : Bry; float& Xrz = XA ? Arz : Brz;
+      const float& Ylx = XA ? Blx : Alx; const float& Yly = XA ? Bly : Aly; const float& Ylz = XA ? Blz : Alz;
+      const float& Yrx = XA ? Brx : Arx; const float& Yry = XA ? Bry : Ary; const float& Yrz = XA ? Brz : Arz;
+      const int i = sc - 4;
+      if (i >= 0 && i < H - 3) {
+        const float term = slope_term<false>(Xlx, Xly, Xlz, Ylx, Yly, Ylz, Xrx, Xry, Xrz, Yrx, Yry, Yrz, nobad);
+        sw = sw + term;
+      }
+      contacts(sc, Xlx, Xly, Xlz, Xrx, Xry, Xrz);
+      if constexpr (DUMP) {  // odd-step contacts are written for the dump only
+        if (sc + 1 < H) {
+          float lx, ly, lz, rx, ry, rz;
+          contacts(sc + 1, lx, ly, lz, rx, ry, rz);
+        }
+        lds_store_release(f_wheel, min(sc + 2, H));
+      } else {
+        // the odd step's slot is not read here: release it with the even one
+        lds_store_release(f_wheel, min(sc + 2, H));
+      }
+    };
+    int sc = 0;
+    for (; sc + 2 < H; sc += 4) {
+      wstep(T_{}, sc);
+      wstep(F_{}, sc + 2);
+    }
+    if (sc < H) {
+      wstep(T_{}, sc);
+      sc += 2;
+    }
+    // sc - 2 = the last even step processed; its set is A if (sc - 2) % 4 == 0
+    const int last = sc - 2;
+    const int i = last - 2;  // the term (last - 2, last)
+    if (i >= 0 && i < H - 3) {
+      const float term = (last % 4 == 0)
+          ? slope_term<false>(Blx, Bly, Blz, Alx, Aly, Alz, Brx, Bry, Brz, Arx, Ary, Arz, nobad)
+          : slope_term<false>(Alx, Aly, Alz, Blx, Bly, Blz, Arx, Ary, Arz, Brx, Bry, Brz, nobad);
+      sw = sw + term;
+    }
+    sw_lds[tj] = sw;
+  } else {
+    // ---------------- costmap gather (used one step later), path-follow, speed, obstacle
+    int seen_chain = 0;
+    float pf_sum = 0.f, sp = 0.f, ob = 0.f, last_x = a.x0, last_y = a.y0;
+    float cmA = 0.f, cmB = 0.f;  // costmap value of the even / odd step
+    Recip rcm;
+    rcm.b = a.res_c;
+    auto cstep = [&](int sc, float& cm_mine, float& cm_prev) __attribute__((always_inline)) {
+      wait_ge(f_chain, sc + 1, seen_chain);
+      const float* ro = ring_out + (sc % D) * 4 * TB + tj;
+      const float x = ro[0], y = ro[TB];
+      const float vq = ring_in[(sc % D) * RI * TB + tj];  // v of step sc (slot not reused yet)
+      cm_mine = a.cm[costmap_index<false>(a.cm_size, a.hw, rcm, x, y, nobad, a.rinv_res_c, a.cdiv_res_c)];
+      const float pft = pf_sum + 10.0f * (fabsf(x - a.gx) + fabsf(y - a.gy));
+      pf_sum = (sc < H - 1) ? pft : pf_sum;  // _path_follow_critic sum over t < H-1
+      last_x = x;
+      last_y = y;
+      const float spt = sp + (a.vmax - vq) / (vq + 0.0001f);  // _maximise_speed
+      sp = a.speed_on ? spt : sp;
+      // _avoid_obstacle: the costmap value gathered one step earlier (step sc - 1)
+      const float ob1 = (cm_prev > a.thr) ? ob + a.pen : ob;
+      ob = (sc > 0) ? ob1 + cm_prev : ob;
+      if constexpr (DUMP) {
+        if (valid && a.d_v) a.d_v[(size_t)kl * H + sc] = vq;
+      }
+      lds_store_release(f_cost, sc + 1);
+    };
+    int sc = 0;
+    for (; sc + 1 < H; sc += 2) {
+      cstep(sc, cmA, cmB);
+      cstep(sc + 1, cmB, cmA);
+    }
+    if (sc < H) cstep(sc, cmA, cmB);
+    const float cm_last = ((H - 1) & 1) ? cmB : cmA;
+    if (cm_last > a.thr) ob = ob + a.pen;  // last step's obstacle term
+    ob = ob + cm_last;
+    float pf;  // _evaluate_trajectories_kernel (critics_warp.py:325-329)
+    if (a.pf_far) {
+      const float dx = last_x - a.igx, dy = last_y - a.igy;
+      pf = (dx * dx + dy * dy) * a.pf_scale;
+    } else {
+      pf = pf_sum;
+    }
+    c_pf = pf;
+    c_sp = sp;
+    c_ob = ob;
+  }
+#ifdef MPPI_STAMPS
+  // per wave of the first 64 workgroups: [work cycles, wait cycles, waits that read LDS]
+  if ((tid & 63) == 0 && blockIdx.x < 64) {
+    uint64_t* g = g_dbg_stamps + (blockIdx.x * 16 + wave) * 2;
+    g[0] = (dbg_stamp() - k_t0) - st_wait;
+    g[1] = st_wait;
+    g_dbg_stamps[64 * 16 * 2 + blockIdx.x * 16 + wave] = st_n;
+  }
+#endif
+  __syncthreads();  // WHEEL's slope sums are in sw_lds
+  if (role == ROLE_COST) {  // critics_warp.py:325-329, this f32 add order
+    float cost = a.w_path * c_pf;
+    cost = cost + a.w_slope * sw_lds[tj];
+    cost = cost + a.w_speed * c_sp;
+    cost = cost + a.w_obs * c_ob;
+    if (valid) a.cost_out[kl] = cost;
+    cost_lds[tj] = valid ? cost : INFINITY;
+  }
+  __syncthreads();
+  if constexpr (MODE == 0)  // rows hold the normals; the leaf recomputes the sampled controls
+    leaf_records<TB, NT, true>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB, ucache,
+                               a.ucache_steps);
+  else
+    leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
 }
 
 // =====================================================================  finish kernel
@@ -2103,8 +2705,30 @@ static hipError_t launch_pair_m(const RolloutArgs& a, int blocks, size_t lds, hi
   return hipGetLastError();
 }
 
+template <int TB, int PROJ>
+static hipError_t launch_roles_m(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int mode,
+                                 bool dump) {
+  const dim3 g(blocks), b(NROLES * TB);
+  if (mode == 0) {
+    if (dump)
+      hipLaunchKernelGGL((mppi_rollout_roles_kernel<TB, PROJ, 0, true>), g, b, lds, st, a);
+    else
+      hipLaunchKernelGGL((mppi_rollout_roles_kernel<TB, PROJ, 0, false>), g, b, lds, st, a);
+  } else {
+    if (dump)
+      hipLaunchKernelGGL((mppi_rollout_roles_kernel<TB, PROJ, 1, true>), g, b, lds, st, a);
+    else
+      hipLaunchKernelGGL((mppi_rollout_roles_kernel<TB, PROJ, 1, false>), g, b, lds, st, a);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
-                               int mode, bool dump) {
+                               int mode, bool dump, bool roles) {
+  if (roles) {
+    if (proj == 3) return launch_roles_m<256, 3>(a, blocks, lds, st, mode, dump);
+    return launch_roles_m<256, 2>(a, blocks, lds, st, mode, dump);
+  }
   if (proj == 3) return launch_pair_m<256, 3>(a, blocks, lds, st, mode, dump);
   return launch_pair_m<256, 2>(a, blocks, lds, st, mode, dump);
 }
@@ -2203,15 +2827,14 @@ __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t
   }
 }
 
-constexpr int64_t kNoiseMaxGroups = 4 * 256;
 hipError_t launch_noise(uint64_t seed, uint64_t n_base, int64_t k_offset, int blocks, int H, float* eps,
-                        hipStream_t st) {
-  // Grid capped at 4 workgroups (16 waves) per CU: the noise of step i+1 is generated
-  // while the finish of step i runs, and a full-size grid fills every wave slot ahead of
-  // the finish's one 16-wave workgroup, which then waits for the whole noise kernel.
+                        hipStream_t st, int max_groups) {
+  // Grid capped (max_groups, a few workgroups per CU): the noise of step i+2 is generated
+  // while the finish of step i runs and the next rollout starts; a full-size grid fills every
+  // wave slot ahead of their 16-wave workgroups, which then wait for the whole noise kernel.
   const int NB = (H + 1) >> 1;
   const int64_t total = (int64_t)blocks * NB;
-  const unsigned grid = (unsigned)std::min<int64_t>(total, kNoiseMaxGroups);
+  const unsigned grid = (unsigned)std::min<int64_t>(total, std::max(max_groups, 1));
   hipLaunchKernelGGL(mppi_noise_kernel, dim3(grid), dim3(256), 0, st, seed, n_base, k_offset, H, blocks, eps);
   return hipGetLastError();
 }

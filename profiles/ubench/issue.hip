@@ -17,6 +17,7 @@ __global__ void issue_kernel(float* out, int iters, unsigned long long* cyc) {
         a6 = a0 + 6, a7 = a0 + 7;
   f2 p0 = {a0, a1}, p1 = {a2, a3}, p2 = {a4, a5}, p3 = {a6, a7};
   const float c = 0.99991f;
+  unsigned si = blockIdx.x;
   if (threadIdx.x == 0) lds[0] = 0.f;
   __syncthreads();
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -54,6 +55,25 @@ __global__ void issue_kernel(float* out, int iters, unsigned long long* cyc) {
           " v_pk_fma_f32 %0, %0, %1, %1\n v_pk_fma_f32 %0, %0, %1, %1"
           : "+v"(p0)
           : "v"(f2{c, c}));)
+    } else if constexpr (OP == 6) {  // 4 independent v_fma_f32 interleaved with 4 s_add_u32, x8
+      REP8(asm volatile(
+          "v_fma_f32 %0, %0, %5, 0.5\n s_add_u32 %4, %4, 3\n v_fma_f32 %1, %1, %5, 0.5\n s_add_u32 %4, %4, 5\n"
+          " v_fma_f32 %2, %2, %5, 0.5\n s_add_u32 %4, %4, 7\n v_fma_f32 %3, %3, %5, 0.5\n s_add_u32 %4, %4, 9"
+          : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+s"(si)
+          : "v"(c) : "scc");)
+    } else if constexpr (OP == 7) {  // 8 v_mov_b32 from SGPR, x8
+      REP8(asm volatile(
+          "v_mov_b32 %0, %8\n v_mov_b32 %1, %8\n v_mov_b32 %2, %8\n v_mov_b32 %3, %8\n"
+          " v_mov_b32 %4, %8\n v_mov_b32 %5, %8\n v_mov_b32 %6, %8\n v_mov_b32 %7, %8"
+          : "=v"(a0), "=v"(a1), "=v"(a2), "=v"(a3), "=v"(a4), "=v"(a5), "=v"(a6), "=v"(a7)
+          : "s"(si));)
+    } else if constexpr (OP == 8) {  // 7 independent v_fma_f32 + 1 v_sqrt_f32, x8
+      REP8(asm volatile(
+          "v_fma_f32 %0, %0, %8, 0.5\n v_fma_f32 %1, %1, %8, 0.5\n v_fma_f32 %2, %2, %8, 0.5\n"
+          " v_sqrt_f32 %3, %3\n v_fma_f32 %4, %4, %8, 0.5\n v_fma_f32 %5, %5, %8, 0.5\n"
+          " v_fma_f32 %6, %6, %8, 0.5\n v_fma_f32 %7, %7, %8, 0.5"
+          : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+          : "v"(c));)
     } else {  // dependent v_sqrt_f32 chain
       REP8(asm volatile(
           "v_sqrt_f32 %0, %0\n v_sqrt_f32 %0, %0\n v_sqrt_f32 %0, %0\n v_sqrt_f32 %0, %0\n"
@@ -63,7 +83,7 @@ __global__ void issue_kernel(float* out, int iters, unsigned long long* cyc) {
   }
   unsigned long long t1 = __builtin_amdgcn_s_memtime();
   const float s = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + p0.x + p0.y + p1.x + p1.y + p2.x + p2.y + p3.x + p3.y;
-  out[blockIdx.x * blockDim.x + threadIdx.x] = s + lds[0];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s + lds[0] + (float)si;
   if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
 }
 
@@ -91,13 +111,16 @@ static void run(const char* name, int threads) {
 }
 
 int main() {
-  for (int t : {256, 512, 1024}) {
+  for (int t : {256, 512, 768, 1024}) {
     run<0>("fma x8", t);
     run<1>("fma dep", t);
     run<2>("pk_fma x4", t);
     run<4>("pk_fma dep", t);
     run<3>("sqrt x8", t);
     run<5>("sqrt dep", t);
+    run<6>("fma+salu", t);
+    run<7>("vmov x8", t);
+    run<8>("fma7+sqrt", t);
   }
   return 0;
 }
