@@ -462,19 +462,27 @@ __device__ __forceinline__ void chain3d_lean(const Dem<false>& dem, float res_ha
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 bc2(float s) { return f2{s, s}; }
+// [x > 0] for an int x in one v_med3_i32 (written out: the compiler rewrites min(max(x, 0), 1)
+// into a compare + select pair, which also costs VCC wait states)
+__device__ __forceinline__ int pos01(int x) {
+  int r;
+  asm("v_med3_i32 %0, %1, 0, 1" : "=v"(r) : "v"(x));
+  return r;
+}
 
-// sqrt_cr with the two neighbour residuals in one packed fma:
-// sqrt_cr = sdn + [rdn > 0] + [rup > 0] (rdn <= 0 < rup is impossible: sdn < sup).
-// The tests stay float compares: with the residual lanes bit-cast to integers, this
-// compiler (ROCm 7.2 LLVM) folded lane 1's test onto lane 0's (sdn + 2 [rdn > 0]).
+// sqrt_cr without compares: sqrt_cr = sdn + [rdn > 0] + [rup > 0] (rdn <= 0 < rup is
+// impossible: sdn < sup), and a residual n - x*s is exactly zero only as +0, so [r > 0] is
+// med3(bits(r), 0, 1) on its bit pattern as an integer (pos01: one instruction, no VCC, no
+// wait states).  The residuals stay two scalar fmas: with the lanes of a packed fma bit-cast to
+// integers this compiler (ROCm 7.2 LLVM) folded lane 1's test onto lane 0's.
 __device__ __forceinline__ float sqrt_cr2(float n) {
   const float s = __builtin_amdgcn_sqrtf(n);
   const int si = __builtin_bit_cast(int, s);
-  const f2 nb = {__builtin_bit_cast(float, si - 1), __builtin_bit_cast(float, si + 1)};
-  const f2 r = pk_fma(-nb, bc2(s), bc2(n));
-  const int inc_dn = r.x > 0.0f ? 1 : 0;
-  const int inc_up = r.y > 0.0f ? 1 : 0;
-  return __builtin_bit_cast(float, (si - 1) + inc_dn + inc_up);
+  const float sdn = __builtin_bit_cast(float, si - 1), sup = __builtin_bit_cast(float, si + 1);
+  const float rdn = __builtin_fmaf(-sdn, s, n);
+  const float rup = __builtin_fmaf(-sup, s, n);
+  return __builtin_bit_cast(float, (si - 1) + pos01(__builtin_bit_cast(int, rdn)) +
+                                       pos01(__builtin_bit_cast(int, rup)));
 }
 __device__ __forceinline__ Recip lean_norm2(float n, Lean& l) {
   const int nb = __builtin_bit_cast(int, n);
@@ -486,16 +494,27 @@ __device__ __forceinline__ Recip lean_norm2(float n, Lean& l) {
   r.y = __builtin_fmaf(__builtin_fmaf(-r.b, y0, 1.0f), y0, y0);
   return r;
 }
-// (a.x, a.y) / r.b, each lane lean_div
+// a / r.b without the sign fix-up: the residuals are formed negated, E = b q - a (= -(a - b q)
+// exactly, round-to-nearest is symmetric), and subtracted, q' = q - E y.  For a != 0 that is
+// lean_div's sequence; for a = +-0 every intermediate is a zero and q0 = a y, q' = (-E) y + q
+// keep the sign of a (lean_div needed a copysign there).
+__device__ __forceinline__ float lean_div_s(float a, const Recip& r, Lean& l) {
+  l.emin = min(l.emin, __builtin_amdgcn_frexp_expf(a));
+  const float q0 = a * r.y;
+  const float e0 = __builtin_fmaf(r.b, q0, -a);
+  const float q1 = __builtin_fmaf(-e0, r.y, q0);
+  const float e1 = __builtin_fmaf(r.b, q1, -a);
+  return __builtin_fmaf(-e1, r.y, q1);
+}
+// (a.x, a.y) / r.b, each lane lean_div_s
 __device__ __forceinline__ f2 lean_div2(f2 a, const Recip& r, Lean& l) {
   l.emin = min(l.emin, min(__builtin_amdgcn_frexp_expf(a.x), __builtin_amdgcn_frexp_expf(a.y)));
   const f2 b = bc2(r.b), y = bc2(r.y);
   const f2 q0 = a * y;
-  const f2 e0 = pk_fma(-b, q0, a);
-  const f2 q1 = pk_fma(e0, y, q0);
-  const f2 e1 = pk_fma(-b, q1, a);
-  const f2 q2 = pk_fma(e1, y, q1);
-  return f2{__builtin_copysignf(q2.x, a.x), __builtin_copysignf(q2.y, a.y)};
+  const f2 e0 = pk_fma(b, q0, -a);
+  const f2 q1 = pk_fma(-e0, y, q0);
+  const f2 e1 = pk_fma(b, q1, -a);
+  return pk_fma(-e1, y, q1);
 }
 // cross(n, o).xy = (ny oz - nz oy, nz ox - nx oz), as (ny oz, -nx oz) + (-nz oy, nz ox)
 __device__ __forceinline__ f2 cross_xy(f2 nxy, float nz, f2 oxy, float oz) {
@@ -524,11 +543,11 @@ __device__ __forceinline__ Head orient_step(f2 nxy, float nz, const Head& h, flo
     const f2 p2 = pxy * pxy;
     const Recip r = lean_norm2((p2.x + p2.y) + pz * pz, l);
     txy = lean_div2(pxy, r, l);
-    tz = lean_div(pz, r, l);
+    tz = lean_div_s(pz, r, l);
     const f2 t2 = txy * txy;
     const Recip ro = lean_norm2((t2.x + t2.y) + tz * tz, l);
     oxy = lean_div2(txy, ro, l);
-    oz = lean_div(tz, ro, l);
+    oz = lean_div_s(tz, ro, l);
   } else {
     const float pn = sqrtf((pxy.x * pxy.x + pxy.y * pxy.y) + pz * pz);
     txy = f2{pxy.x / pn, pxy.y / pn};
@@ -549,7 +568,7 @@ __device__ __forceinline__ Head orient_step(f2 nxy, float nz, const Head& h, flo
     const f2 r2 = rxy * rxy;
     const Recip r = lean_norm2((r2.x + r2.y) + rz * rz, l);
     o.xy = lean_div2(rxy, r, l);
-    o.z = lean_div(rz, r, l);
+    o.z = lean_div_s(rz, r, l);
   } else {
     const float rn = sqrtf((rxy.x * rxy.x + rxy.y * rxy.y) + rz * rz);
     o.xy = f2{rxy.x / rn, rxy.y / rn};
@@ -1430,8 +1449,8 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const R
         const int tjj = (int)__builtin_amdgcn_fmed3f(f.y, fj_lo, 1.0f);  // -min(j, rows - 1)
         nv = ntab0[ti - tjj * nrow];
       };
-      auto read_in = [&](int t, float& v, float& sn, float& cs, float& om) __attribute__((always_inline)) {
-        wait_ge(f_prod, t + 1, seen_prod);
+      auto read_in = [&](int t, float& v, float& sn, float& cs, float& om, int need) __attribute__((always_inline)) {
+        if (need) wait_ge(f_prod, need, seen_prod);
         const float* ri = ring_in + (t % D) * RI * TB + tj;
         v = ri[0];
         sn = ri[TB];
@@ -1440,7 +1459,7 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const R
       };
       {  // step 0's position and normal
         float v0;
-        read_in(0, v0, snA, csA, omA);
+        read_in(0, v0, snA, csA, omA, 1);
         Lean l;
         lean_init(l);
         f2 p = advance_step<true>(hd, v0, a.dt, posA, l);
@@ -1448,12 +1467,15 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const R
         posA = p;
         gather(posA, nvA);
       }
-      // step t in set X (pos, normal in flight, sin / cos / 1 - cos); step t + 1 into set Y
-      auto it = [&](int t, f2& pX, float4& nX, float& snX, float& csX, float& omX, f2& pY, float4& nY,
-                    float& snY, float& csY, float& omY) __attribute__((always_inline)) {
+      // step t in set X (pos, normal in flight, sin / cos / 1 - cos); step t + 1 into set Y.
+      // Even steps wait for two steps' worth of progress (the producer's steps t + 1, t + 2 and
+      // the consumers' ring slots of t, t + 1), odd steps are covered by them.
+      auto it = [&](auto even_tag, int t, f2& pX, float4& nX, float& snX, float& csX, float& omX, f2& pY,
+                    float4& nY, float& snY, float& csY, float& omY) __attribute__((always_inline)) {
+        constexpr bool EVEN = decltype(even_tag)::value;
         const bool more = t + 1 < H;  // uniform
         float v1 = 0.f;
-        if (more) read_in(t + 1, v1, snY, csY, omY);
+        if (more) read_in(t + 1, v1, snY, csY, omY, EVEN ? min(t + 3, H) : 0);
         const f2 nxy = f2{nX.x, nX.y};
         const float nz = nX.z;
         Lean l;
@@ -1471,8 +1493,10 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const R
         }
         // wheel offset right = 0.2 * cross(normal, current_hv) (projection_warp.py:333)
         const f2 cxy = bc2(a.off) * cross_xy(nxy, nz, ho.xy, ho.z);
-        wait_ge(f_wheel, t - D + 1, seen_wheel);
-        wait_ge(f_cost, t - D + 1, seen_cost);
+        if constexpr (EVEN) {
+          wait_ge(f_wheel, t - D + 2, seen_wheel);
+          wait_ge(f_cost, t - D + 2, seen_cost);
+        }
         float* ro = ring_out + (t % D) * 4 * TB + tj;
         ro[0] = pX.x;
         ro[TB] = pX.y;
@@ -1493,10 +1517,10 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const R
       };
       int t = 0;
       for (; t + 1 < H; t += 2) {
-        it(t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
-        it(t + 1, posB, nvB, snB, csB, omB, posA, nvA, snA, csA, omA);
+        it(T_{}, t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
+        it(F_{}, t + 1, posB, nvB, snB, csB, omB, posA, nvA, snA, csA, omA);
       }
-      if (t < H) it(t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
+      if (t < H) it(T_{}, t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
     } else
     for (int sc = 0; sc < H; ++sc) {
       wait_ge(f_prod, sc + 1, seen_prod);
