@@ -334,6 +334,7 @@ __device__ __forceinline__ void chain3d(const Dem<LDS>& dem, float res_half_neg,
 struct Lean {
   int emin;      // min frexp exponent of the numerators
   int nlo, nhi;  // min / max bit pattern of the squared norms
+  int n1lo = 0x3F800000, n1hi = 0x3F800000;  // ... of the squared norms of unit vectors (sqrt_near1)
 };
 constexpr int kLeanEmin = -79;          // |a| >= 2^-80 <=> frexp exponent >= -79
 constexpr int kLeanNlo = 0x17800000;    // 2^-80
@@ -343,8 +344,10 @@ __device__ __forceinline__ void lean_init(Lean& l) {
   l.nlo = kLeanNhi;
   l.nhi = kLeanNlo;
 }
+constexpr int kNear1 = 4095;  // sqrt_near1: squared norms within 4095 ulps of 1
 __device__ __forceinline__ bool lean_bad(const Lean& l) {
-  return (l.emin < kLeanEmin) | (l.nlo < kLeanNlo) | (l.nhi > kLeanNhi);
+  return (l.emin < kLeanEmin) | (l.nlo < kLeanNlo) | (l.nhi > kLeanNhi) | (l.n1lo < 0x3F800000 - kNear1) |
+         (l.n1hi > 0x3F800000 + kNear1);
 }
 // correctly rounded sqrt of a normal positive n (neighbour residual test)
 __device__ __forceinline__ float sqrt_cr(float n) {
@@ -484,6 +487,23 @@ __device__ __forceinline__ float sqrt_cr2(float n) {
   return __builtin_bit_cast(float, (si - 1) + pos01(__builtin_bit_cast(int, rdn)) +
                                        pos01(__builtin_bit_cast(int, rup)));
 }
+// Correctly rounded sqrt of the squared norm of a vector that is already unit up to rounding
+// (the reference normalises the tangent and the rotated heading twice).  With n = 1 + k 2^-23
+// (k >= 0) sqrt(n) = 1 + k 2^-24 - k^2 2^-49 + ..., with n = 1 - k 2^-24 it is 1 - k 2^-25 -
+// k^2 2^-51 - ...: for |k| < 5792 the quadratic term never crosses a rounding boundary (even k:
+// it stays within half an ulp of the grid point, odd k: it moves the midpoint down), so
+// RN(sqrt(n)) = 1 + floor(k / 2) ulp above 1, 1 - ceil(k / 2) ulp below: in bits,
+// C + ((bits(n) - C) >> 1) = (bits(n) + C) >> 1 with C = bits(1.0f).  Guarded to |k| <= 4095.
+__device__ __forceinline__ Recip lean_norm_near1(float n, Lean& l) {
+  const int nb = __builtin_bit_cast(int, n);
+  l.n1lo = min(l.n1lo, nb);
+  l.n1hi = max(l.n1hi, nb);
+  Recip r;
+  r.b = __builtin_bit_cast(float, (int)((unsigned)(nb + 0x3F800000) >> 1));
+  const float y0 = __builtin_amdgcn_rcpf(r.b);
+  r.y = __builtin_fmaf(__builtin_fmaf(-r.b, y0, 1.0f), y0, y0);
+  return r;
+}
 __device__ __forceinline__ Recip lean_norm2(float n, Lean& l) {
   const int nb = __builtin_bit_cast(int, n);
   l.nlo = min(l.nlo, nb);
@@ -545,7 +565,7 @@ __device__ __forceinline__ Head orient_step(f2 nxy, float nz, const Head& h, flo
     txy = lean_div2(pxy, r, l);
     tz = lean_div_s(pz, r, l);
     const f2 t2 = txy * txy;
-    const Recip ro = lean_norm2((t2.x + t2.y) + tz * tz, l);
+    const Recip ro = lean_norm_near1((t2.x + t2.y) + tz * tz, l);
     oxy = lean_div2(txy, ro, l);
     oz = lean_div_s(tz, ro, l);
   } else {
@@ -566,7 +586,7 @@ __device__ __forceinline__ Head orient_step(f2 nxy, float nz, const Head& h, flo
   Head o;
   if constexpr (F) {
     const f2 r2 = rxy * rxy;
-    const Recip r = lean_norm2((r2.x + r2.y) + rz * rz, l);
+    const Recip r = lean_norm_near1((r2.x + r2.y) + rz * rz, l);
     o.xy = lean_div2(rxy, r, l);
     o.z = lean_div_s(rz, r, l);
   } else {
@@ -582,7 +602,7 @@ __device__ __forceinline__ f2 advance_step(const Head& h, float v, float dt, f2 
   f2 u;
   if constexpr (F) {
     const f2 h2 = h.xy * h.xy;
-    const Recip r = lean_norm2((h2.x + h2.y) + h.z * h.z, l);
+    const Recip r = lean_norm_near1((h2.x + h2.y) + h.z * h.z, l);
     u = lean_div2(h.xy, r, l);
   } else {
     const float hn = sqrtf((h.xy.x * h.xy.x + h.xy.y * h.xy.y) + h.z * h.z);
