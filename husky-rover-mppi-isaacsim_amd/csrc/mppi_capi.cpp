@@ -1174,7 +1174,7 @@ int mppi_set_dem_device(mppi_ctx* c, const float* z, int32_t rows, int32_t cols,
   int rc = check_grid(rows, cols, resolution);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipDeviceSynchronize());  // the DEM's writer may be on any stream of the device
   rc = sync_tail(c);
   if (rc) return rc;
   if (c->Z_owned && c->Z) HIP_TRY(hipFree(c->Z));
@@ -1189,6 +1189,16 @@ int mppi_set_dem_device(mppi_ctx* c, const float* z, int32_t rows, int32_t cols,
   rc = build_normal_table(c);
   if (rc) return rc;
   return verified_reciprocal(c, resolution, &c->rinv_res);
+}
+
+int mppi_dem_updated(mppi_ctx* c) {
+  if (!c) return fail(MPPI_EINVAL, "null argument");
+  if (!c->Z || c->rows <= 0) return fail(MPPI_EINVAL, "no DEM bound");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());  // the in-place write may be on any stream of the device
+  const int rc = sync_tail(c);      // a deferred optimal rollout may still read the table
+  if (rc) return rc;
+  return build_normal_table(c);
 }
 
 int mppi_set_costmap(mppi_ctx* c, const float* cm, int32_t size, float half_width, float resolution) {

@@ -1467,7 +1467,13 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const R
         }
         const int ti = (int)__builtin_amdgcn_fmed3f(f.x, -1.0f, fi_hi);  // min(i, grid - 1)
         const int tjj = (int)__builtin_amdgcn_fmed3f(f.y, fj_lo, 1.0f);  // -min(j, rows - 1)
+#if defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 1  // diagnostic builds only: one cell (L1 hits)
+        nv = ntab0[(ti - tjj * nrow) & 0];
+#elif defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 2  // diagnostic: no load
+        nv = make_float4(__builtin_bit_cast(float, ti) * 1e-30f, __builtin_bit_cast(float, tjj) * 1e-30f, 1.0f, 0.f);
+#else
         nv = ntab0[ti - tjj * nrow];
+#endif
       };
       auto read_in = [&](int t, float& v, float& sn, float& cs, float& om, int need) __attribute__((always_inline)) {
         if (need) wait_ge(f_prod, need, seen_prod);

@@ -70,6 +70,7 @@ _PROTOS = {
     "mppi_destroy": (None, [C.c_void_p]),
     "mppi_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mppi_set_dem": (C.c_int, [C.c_void_p, _FP, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float]),
+    "mppi_dem_updated": (C.c_int, [C.c_void_p]),
     "mppi_set_dem_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_float,
                                       C.c_float, C.c_float]),
     "mppi_set_costmap": (C.c_int, [C.c_void_p, _FP, C.c_int32, C.c_float, C.c_float]),
@@ -292,6 +293,10 @@ class Engine:
         self._c(self.lib.mppi_set_dem_device(self.ctx, C.c_void_p(int(ptr)), rows, cols, -half_width,
                                              -half_width, resolution), "mppi_set_dem_device")
         self._keep = [keepalive]
+
+    def dem_updated(self):
+        """The bound device DEM was written in place: rebuild the per-cell normal table."""
+        self._c(self.lib.mppi_dem_updated(self.ctx), "mppi_dem_updated")
 
     def set_costmap(self, cm, half_width, resolution=None):
         cm = np.ascontiguousarray(cm, dtype=np.float32)

@@ -270,18 +270,22 @@ class MPPI_Controller:
 
     # ------------------------------------------------------------ device-array plumbing
     def _upload_dem(self, Z):
-        """Z_wp binding: ndarray, object with .numpy()/__array__, or a CUDA tensor (zero copy)."""
+        """Z_wp binding (visual_terrain_stack_full_terrain.py:567: ``controller_3d.Z_wp = DEM_warp``).
+
+        Device arrays are bound zero copy: anything exposing ``__cuda_array_interface__`` (a Warp
+        array such as the terrain manager's ``dem_wp``, geometry_clipmaps.py:300/332), a CUDA
+        ``torch.Tensor``, or a ``__dlpack__`` producer on the GPU.  They must be float32 and
+        C-contiguous (refused otherwise: a silent copy would stop following the caller's buffer),
+        1-D of n*n cells (the reference's flat dem_wp) or 2-D (rows, cols).  Host arrays (ndarray,
+        ``.numpy()``/``__array__`` objects) are uploaded.  After an in-place write of a bound
+        device DEM call :meth:`dem_updated` (or bind it again).
+        """
         hw = self.surface.half_width
-        try:
-            import torch
-            if isinstance(Z, torch.Tensor) and Z.is_cuda:
-                Zt = Z.contiguous().to(torch.float32)
-                n = int(round(np.sqrt(Zt.numel()))) if Zt.dim() == 1 else Zt.shape[1]
-                rows = Zt.numel() // n
-                self.engine.set_dem_device(Zt.data_ptr(), rows, n, hw, keepalive=Zt)
-                return
-        except ImportError:
-            pass
+        dev = _device_dem(Z)
+        if dev is not None:
+            ptr, rows, cols, keep = dev
+            self.engine.set_dem_device(ptr, rows, cols, hw, keepalive=keep)
+            return
         if hasattr(Z, "numpy") and not isinstance(Z, np.ndarray):
             Z = Z.numpy()
         Z = np.asarray(Z, np.float32)
@@ -289,6 +293,12 @@ class MPPI_Controller:
             n = int(round(np.sqrt(Z.size)))
             Z = Z.reshape(n, n)
         self.engine.set_dem(Z, hw)
+
+    def dem_updated(self):
+        """The bound device DEM was written in place (geometry_clipmaps.py:293 ``dem_wp.assign``):
+        rebuild the per-cell normal table the rollout reads (the reference's kernels read the live
+        heights at every step)."""
+        self.engine.dem_updated()
 
     def _upload_costmap(self, cm):
         cm = np.asarray(cm, np.float32)
@@ -417,3 +427,48 @@ class MPPI_Controller:
             self.robot.right_wheel_speed = lin_vel + ang_vel * self.robot.radius / 2
             self.loop += 1
         print("Number of loops:", self.loop)
+
+
+def _grid_shape(shape):
+    """(rows, cols) of a DEM buffer: 2-D as given, 1-D of n*n cells as n x n."""
+    if len(shape) == 2:
+        return int(shape[0]), int(shape[1])
+    if len(shape) == 1:
+        n = int(round(np.sqrt(shape[0])))
+        if n * n != shape[0]:
+            raise ValueError(f"1-D DEM of {shape[0]} cells is not square")
+        return n, n
+    raise ValueError(f"DEM must be 1-D (n*n) or 2-D, got shape {tuple(shape)}")
+
+
+def _device_dem(Z):
+    """(device pointer, rows, cols, keepalive) for a GPU-resident float32 C-contiguous DEM, None for a
+    host array; raises for a device array that would need a copy."""
+    cai = getattr(Z, "__cuda_array_interface__", None)
+    if cai is not None:
+        shape = tuple(cai["shape"])
+        if cai.get("typestr") not in ("<f4", "=f4", "f4"):
+            raise ValueError(f"device DEM must be float32, got typestr {cai.get('typestr')!r}")
+        strides = cai.get("strides")
+        if strides is not None and tuple(strides) != tuple(
+                4 * int(np.prod(shape[i + 1:])) for i in range(len(shape))):
+            raise ValueError(f"device DEM must be C-contiguous, got strides {strides}")
+        rows, cols = _grid_shape(shape)
+        return int(cai["data"][0]), rows, cols, Z
+    try:
+        import torch
+    except ImportError:
+        torch = None
+    if torch is not None and not isinstance(Z, torch.Tensor) and hasattr(Z, "__dlpack__"):
+        dev = Z.__dlpack_device__()[0] if hasattr(Z, "__dlpack_device__") else None
+        if dev in (2, 10):  # kDLCUDA, kDLROCM: a device producer, viewed as a tensor (no copy)
+            Z = torch.from_dlpack(Z)
+    if torch is not None and isinstance(Z, torch.Tensor) and Z.is_cuda:
+        if Z.dtype != torch.float32:
+            raise ValueError(f"device DEM must be float32, got {Z.dtype}")
+        if not Z.is_contiguous():
+            raise ValueError("device DEM must be contiguous (bind a contiguous buffer: a copy would not "
+                             "follow the caller's updates)")
+        rows, cols = _grid_shape(tuple(Z.shape))
+        return Z.data_ptr(), rows, cols, Z
+    return None

@@ -111,10 +111,19 @@ int mppi_set_dem(mppi_ctx* ctx, const float* z_host, int32_t rows, int32_t cols,
 
 /* controller.Z_wp = DEM_warp rebinding (visual_terrain_stack_full_terrain.py:567):
  * binds a DEM already resident in device memory (zero copy; the caller keeps
- * it alive and unchanged while steps run: the per-cell normal table the rollout
- * reads is derived from it here, so bind it again after changing it). */
+ * it alive while steps run).  Waits for every stream of the device (the DEM may
+ * have been written on any of them), then derives the per-cell normal table the
+ * rollout reads from it. */
 int mppi_set_dem_device(mppi_ctx* ctx, const float* z_device, int32_t rows, int32_t cols,
                         float x_min, float y_min, float resolution);
+
+/* The bound DEM was written in place (the terrain manager's dem_wp.assign(...),
+ * geometry_clipmaps.py:293): waits for every stream of the device and rebuilds
+ * the per-cell normal table from the current heights.  The reference's kernels
+ * read the live DEM at every step; here the table is derived, so an in-place
+ * write without this call (or a rebinding) leaves the normals of the old
+ * heights.  MPPI_EINVAL when no DEM is bound. */
+int mppi_dem_updated(mppi_ctx* ctx);
 
 /* self.costmap_wp (MPPI_isaac.py:461) / costmap_wp.assign(...)
  * (visual_terrain_stack_full_terrain.py:563): size x size row-major costmap;
