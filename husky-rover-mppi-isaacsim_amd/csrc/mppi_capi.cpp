@@ -870,8 +870,10 @@ void costmap_free(CostmapScratch& sc) {
   sc = CostmapScratch{};
 }
 
-int costmap_check(const double* obstacles, int32_t n, int32_t size, int32_t power) {
+int costmap_check(const double* obstacles, int32_t n, int32_t size, int32_t power, int32_t metric) {
   if (n < 0 || (n > 0 && !obstacles)) return fail(MPPI_EINVAL, "obstacles: null pointer or negative count");
+  if (metric != MPPI_COSTMAP_CHAMFER5 && metric != MPPI_COSTMAP_EXACT)
+    return fail(MPPI_EINVAL, "costmap metric must be MPPI_COSTMAP_CHAMFER5 or MPPI_COSTMAP_EXACT");
   if (size < 2 || size > COSTMAP_MAX_SIZE) return fail(MPPI_EINVAL, "costmap size must be in [2, 8192]");
   if (power < 0) return fail(MPPI_EINVAL, "costmap power must be >= 0");
   return MPPI_OK;
@@ -1478,9 +1480,10 @@ int mppi_selftest(mppi_ctx* c, int32_t what, int64_t n, uint64_t seed, int64_t* 
 }
 
 int mppi_build_costmap(mppi_ctx* c, const double* obstacles, int32_t n, int32_t size, double half_width,
-                       double origin_x, double origin_y, double r_robot, int32_t power, float* out_host) {
+                       double origin_x, double origin_y, double r_robot, int32_t power, float* out_host,
+                       int32_t metric) {
   if (!c) return fail(MPPI_EINVAL, "null context");
-  int rc = costmap_check(obstacles, n, size, power);
+  int rc = costmap_check(obstacles, n, size, power, metric);
   if (rc) return rc;
   const float res = (float)(2 * half_width / size);  // Surface.costmap_resolution (MPPI_isaac.py:272)
   if (!(res > 0.0f)) return fail(MPPI_EINVAL, "costmap resolution must be > 0");
@@ -1497,7 +1500,7 @@ int mppi_build_costmap(mppi_ctx* c, const double* obstacles, int32_t n, int32_t 
   std::vector<double> obs, xs;
   rc = costmap_stage(c->cms, obstacles, n, size, half_width, origin_x, origin_y, r_robot, obs, xs, c->stream);
   if (rc) return rc;
-  HIP_TRY(launch_costmap_build(c->cms, n, size, power, c->cm, c->stream));
+  HIP_TRY(launch_costmap_build(c->cms, n, size, power, c->cm, c->stream, metric));
   if (out_host) HIP_TRY(hipMemcpyAsync(out_host, c->cm, bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->cm_size = size;
@@ -1535,9 +1538,9 @@ void mppi_costmap_builder_destroy(mppi_costmap_builder* b) {
 
 int mppi_costmap_builder_build(mppi_costmap_builder* b, const double* obstacles, int32_t n, int32_t size,
                                double half_width, double origin_x, double origin_y, double r_robot, int32_t power,
-                               float* out_host, float* out_device) {
+                               float* out_host, float* out_device, int32_t metric) {
   if (!b) return fail(MPPI_EINVAL, "null builder");
-  int rc = costmap_check(obstacles, n, size, power);
+  int rc = costmap_check(obstacles, n, size, power, metric);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(b->device));
   const size_t bytes = (size_t)size * size * sizeof(float);
@@ -1557,7 +1560,7 @@ int mppi_costmap_builder_build(mppi_costmap_builder* b, const double* obstacles,
   rc = costmap_stage(b->sc, obstacles, n, size, half_width, origin_x, origin_y, r_robot, obs, xs, b->stream);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(b->ev[0], b->stream));
-  HIP_TRY(launch_costmap_build(b->sc, n, size, power, dst, b->stream));
+  HIP_TRY(launch_costmap_build(b->sc, n, size, power, dst, b->stream, metric));
   HIP_TRY(hipEventRecord(b->ev[1], b->stream));
   if (out_host) HIP_TRY(hipMemcpyAsync(out_host, dst, bytes, hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));

@@ -23,10 +23,15 @@ struct CostmapScratch {
 constexpr int COSTMAP_SEG = 32;         // rows per column segment of the column pass
 constexpr int COSTMAP_MAX_SIZE = 8192;  // (2*size+1)^2 must fit int32 (the no-obstacle marker)
 
-// Enqueue the whole build on `st`: raster -> exact EDT (column pass, row pass) -> min/max ->
-// min-max normalise -> (1 - d)^power, written to out[size*size] (device, float32, row-major).
-// sc.obs / sc.xs must already hold the n obstacle triples and the size grid coordinates.
+// distance metric of the build
+constexpr int COSTMAP_CHAMFER5 = 0;  // cv2.distanceTransform(DIST_L2, 5), the reference (default)
+constexpr int COSTMAP_EXACT = 1;     // exact Euclidean distance
+
+// Enqueue the whole build on `st`: raster -> distance (chamfer: two raster passes on one wave;
+// exact: column pass, row pass) -> min/max -> min-max normalise -> (1 - d)^power, written to
+// out[size*size] (device, float32, row-major).  sc.obs / sc.xs must already hold the n obstacle
+// triples and the size grid coordinates.
 hipError_t launch_costmap_build(const CostmapScratch& sc, int n_obs, int size, int power, float* out,
-                                hipStream_t st);
+                                hipStream_t st, int metric);
 
 }  // namespace mppi

@@ -224,15 +224,228 @@ __global__ __launch_bounds__(CM_THREADS) void costmap_scale_kernel(const int32_t
   }
 }
 
+// ---------------------------------------------------------------------  cv2 DIST_L2 mask-5 chamfer
+// cv2.distanceTransform(obs_costmap, DIST_L2, 5) (MPPI_isaac.py:374), restated from OpenCV's
+// published distanceTransform_5x5 (imgproc/src/distransform.cpp; oracle/costmap_ref.py
+// chamfer_l2_5x5): metrics {1, 1.4, 2.1969} in 16.16 fixed point, INIT_DIST0 = INT_MAX on a
+// 2-pixel border, a forward raster pass over the upper half-mask, a backward one over the lower
+// half, d = float(t) / 65536.  Rows depend on the two previous rows, so both passes walk the rows
+// in order on ONE wave (no workgroup barrier; LDS holds the last three rows); inside a row the
+// left-to-right chain t[j] = min(a[j], t[j-1] + 1.0) is a min-plus scan: each lane runs it over
+// its contiguous chunk, a 64-lane exclusive min-scan of (chunk end - column * 1.0) carries the
+// chain across chunks, exact in integers (the sequential sums never exceed 2^32 at size <= 8192).
+constexpr uint32_t CV_HV = 65536u, CV_DIAG = 91750u, CV_LONG = 143976u, CV_INIT = 0x7FFFFFFFu;
+constexpr int CH_B = 2;  // border columns each side
+
+// Exclusive min-scans over the 64 lanes of a wave with DPP row shifts / broadcasts (no LDS):
+// up = min over lanes < lane, down = min over lanes > lane (the lane order reversed around an
+// upward scan); UINT_MAX for none.
+__device__ inline uint32_t dpp_min(uint32_t x, uint32_t y) { return x < y ? x : y; }
+__device__ inline uint32_t wave_incl_min_scan(uint32_t x) {
+  x = dpp_min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x111, 0xF, 0xF, false));  // row_shr:1
+  x = dpp_min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x112, 0xF, 0xF, false));  // row_shr:2
+  x = dpp_min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x114, 0xF, 0xF, false));  // row_shr:4
+  x = dpp_min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x118, 0xF, 0xF, false));  // row_shr:8
+  x = dpp_min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  x = dpp_min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return x;
+}
+__device__ inline uint32_t wave_excl_min_scan_up(uint32_t v) {
+  const uint32_t x = wave_incl_min_scan(v);
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x138, 0xF, 0xF, false);  // wave_shr:1
+}
+__device__ inline uint32_t wave_excl_min_scan_down(uint32_t v, int lane) {
+  const uint32_t r = (uint32_t)__shfl((int)v, 63 - lane, 64);
+  const uint32_t x = wave_excl_min_scan_up(r);
+  return (uint32_t)__shfl((int)x, 63 - lane, 64);
+}
+
+// CM = columns per lane (a power of two >= ceil(W / 64)): a lane's chunk of a row stays in
+// registers from its chain to its final value.
+template <int CM>
+__global__ __launch_bounds__(64) void costmap_chamfer_kernel(const uint8_t* __restrict__ occ, int H, int W,
+                                                             uint32_t* __restrict__ tmp, float* __restrict__ dist,
+                                                             int32_t* __restrict__ range) {
+  extern __shared__ uint32_t srows[];  // [3][W + 4]
+  const int lane = threadIdx.x;
+  const int S = W + 2 * CH_B;
+  const int C = (W + 63) / 64;
+  const int j0 = min(W, lane * C), j1 = min(W, j0 + C);
+  for (int k = lane; k < 3 * S; k += 64) srows[k] = CV_INIT;
+  __syncthreads();
+  uint32_t loc[CM];
+  // global reads of a row are issued one row ahead (their latency would otherwise sit on every row)
+  uint8_t ocur[CM], onext[CM];
+#pragma unroll
+  for (int k = 0; k < CM; ++k) ocur[k] = j0 + k < j1 ? occ[j0 + k] : 0;
+  // ---- forward pass: rows top to bottom, columns left to right
+  for (int i = 0; i < H; ++i) {
+    const uint32_t* up2 = srows + ((i + 1) % 3) * S + CH_B;  // row i - 2 (INIT above the map)
+    const uint32_t* up1 = srows + ((i + 2) % 3) * S + CH_B;  // row i - 1
+    uint32_t* cur = srows + (i % 3) * S + CH_B;
+    const uint8_t* onrow = occ + (size_t)min(i + 1, H - 1) * W;
+#pragma unroll
+    for (int k = 0; k < CM; ++k) onext[k] = j0 + k < j1 ? onrow[j0 + k] : 0;
+    uint64_t run = 0xFFFFFFFFull;  // the chain inside the chunk, no left input yet
+#pragma unroll
+    for (int g = 0; g < CM; g += 8) {  // 8 columns at a time: the group's loads before its chain
+      const int jb = j0 + g;
+      uint32_t w1[12], w2[10];
+#pragma unroll
+      for (int k = 0; k < 12; ++k) w1[k] = up1[min(jb - 2 + k, W + 1)];  // up1[jb-2 .. jb+9]
+#pragma unroll
+      for (int k = 0; k < 10; ++k) w2[k] = up2[min(jb - 1 + k, W + 1)];  // up2[jb-1 .. jb+8]
+      const uint8_t* o = ocur + g;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint32_t t = min(w2[k] + CV_LONG, w2[k + 2] + CV_LONG);
+        t = min(t, w1[k] + CV_LONG);
+        t = min(t, w1[k + 1] + CV_DIAG);
+        t = min(t, w1[k + 2] + CV_HV);
+        t = min(t, w1[k + 3] + CV_DIAG);
+        t = min(t, w1[k + 4] + CV_LONG);
+        const uint64_t nr = o[k] ? 0ull : min((uint64_t)t, run + CV_HV);
+        run = jb + k < j1 ? nr : run;
+        loc[g + k] = (uint32_t)nr;
+      }
+    }
+    // value at column j0 - 1: a source at column js holding v contributes v + (j - js) HV, the
+    // border (INIT at column -1) INIT + (j + 1) HV; carried as v + (W - js) HV, which stays below
+    // 2^32 (v < 3.3e9, W HV < 5.4e8 at W <= 8192), and the minimum exceeds (W - j) HV
+    const uint32_t mine = j0 < j1 ? (uint32_t)run + (uint32_t)(W - (j1 - 1)) * CV_HV : 0xFFFFFFFFu;
+    const uint32_t carry = min(wave_excl_min_scan_up(mine), CV_INIT + (uint32_t)(W + 1) * CV_HV);
+    __syncthreads();  // every lane has read the previous rows' slots it needs (cur is written below)
+#pragma unroll
+    for (int k = 0; k < CM; ++k) {
+      const int j = j0 + k;
+      if (j < j1) {
+        const uint32_t v = min(loc[k], carry - (uint32_t)(W - j) * CV_HV);
+        cur[j] = v;
+        tmp[(size_t)i * W + j] = v;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CM; ++k) ocur[k] = onext[k];
+    __syncthreads();
+  }
+  __threadfence_block();  // the forward rows in tmp are re-read below by the same lanes only
+  // ---- backward pass: rows bottom to top, columns right to left
+  for (int k = lane; k < 3 * S; k += 64) srows[k] = CV_INIT;
+  __syncthreads();
+  float dmin = INFINITY, dmax = -INFINITY;
+  uint32_t fcur[CM], fnext[CM];
+#pragma unroll
+  for (int k = 0; k < CM; ++k) fcur[k] = j0 + k < j1 ? tmp[(size_t)(H - 1) * W + j0 + k] : 0u;
+  for (int i = H - 1; i >= 0; --i) {
+    const int r = H - 1 - i;                                  // rows done so far
+    const uint32_t* dn2 = srows + ((r + 1) % 3) * S + CH_B;  // row i + 2 (INIT below the map)
+    const uint32_t* dn1 = srows + ((r + 2) % 3) * S + CH_B;  // row i + 1
+    uint32_t* cur = srows + (r % 3) * S + CH_B;
+    const uint32_t* tnrow = tmp + (size_t)max(i - 1, 0) * W;
+#pragma unroll
+    for (int k = 0; k < CM; ++k) fnext[k] = j0 + k < j1 ? tnrow[j0 + k] : 0u;
+    uint64_t run = 0xFFFFFFFFull;
+#pragma unroll
+    for (int g = CM - 8; g >= 0; g -= 8) {  // right to left, 8 columns at a time
+      const int jl = j0 + g;  // columns jl .. jl + 7 (those < j1)
+      uint32_t w1[12], w2[10];
+#pragma unroll
+      for (int k = 0; k < 12; ++k) w1[k] = dn1[min(jl - 2 + k, W + 1)];  // dn1[jl-2 .. jl+9]
+#pragma unroll
+      for (int k = 0; k < 10; ++k) w2[k] = dn2[min(jl - 1 + k, W + 1)];  // dn2[jl-1 .. jl+8]
+      const uint32_t* f = fcur + g;
+#pragma unroll
+      for (int k = 7; k >= 0; --k) {
+        uint32_t t = f[k];
+        t = min(t, w2[k + 2] + CV_LONG);  // dn2[j + 1]
+        t = min(t, w2[k] + CV_LONG);      // dn2[j - 1]
+        t = min(t, w1[k + 4] + CV_LONG);  // dn1[j + 2]
+        t = min(t, w1[k + 3] + CV_DIAG);  // dn1[j + 1]
+        t = min(t, w1[k + 2] + CV_HV);    // dn1[j]
+        t = min(t, w1[k + 1] + CV_DIAG);  // dn1[j - 1]
+        t = min(t, w1[k] + CV_LONG);      // dn1[j - 2]
+        const uint64_t nr = min((uint64_t)t, run + CV_HV);
+        run = jl + k < j1 ? nr : run;
+        loc[g + k] = (uint32_t)nr;
+      }
+    }
+    // value at column j1: a source at column js holding v contributes v + (js - j) HV, the border
+    // (INIT at column W) INIT + (W - j) HV; carried as v + js HV (< 2^32 as above)
+    const uint32_t mine = j0 < j1 ? (uint32_t)run + (uint32_t)j0 * CV_HV : 0xFFFFFFFFu;
+    const uint32_t carry = min(wave_excl_min_scan_down(mine, lane), CV_INIT + (uint32_t)W * CV_HV);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CM; ++k) {
+      const int j = j0 + k;
+      if (j < j1) {
+        const uint32_t v = min(loc[k], carry - (uint32_t)j * CV_HV);
+        cur[j] = v;
+        const float d = (float)v * (1.0f / 65536.0f);
+        dist[(size_t)i * W + j] = d;
+        dmin = fminf(dmin, d);
+        dmax = fmaxf(dmax, d);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CM; ++k) fcur[k] = fnext[k];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    dmin = fminf(dmin, __shfl_xor(dmin, o, 64));
+    dmax = fmaxf(dmax, __shfl_xor(dmax, o, 64));
+  }
+  if (lane == 0) {
+    range[0] = __builtin_bit_cast(int32_t, dmin);
+    range[1] = __builtin_bit_cast(int32_t, dmax);
+  }
+}
+
+// cv2.normalize(NORM_MINMAX, 0, 1) (:375) in float64 from the float32 map, then (1 - d)**power
+// (:376): 1 - d in float32, the power correctly rounded to float32.
+__global__ __launch_bounds__(CM_THREADS) void costmap_cv_scale_kernel(const float* __restrict__ dist, int64_t n,
+                                                                      const int32_t* __restrict__ range, int power,
+                                                                      float* __restrict__ out) {
+  const double lo = (double)__builtin_bit_cast(float, range[0]);
+  const double hi = (double)__builtin_bit_cast(float, range[1]);
+  const double scale = (hi - lo > 2.220446049250313e-16) ? 1.0 / (hi - lo) : 0.0;
+  const double shift = 0.0 - lo * scale;
+  for (int64_t i = (int64_t)blockIdx.x * CM_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * CM_THREADS) {
+    const float dn = (float)((double)dist[i] * scale + shift);
+    const float b = 1.0f - dn;
+    out[i] = (float)pow_int_dd((double)b, power);
+  }
+}
+
 }  // namespace
 
 hipError_t launch_costmap_build(const CostmapScratch& sc, int n_obs, int size, int power, float* out,
-                                hipStream_t st) {
+                                hipStream_t st, int metric) {
   const size_t cells = (size_t)size * size;
   hipError_t e = hipMemsetAsync(sc.occ, 0, cells, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(costmap_raster_kernel, dim3(n_obs > 0 ? n_obs : 1), dim3(CM_THREADS), 0, st, sc.obs, n_obs,
                      sc.xs, size, sc.occ, sc.range);
+  if (metric == COSTMAP_CHAMFER5) {
+    float* dist = reinterpret_cast<float*>(sc.d2);
+    const size_t lds = (size_t)3 * (size + 2 * CH_B) * sizeof(uint32_t);
+    uint32_t* t32 = reinterpret_cast<uint32_t*>(sc.g2);
+    const int per = (size + 63) / 64;  // columns per lane
+    if (per <= 8)
+      hipLaunchKernelGGL(costmap_chamfer_kernel<8>, dim3(1), dim3(64), lds, st, sc.occ, size, size, t32, dist, sc.range);
+    else if (per <= 16)
+      hipLaunchKernelGGL(costmap_chamfer_kernel<16>, dim3(1), dim3(64), lds, st, sc.occ, size, size, t32, dist, sc.range);
+    else if (per <= 32)
+      hipLaunchKernelGGL(costmap_chamfer_kernel<32>, dim3(1), dim3(64), lds, st, sc.occ, size, size, t32, dist, sc.range);
+    else if (per <= 64)
+      hipLaunchKernelGGL(costmap_chamfer_kernel<64>, dim3(1), dim3(64), lds, st, sc.occ, size, size, t32, dist, sc.range);
+    else
+      hipLaunchKernelGGL(costmap_chamfer_kernel<128>, dim3(1), dim3(64), lds, st, sc.occ, size, size, t32, dist, sc.range);
+    const unsigned blocks = (unsigned)std::min<size_t>((cells + CM_THREADS - 1) / CM_THREADS, 256 * 8);
+    hipLaunchKernelGGL(costmap_cv_scale_kernel, dim3(blocks), dim3(CM_THREADS), 0, st, dist, (int64_t)cells,
+                       sc.range, power, out);
+    return hipGetLastError();
+  }
   const int nseg = (size + COSTMAP_SEG - 1) / COSTMAP_SEG;
   const dim3 cgrid((size + CM_THREADS - 1) / CM_THREADS, nseg);
   hipLaunchKernelGGL(costmap_colseg_kernel, cgrid, dim3(CM_THREADS), 0, st, sc.occ, size, sc.first, sc.last);

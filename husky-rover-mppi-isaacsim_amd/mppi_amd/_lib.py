@@ -99,11 +99,11 @@ _PROTOS = {
     "mppi_bilinear_tiled": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mppi_sync": (C.c_int, [C.c_void_p]),
     "mppi_build_costmap": (C.c_int, [C.c_void_p, _DP, C.c_int32, C.c_int32, C.c_double, C.c_double,
-                                     C.c_double, C.c_double, C.c_int32, _FP]),
+                                     C.c_double, C.c_double, C.c_int32, _FP, C.c_int32]),
     "mppi_costmap_builder_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
     "mppi_costmap_builder_destroy": (None, [C.c_void_p]),
     "mppi_costmap_builder_build": (C.c_int, [C.c_void_p, _DP, C.c_int32, C.c_int32, C.c_double, C.c_double,
-                                             C.c_double, C.c_double, C.c_int32, _FP, C.c_void_p]),
+                                             C.c_double, C.c_double, C.c_int32, _FP, C.c_void_p, C.c_int32]),
     "mppi_costmap_builder_last_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
     "mppi_rollout_python25d": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, _DP, _DP, _DP, _DP, _DP, C.c_double,
                                          C.c_double, C.c_double, C.c_double, _DP, C.POINTER(C.c_int32)]),
@@ -151,6 +151,15 @@ def _obstacles(obstacles):
     return a, a.ctypes.data_as(_DP)
 
 
+COSTMAP_METRICS = {"chamfer": 0, "exact": 1}   # mppi_costmap_metric (include/mppi.h)
+
+
+def _metric(m):
+    if m not in COSTMAP_METRICS:
+        raise ValueError(f"costmap metric must be one of {sorted(COSTMAP_METRICS)}, got {m!r}")
+    return COSTMAP_METRICS[m]
+
+
 class CostmapBuilder:
     """Surface.create_obstacles_costmap (MPPI_isaac.py:361-378) on the GPU, no controller context needed.
 
@@ -166,13 +175,15 @@ class CostmapBuilder:
                "mppi_costmap_builder_create")
         self.h = h
 
-    def build(self, obstacles, origin, size, half_width, r_robot, power=20, out_device=None):
+    def build(self, obstacles, origin, size, half_width, r_robot, power=20, out_device=None, metric="chamfer"):
+        """metric "chamfer": the reference's cv2.distanceTransform(DIST_L2, 5); "exact": exact EDT."""
         obs, optr = _obstacles(obstacles)
         out = None if out_device is not None else np.empty((size, size), np.float32)
         _check(self.lib, self.lib.mppi_costmap_builder_build(
             self.h, optr, obs.shape[0], int(size), float(half_width), float(origin[0]), float(origin[1]),
             float(r_robot), int(power), None if out is None else _fp(out),
-            None if out_device is None else C.c_void_p(int(out_device))), "mppi_costmap_builder_build")
+            None if out_device is None else C.c_void_p(int(out_device)), _metric(metric)),
+            "mppi_costmap_builder_build")
         return out
 
     def last_ms(self):
@@ -305,14 +316,16 @@ class Engine:
             resolution = 2.0 * half_width / size
         self._c(self.lib.mppi_set_costmap(self.ctx, _fp(cm), size, half_width, resolution), "mppi_set_costmap")
 
-    def build_costmap(self, obstacles, origin, size, half_width, r_robot, power=20, copy_out=True):
+    def build_costmap(self, obstacles, origin, size, half_width, r_robot, power=20, copy_out=True,
+                      metric="chamfer"):
         """Surface.create_obstacles_costmap + costmap_wp.assign in one device pass
         (visual_terrain_stack_full_terrain.py:561-563); returns the map if copy_out."""
         obs, optr = _obstacles(obstacles)
         out = np.empty((size, size), np.float32) if copy_out else None
         self._c(self.lib.mppi_build_costmap(self.ctx, optr, obs.shape[0], int(size), float(half_width),
                                             float(origin[0]), float(origin[1]), float(r_robot), int(power),
-                                            None if out is None else _fp(out)), "mppi_build_costmap")
+                                            None if out is None else _fp(out), _metric(metric)),
+                "mppi_build_costmap")
         return out
 
     def rollout_python25d(self, x0, y0, heading, lin_vel, ang_vel, dt, half_width, resolution, bound=20.0):

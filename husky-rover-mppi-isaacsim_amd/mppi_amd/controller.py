@@ -136,16 +136,20 @@ class Surface:
 
     # device the HIP costmap builder runs on (the reference's Warp arrays live on "cuda" = device 0)
     device = 0
+    # distance metric of the costmap builder: "chamfer" = cv2.distanceTransform(DIST_L2, 5) (reference)
+    costmap_metric = "chamfer"
 
     def create_obstacles_costmap(self, obstacles, origin):
-        """MPPI_isaac.py:361-378 on the GPU (csrc/mppi_costmap.hip): disc raster, exact EDT in place of
-        cv2.distanceTransform, min-max normalise, (1 - d)**20; returns the ndarray."""
+        """MPPI_isaac.py:361-378 on the GPU (csrc/mppi_costmap.hip): disc raster, cv2.distanceTransform
+        (DIST_L2, 5) as OpenCV's published 5x5 chamfer, min-max normalise, (1 - d)**20; returns the
+        ndarray (``costmap_metric = "exact"`` selects the exact EDT instead)."""
         from . import _lib
         b = getattr(self, "_builder", None)
         if b is None:
             b = self._builder = _lib.CostmapBuilder(self.device)
         self.obstacles = obstacles
-        return b.build(obstacles, origin, self.costmap_size, self.half_width, self.r_robot, power=20)
+        return b.build(obstacles, origin, self.costmap_size, self.half_width, self.r_robot, power=20,
+                       metric=self.costmap_metric)
 
 
 # =====================================================================  Robot
@@ -320,7 +324,8 @@ class MPPI_Controller:
             raise RuntimeError("call warp_setup() first")
         s = self.surface
         s.obstacles = obstacles
-        s.costmap = self.engine.build_costmap(obstacles, origin, s.costmap_size, s.half_width, s.r_robot, 20)
+        s.costmap = self.engine.build_costmap(obstacles, origin, s.costmap_size, s.half_width, s.r_robot, 20,
+                                              metric=getattr(s, "costmap_metric", "chamfer"))
         return s.costmap
 
     @property

@@ -139,27 +139,36 @@ int mppi_set_costmap(mppi_ctx* ctx, const float* costmap_host, int32_t size, flo
  * obstacle the disc x_local = y_global - y0, y_local = x_global - x0, radius
  * r_obs/2 + r_robot + 0.1 is marked on the size x size grid
  * X, Y = meshgrid(linspace(-half_width, half_width, size)) (float64, as the
- * reference); then exact Euclidean distance to the nearest marked cell, min-max
- * normalised, (1 - d)^power (the reference: 20), rounded to float32.  DEFINED:
- * exact EDT where the reference calls cv2.distanceTransform(DIST_L2, 5) (a 5x5
- * chamfer approximation; cv2 is unavailable); no obstacle
- * at all gives an all-1 map.  2 <= size <= 8192.
+ * reference); then the distance to the nearest marked cell, min-max normalised,
+ * (1 - d)^power (the reference: 20), float32.  metric MPPI_COSTMAP_CHAMFER5 (the
+ * reference's cv2.distanceTransform(DIST_L2, 5), :374): OpenCV's published
+ * 5x5 chamfer (distanceTransform_5x5, 16.16 fixed point), cv2.normalize
+ * NORM_MINMAX in float64, (1 - d) in float32, the power correctly rounded
+ * (oracle/costmap_ref.py; parity unpinned: cv2 is unavailable).
+ * MPPI_COSTMAP_EXACT: exact Euclidean distance, float64 normalise + power, one
+ * rounding; no obstacle at all gives an all-1 map.
+ * 2 <= size <= 8192.
  *
  * mppi_build_costmap builds straight into the context's costmap (what the
  * reference's create + assign pair leaves in costmap_wp; resolution becomes
  * 2*half_width/size, MPPI_isaac.py:272) and, if out_host != NULL, also copies
  * it to out_host [size*size] (the ndarray the reference returns).  Synchronous.
  * The builder object does the same without a controller context. */
+enum mppi_costmap_metric {
+  MPPI_COSTMAP_CHAMFER5 = 0, /* cv2.distanceTransform(DIST_L2, 5), MPPI_isaac.py:374 (default) */
+  MPPI_COSTMAP_EXACT = 1,    /* exact Euclidean distance transform */
+};
 typedef struct mppi_costmap_builder mppi_costmap_builder;
 int mppi_build_costmap(mppi_ctx* ctx, const double* obstacles, int32_t n, int32_t size,
                        double half_width, double origin_x, double origin_y, double r_robot,
-                       int32_t power, float* out_host);
+                       int32_t power, float* out_host, int32_t metric);
 int mppi_costmap_builder_create(int32_t device, mppi_costmap_builder** out);
 void mppi_costmap_builder_destroy(mppi_costmap_builder* b);
 /* out_host [size*size] (host) or out_device [size*size] (device memory); either may be NULL. */
 int mppi_costmap_builder_build(mppi_costmap_builder* b, const double* obstacles, int32_t n,
                                int32_t size, double half_width, double origin_x, double origin_y,
-                               double r_robot, int32_t power, float* out_host, float* out_device);
+                               double r_robot, int32_t power, float* out_host, float* out_device,
+                               int32_t metric);
 /* Device time (HIP events) of the builder's last build, in milliseconds. */
 int mppi_costmap_builder_last_ms(mppi_costmap_builder* b, double* ms);
 

@@ -17,12 +17,24 @@ Line by line:
   :375  distance_map = cv2.normalize(distance_map, None, 0, 1.0, NORM_MINMAX)
   :376  costmap = (1 - distance_map)**20
 
-DEFINED: cv2 is not installable here, so its 5x5 chamfer approximation cannot
-be reproduced or pinned ("parity unpinned" for that one call).  The distance is the EXACT
-Euclidean distance to the nearest occupied cell (scipy.ndimage.distance_transform_edt, checked
-below against a brute-force numpy EDT), the normalisation and the power run in float64 and the
-result is rounded once to float32.  No occupied cell at all -> all-1 map (what cv2.normalize
-gives a constant map: scale 0, shift 0, then (1 - 0)**20).
+:374 (default, `chamfer_l2_5x5`): cv2 is not installable here (opencv-python, unpinned in the
+reference's pyproject.toml:22), so its published algorithm is restated: OpenCV
+imgproc/src/distransform.cpp, distanceTransform_5x5 with the DIST_L2 mask-5 metrics
+{a, b, c} = {1, 1.4, 2.1969} (getDistanceTransformMask, maskType 52) in 16-bit fixed point
+(CV_FLT_TO_FIX: 65536, 91750, 143976), INIT_DIST0 = INT_MAX on a 2-pixel border, a forward raster
+pass over the upper half-mask and a backward pass over the lower one, d = float(t) / 65536.
+Pinned only against the literal per-pixel loop below (`chamfer_l2_5x5_loops`), not against cv2
+itself (parity unpinned: x86 wheels of opencv may route this call through IPP's float
+implementation instead, which can differ in the last bits).
+:375 cv2.normalize(NORM_MINMAX, 0, 1): scale = 1 / (max - min), shift = -min * scale in float64,
+dst = float32(src * scale + shift) (OpenCV's convertTo with alpha, beta); a constant map gives
+scale 0 -> all zeros.
+:376 (1 - d)**20 on the float32 map: 1 - d rounded to float32, the power correctly rounded to
+float32 (computed in float64: what numpy's float32 power / libm powf return barring last-bit ties).
+
+`exact` metric (the builder's option): the exact Euclidean distance
+(scipy.ndimage.distance_transform_edt, checked against a brute-force numpy EDT), normalised and
+raised to the power in float64, rounded once to float32.  No occupied cell at all -> all-1 map.
 """
 from __future__ import annotations
 
@@ -79,3 +91,99 @@ def create_obstacles_costmap(obstacles, origin, size, half_width, r_robot, power
     if out is None:
         return np.ones((size, size), np.float32)
     return out
+
+
+# ------------------------------------------------------------------ cv2.distanceTransform(DIST_L2, 5)
+CV_HV, CV_DIAG, CV_LONG = 65536, 91750, 143976   # CV_FLT_TO_FIX(1, 1.4f, 2.1969f, 16)
+CV_INIT = 0x7FFFFFFF                              # INIT_DIST0 = INT_MAX
+
+
+def _row_min_scan(a, step):
+    """t[j] = min(a[j], t[j-1] + step) left to right (a prefix min of a[k] - k*step)."""
+    k = np.arange(a.size, dtype=np.int64) * step
+    return np.minimum.accumulate(a - k) + k
+
+
+def chamfer_l2_5x5(occ):
+    """OpenCV distanceTransform_5x5 (distransform.cpp) on the reference's uint8 map (255 free, 0
+    obstacle): the two raster passes in 16.16 fixed point, vectorised per row (the left-to-right /
+    right-to-left chains of a row as min-plus scans, exact in int64).  Returns float32 distances."""
+    H, W = occ.shape
+    B = 2
+    T = np.full((H + 2 * B, W + 2 * B), CV_INIT, np.int64)
+    free = ~occ
+    for i in range(H):                       # forward pass (upper half of the mask)
+        r = i + B
+        up2, up1 = T[r - 2], T[r - 1]
+        c = slice(B, B + W)
+        a = np.minimum.reduce([up2[B - 1:B - 1 + W] + CV_LONG, up2[B + 1:B + 1 + W] + CV_LONG,
+                               up1[B - 2:B - 2 + W] + CV_LONG, up1[B - 1:B - 1 + W] + CV_DIAG,
+                               up1[c] + CV_HV, up1[B + 1:B + 1 + W] + CV_DIAG,
+                               up1[B + 2:B + 2 + W] + CV_LONG])
+        a = np.where(free[i], a, 0)
+        # left border pixel tmp[-1] = INIT: a[0] also competes with INIT + HV
+        a[0] = min(a[0], CV_INIT + CV_HV) if free[i, 0] else 0
+        T[r, c] = _row_min_scan(a, CV_HV)
+    for i in range(H - 1, -1, -1):           # backward pass (lower half of the mask)
+        r = i + B
+        dn1, dn2 = T[r + 1], T[r + 2]
+        c = slice(B, B + W)
+        a = np.minimum.reduce([T[r, c], dn2[B + 1:B + 1 + W] + CV_LONG, dn2[B - 1:B - 1 + W] + CV_LONG,
+                               dn1[B + 2:B + 2 + W] + CV_LONG, dn1[B + 1:B + 1 + W] + CV_DIAG,
+                               dn1[c] + CV_HV, dn1[B - 1:B - 1 + W] + CV_DIAG, dn1[B - 2:B - 2 + W] + CV_LONG])
+        a[W - 1] = min(a[W - 1], CV_INIT + CV_HV)
+        T[r, c] = _row_min_scan(a[::-1], CV_HV)[::-1]
+    t = T[B:B + H, B:B + W]
+    return (t.astype(np.uint32).astype(np.float32) * np.float32(1.0 / 65536)).astype(np.float32)
+
+
+def chamfer_l2_5x5_loops(occ):
+    """The same, pixel by pixel as distransform.cpp writes it (small maps only): pins the above."""
+    H, W = occ.shape
+    B = 2
+    T = [[CV_INIT] * (W + 2 * B) for _ in range(H + 2 * B)]
+    for i in range(H):
+        r = i + B
+        for j in range(B, W + B):
+            if occ[i, j - B]:
+                T[r][j] = 0
+                continue
+            t0 = T[r - 2][j - 1] + CV_LONG
+            for t in (T[r - 2][j + 1] + CV_LONG, T[r - 1][j - 2] + CV_LONG, T[r - 1][j - 1] + CV_DIAG,
+                      T[r - 1][j] + CV_HV, T[r - 1][j + 1] + CV_DIAG, T[r - 1][j + 2] + CV_LONG,
+                      T[r][j - 1] + CV_HV):
+                t0 = min(t0, t)
+            T[r][j] = t0
+    out = np.zeros((H, W), np.float32)
+    for i in range(H - 1, -1, -1):
+        r = i + B
+        for j in range(W + B - 1, B - 1, -1):
+            t0 = T[r][j]
+            if t0 > CV_HV:
+                for t in (T[r + 2][j + 1] + CV_LONG, T[r + 2][j - 1] + CV_LONG, T[r + 1][j + 2] + CV_LONG,
+                          T[r + 1][j + 1] + CV_DIAG, T[r + 1][j] + CV_HV, T[r + 1][j - 1] + CV_DIAG,
+                          T[r + 1][j - 2] + CV_LONG, T[r][j + 1] + CV_HV):
+                    t0 = min(t0, t)
+                T[r][j] = t0
+            out[i, j - B] = np.float32(np.float32(t0 & 0xFFFFFFFF) * np.float32(1.0 / 65536))
+    return out
+
+
+def cv_normalize_minmax(d):
+    """cv2.normalize(d, None, 0, 1.0, NORM_MINMAX) on a float32 map."""
+    lo, hi = float(d.min()), float(d.max())
+    scale = 1.0 / (hi - lo) if hi - lo > np.finfo(np.float64).eps else 0.0
+    shift = 0.0 - lo * scale
+    return (d.astype(np.float64) * scale + shift).astype(np.float32)
+
+
+def cv_power(dn, power):
+    """(1 - dn)**power on the float32 map: 1 - dn in float32, the power rounded once to float32."""
+    b = (np.float32(1.0) - dn).astype(np.float32)
+    return (b.astype(np.float64) ** power).astype(np.float32)
+
+
+def create_obstacles_costmap_cv(obstacles, origin, size, half_width, r_robot, power=20):
+    """Surface.create_obstacles_costmap (MPPI_isaac.py:361-378) with the restated cv2 calls."""
+    occ = raster(obstacles, origin, size, half_width, r_robot)
+    return cv_power(cv_normalize_minmax(chamfer_l2_5x5(occ)), power)

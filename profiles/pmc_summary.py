@@ -20,7 +20,8 @@ from collections import defaultdict
 
 def short(name):
     name = name.strip('"')
-    for key in ("mppi_rollout_pair_kernel", "mppi_rollout_ws_kernel", "mppi_noise_kernel", "mppi_tail_kernel", "mppi_rollout_kernel", "mppi_finish_kernel", "mppi_bilinear_kernel"):
+    for key in ("mppi_rollout_roles_kernel", "mppi_rollout_pair_kernel", "mppi_noise_kernel", "mppi_tail_kernel",
+                "mppi_colfin_kernel", "mppi_finish_kernel", "mppi_bilinear_kernel"):
         if key in name:
             return key
     return name.split("(")[0][:60]
@@ -43,8 +44,7 @@ def main(root, K=65536, H=100):
             d["hbm_bytes_per_launch"] = d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]
         if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d and d["TCC_HIT_sum"] + d["TCC_MISS_sum"] > 0:
             d["l2_hit_rate"] = d["TCC_HIT_sum"] / (d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
-    roll = (out.get("mppi_rollout_pair_kernel") or out.get("mppi_rollout_ws_kernel")
-            or out.get("mppi_rollout_kernel", {}))
+    roll = (out.get("mppi_rollout_roles_kernel") or out.get("mppi_rollout_pair_kernel") or {})
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     summary = {"K": K, "H": H, "src_sha256": bench.source_hash(), "git_head": os.environ.get("GIT_HEAD"),

@@ -1,9 +1,11 @@
 """CPU: the obstacle-costmap restatement (oracle/costmap_ref.py, MPPI_isaac.py:361-378).
 
-Pins the exact-EDT call against an exhaustive search, and the raster against the reference's
-frame convention (x_local = y_global - y0 marks a COLUMN coordinate, y_local = x_global - x0 a
-ROW coordinate of meshgrid(linspace(-hw, hw, size))).  cv2.distanceTransform itself is
-"parity unpinned" (cv2 is absent).
+Pins the exact-EDT call against an exhaustive search, the vectorised 5x5 chamfer (OpenCV's
+distanceTransform_5x5, the reference's cv2.distanceTransform(DIST_L2, 5)) against its literal
+per-pixel loop, and the raster against the reference's frame convention (x_local = y_global - y0
+marks a COLUMN coordinate, y_local = x_global - x0 a ROW coordinate of
+meshgrid(linspace(-hw, hw, size))).  cv2 itself is absent: the chamfer restatement is "parity
+unpinned" against it.
 """
 import numpy as np
 import pytest
@@ -39,4 +41,32 @@ def test_edge_cases():
     full = CR.create_obstacles_costmap([[0.0, 0.0, 100.0]], (0, 0), size, 5.0, 1.2)
     assert np.array_equal(full, np.ones((size, size), np.float32))
     cm = CR.create_obstacles_costmap(_rocks(5, 4.0, 3), (0, 0), size, 5.0, 0.3)
+    assert cm.dtype == np.float32 and cm.max() == 1.0 and cm.min() == 0.0
+
+
+@pytest.mark.parametrize("shape,p,seed", [((23, 31), 0.1, 0), ((40, 17), 0.01, 1), ((9, 64), 0.3, 2),
+                                           ((33, 33), 0.0, 3), ((12, 12), 1.0, 4), ((1, 50), 0.05, 5)])
+def test_chamfer_vectorised_matches_per_pixel_loop(shape, p, seed):
+    occ = np.random.RandomState(seed).rand(*shape) < p
+    assert np.array_equal(CR.chamfer_l2_5x5(occ), CR.chamfer_l2_5x5_loops(occ))
+
+
+def test_chamfer_known_distances():
+    """One obstacle pixel: the mask-5 metric {1, 1.4, 2.1969} in 16.16 fixed point along the axes,
+    the diagonal and the knight's move."""
+    occ = np.zeros((9, 9), bool)
+    occ[4, 4] = True
+    d = CR.chamfer_l2_5x5(occ)
+    fx = lambda t: np.float32(np.float32(t) * np.float32(1 / 65536))
+    assert d[4, 4] == 0
+    assert d[4, 7] == fx(3 * 65536) and d[1, 4] == fx(3 * 65536)
+    assert d[6, 6] == fx(2 * 91750)
+    assert d[5, 6] == fx(143976) and d[2, 3] == fx(143976)
+
+
+def test_chamfer_costmap_edges():
+    size = 32
+    full = CR.create_obstacles_costmap_cv([[0.0, 0.0, 100.0]], (0, 0), size, 5.0, 1.2)
+    assert np.array_equal(full, np.ones((size, size), np.float32))   # min == max: scale 0
+    cm = CR.create_obstacles_costmap_cv(_rocks(5, 4.0, 3), (0, 0), size, 5.0, 0.3)
     assert cm.dtype == np.float32 and cm.max() == 1.0 and cm.min() == 0.0

@@ -1,9 +1,11 @@
 """GPU: the HIP obstacle-costmap builder (csrc/mppi_costmap.hip) vs oracle/costmap_ref.py.
 
-Surface.create_obstacles_costmap (MPPI_isaac.py:361-378) with the exact EDT.
-Raster and squared distances are integer/boolean work and must match exactly; the float64
-normalise + power, rounded once to float32, is expected bit-exact too (both sides produce the
-correctly rounded power), so the test asserts equality and reports any cell that differs.
+Surface.create_obstacles_costmap (MPPI_isaac.py:361-378) with both distance metrics: "chamfer",
+the reference's cv2.distanceTransform(DIST_L2, 5) restated from OpenCV's published 5x5 chamfer
+(parity unpinned: no cv2 here), and "exact", the exact EDT.  Raster and the
+fixed-point / squared distances are integer work and must match exactly; the normalise + power
+are expected bit-exact too (both sides round the power correctly), so the test asserts equality
+and reports any cell that differs.
 """
 import numpy as np
 import pytest
@@ -42,11 +44,15 @@ CASES = {
 }
 
 
+ORACLE = {"chamfer": CR.create_obstacles_costmap_cv, "exact": CR.create_obstacles_costmap}
+
+
+@pytest.mark.parametrize("metric", list(ORACLE))
 @pytest.mark.parametrize("name", list(CASES))
-def test_builder_matches_oracle(builder, name):
+def test_builder_matches_oracle(builder, name, metric):
     obs, origin, size, hw, rr, power = CASES[name]
-    want = CR.create_obstacles_costmap(obs, origin, size, hw, rr, power)
-    got = builder.build(obs, origin, size, hw, rr, power)
+    want = ORACLE[metric](obs, origin, size, hw, rr, power)
+    got = builder.build(obs, origin, size, hw, rr, power, metric=metric)
     assert got.shape == want.shape and got.dtype == np.float32
     assert np.array_equal(got, want), hp.mismatch_report(name, got, want)
 
@@ -57,7 +63,7 @@ def test_engine_build_costmap_equals_upload():
     Z, hw, _ = hp.c3_scene()
     st = hp.oracle_state()
     obs = _rocks(750, 50.0, 99, 0.4)
-    want = CR.create_obstacles_costmap(obs, (1.0, -2.0), 187, hw, 1.2, 20)   # grid 1500 / 8
+    want = CR.create_obstacles_costmap_cv(obs, (1.0, -2.0), 187, hw, 1.2, 20)   # grid 1500 / 8
     e1 = hp.engine_for(1024, 40, Z, hw, want, st)
     out1 = e1.step("3d", 0)
     e2 = hp.engine_for(1024, 40, Z, hw, np.zeros((4, 4), np.float32), st)
@@ -78,7 +84,7 @@ def test_surface_manual_costmap_on_gpu():
     obstacles = [[3.0, -2.0, 0.8], [-4.0, 5.0, 1.2]]
     s = Surface("manual", None, "manual", None, 160, 8.0, (0.0, 0.0), scene.BUMPS_9[:2], 1.2, obstacles)
     assert s.costmap.shape == (20, 20)
-    want = CR.create_obstacles_costmap(obstacles, (0.0, 0.0), 20, 8.0, 1.2, 20)
+    want = CR.create_obstacles_costmap_cv(obstacles, (0.0, 0.0), 20, 8.0, 1.2, 20)
     assert np.array_equal(s.costmap, want)
 
 
@@ -87,3 +93,5 @@ def test_bad_arguments_raise(builder):
         builder.build([[0, 0, 1]], (0, 0), 1, 5.0, 1.2)
     with pytest.raises(RuntimeError):
         builder.build([[0, 0, 1]], (0, 0), 9000, 5.0, 1.2)
+    with pytest.raises(ValueError):
+        builder.build([[0, 0, 1]], (0, 0), 16, 5.0, 1.2, metric="l1")
