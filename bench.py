@@ -48,6 +48,9 @@ CONFIGS = {
            "C4: K=1048576, H=100, 1500^2 DEM @0.1 m, 750^2 costmap @0.2 m"),
     "c5": (262144, 128, "scene_c5", (0.0, 0.0), (80.0, 20.0),
            "C5: K=262144, H=128, 8192^2 DEM @0.025 m (synthetic craters + fBm), 1024^2 costmap"),
+    # diagnostic: one GPU's shard of C4 at 8 GPUs (what each rank of the north-star scaling runs)
+    "c4s8": (131072, 100, "scene_c3", (-60.0, -5.0), (65.0, 10.0),
+             "C4 shard at 8 GPUs: K=131072, H=100, 1500^2 DEM @0.1 m, 750^2 costmap @0.2 m"),
 }
 KERNEL_SOURCES = ("mppi_kernels.hip", "mppi_kernels.h", "mppi_detmath.h", "mppi_capi.cpp", "Makefile")
 

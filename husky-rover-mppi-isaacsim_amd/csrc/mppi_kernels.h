@@ -98,12 +98,14 @@ constexpr int PAIR_TRAJ = 256;
 #define MPPI_PAIR_D 8
 #endif
 constexpr int PAIR_RING = MPPI_PAIR_D;  // = PAIR_D in mppi_kernels.hip
-// sin / cos of the Rodrigues angle computed by the side wave at production and handed to the
-// chain through the ring (v, sin, cos), off the chain's serial path; 0 = the chain computes them
+// sin / cos / 1 - cos of the Rodrigues angle computed by the side wave at production and handed to
+// the chain through the ring, off the chain's serial path (the chain is then chain_wave_3d, as in
+// the role-split kernel); 0 = the chain computes them (the unpacked chain3d_lean step)
 #ifndef MPPI_SC_SIDE
-#define MPPI_SC_SIDE 0
+#define MPPI_SC_SIDE 1
 #endif
-constexpr int PAIR_RING_IN = MPPI_SC_SIDE ? 3 : 2;  // floats per trajectory and step, side -> chain
+constexpr int PAIR_RING_IN = MPPI_SC_SIDE ? 4 : 2;  // floats per trajectory and step, side -> chain
+                                                    // (v, sin, cos, 1 - cos) or (v, w)
 hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
                                int mode, bool dump, bool roles = false);
 // The role-split rollout kernel (mppi_rollout_roles_kernel): the same 256 trajectories per

@@ -960,6 +960,154 @@ __device__ __forceinline__ void lds_store_release(int* f, int v) {
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// ---------------------------------------------------------------------  the chain wave (3D)
+// The serial 3D projection of 64 trajectories (projection_warp.py:306-348), shared by both
+// rollout kernels.  Reads (v, sin, cos, 1 - cos) of each step from ring_in [D][4][TB] once
+// f_prod covers it, writes (x, y, cx, cy) to ring_out [D][4][TB] and releases f_chain; a ring
+// slot is rewritten once every consumer counter f_cons[0..NC) has passed it.
+// Software-pipelined: iteration t orients step t (its normal gathered during iteration t - 1),
+// then advances the position of step t + 1 and issues that step's normal gather, which stays in
+// flight while step t's outputs are published.  Arithmetic: packed x / y FP32 (orient_step,
+// advance_step), every quotient and square root correctly rounded; an out-of-range lane redoes
+// its step with the IEEE operators.
+struct WaitStat {
+  uint64_t wait = 0, n = 0;  // MPPI_STAMPS builds: cycles spent in LDS waits, waits that read LDS
+};
+__device__ __forceinline__ void lds_wait_ge(const int* f, int target, int& seen, WaitStat& ws) {
+  if (seen >= target) return;
+#ifdef MPPI_STAMPS
+  const uint64_t t0 = dbg_stamp();
+#endif
+  int v;
+  while ((v = lds_load_acquire(f)) < target) __builtin_amdgcn_s_sleep(1);
+  seen = v;
+#ifdef MPPI_STAMPS
+  ws.wait += dbg_stamp() - t0;
+  ws.n += 1;
+#endif
+  (void)ws;
+}
+
+template <int TB, int NC, bool DUMP>
+__device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<false>& dem, const Traj& s, int tj,
+                                              bool valid, int64_t kl, const float* ring_in, float* ring_out,
+                                              const int* f_prod, int* f_chain, const int* const (&f_cons)[NC],
+                                              int& seen_prod, int (&seen_cons)[NC], WaitStat& ws) {
+  constexpr int D = PAIR_D;
+  constexpr int RI = 4;
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  const int H = a.H;
+  bool nobad = false;
+  {
+      // Software-pipelined: iteration t orients step t (its normal gathered during iteration
+      // t - 1), then advances the position of step t + 1 and issues that step's normal gather,
+      // which stays in flight while step t's outputs are published.  Register sets A / B
+      // alternate between steps (no loop-carried copy of a load in flight).
+      Head hd{f2{s.hx, s.hy}, s.hz};
+      f2 posA = f2{s.x, s.y}, posB = posA;
+      float4 nvA = make_float4(0.f, 0.f, 0.f, 0.f), nvB = nvA;
+      float snA = 0.f, csA = 0.f, omA = 0.f, snB = 0.f, csB = 0.f, omB = 0.f;
+      const f2 cell_off = f2{-a.x_min, a.y_min};
+      const float fi_hi = (float)(a.grid - 1), fj_lo = (float)(1 - a.rows);
+      const float4* ntab0 = dem.N + (a.grid + 2);  // entry (jj, ii) = (1 - tjj, ti + 1): offset ti - tjj * (grid + 1)
+      const int nrow = a.grid + 1;
+      // normal-table entry of the cell holding pos (Dem::cell + Dem::normal_cell)
+      auto gather = [&](f2 pos, float4& nv) __attribute__((always_inline)) {
+        f2 f;
+        if (dem.cdiv) {  // uniform: division by the verified reciprocal (cdiv_f), both axes at once
+          const f2 aa = pos + cell_off;
+          const f2 q0 = aa * bc2(dem.rinv);
+          const f2 r = pk_fma(-q0, bc2(dem.res), aa);
+          f = pk_fma(r, bc2(dem.rinv), q0);
+        } else {
+          f = f2{(pos.x - a.x_min) / a.res, (pos.y + a.y_min) / a.res};
+        }
+        const int ti = (int)__builtin_amdgcn_fmed3f(f.x, -1.0f, fi_hi);  // min(i, grid - 1)
+        const int tjj = (int)__builtin_amdgcn_fmed3f(f.y, fj_lo, 1.0f);  // -min(j, rows - 1)
+#if defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 1  // diagnostic builds only: one cell (L1 hits)
+        nv = ntab0[(ti - tjj * nrow) & 0];
+#elif defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 2  // diagnostic: no load
+        nv = make_float4(__builtin_bit_cast(float, ti) * 1e-30f, __builtin_bit_cast(float, tjj) * 1e-30f, 1.0f, 0.f);
+#else
+        nv = ntab0[ti - tjj * nrow];
+#endif
+      };
+      auto read_in = [&](int t, float& v, float& sn, float& cs, float& om, int need) __attribute__((always_inline)) {
+        if (need) lds_wait_ge(f_prod, need, seen_prod, ws);
+        const float* ri = ring_in + (t % D) * RI * TB + tj;
+        v = ri[0];
+        sn = ri[TB];
+        cs = ri[2 * TB];
+        om = ri[3 * TB];
+      };
+      {  // step 0's position and normal
+        float v0;
+        read_in(0, v0, snA, csA, omA, 1);
+        Lean l;
+        lean_init(l);
+        f2 p = advance_step<true>(hd, v0, a.dt, posA, l);
+        if (__builtin_expect(lean_bad(l), 0)) p = advance_step<false>(hd, v0, a.dt, posA, l);
+        posA = p;
+        gather(posA, nvA);
+      }
+      // step t in set X (pos, normal in flight, sin / cos / 1 - cos); step t + 1 into set Y.
+      // Even steps wait for two steps' worth of progress (the producer's steps t + 1, t + 2 and
+      // the consumers' ring slots of t, t + 1), odd steps are covered by them.
+      auto it = [&](auto even_tag, int t, f2& pX, float4& nX, float& snX, float& csX, float& omX, f2& pY,
+                    float4& nY, float& snY, float& csY, float& omY) __attribute__((always_inline)) {
+        constexpr bool EVEN = decltype(even_tag)::value;
+        const bool more = t + 1 < H;  // uniform
+        float v1 = 0.f;
+        if (more) read_in(t + 1, v1, snY, csY, omY, EVEN ? min(t + 3, H) : 0);
+        const f2 nxy = f2{nX.x, nX.y};
+        const float nz = nX.z;
+        Lean l;
+        lean_init(l);
+        Head ho = orient_step<true>(nxy, nz, hd, snX, csX, omX, l);
+        f2 p1 = pX;
+        if (more) p1 = advance_step<true>(ho, v1, a.dt, pX, l);
+        if (__builtin_expect(lean_bad(l), 0)) {  // operand outside the fast range: IEEE redo
+          ho = orient_step<false>(nxy, nz, hd, snX, csX, omX, l);
+          if (more) p1 = advance_step<false>(ho, v1, a.dt, pX, l);
+        }
+        if (more) {
+          pY = p1;
+          gather(pY, nY);
+        }
+        // wheel offset right = 0.2 * cross(normal, current_hv) (projection_warp.py:333)
+        const f2 cxy = bc2(a.off) * cross_xy(nxy, nz, ho.xy, ho.z);
+        if constexpr (EVEN) {
+#pragma unroll
+          for (int c = 0; c < NC; ++c) lds_wait_ge(f_cons[c], t - D + 2, seen_cons[c], ws);
+        }
+        float* ro = ring_out + (t % D) * 4 * TB + tj;
+        ro[0] = pX.x;
+        ro[TB] = pX.y;
+        ro[2 * TB] = cxy.x;
+        ro[3 * TB] = cxy.y;
+        if constexpr (DUMP) {
+          if (valid) {
+            float q[4];
+            dem.template corners<false>(pX.x, pX.y, q, nobad);
+            const float z = bilinear<false>(pX.x, pX.y, q, dem.template rr<false>(), nobad);
+            const size_t o3 = ((size_t)kl * H + t) * 3;
+            if (a.d_traj) { a.d_traj[o3] = pX.x; a.d_traj[o3 + 1] = pX.y; a.d_traj[o3 + 2] = z; }
+            if (a.d_hv) { a.d_hv[o3] = ho.xy.x; a.d_hv[o3 + 1] = ho.xy.y; a.d_hv[o3 + 2] = ho.z; }
+          }
+        }
+        lds_store_release(f_chain, t + 1);
+        hd = ho;
+      };
+      int t = 0;
+      for (; t + 1 < H; t += 2) {
+        it(T_{}, t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
+        it(F_{}, t + 1, posB, nvB, snB, csB, omB, posA, nvA, snA, csA, omA);
+      }
+      if (t < H) it(T_{}, t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
+  }
+}
+
 template <int TB, int PROJ, int MODE, bool DUMP>
 __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -1077,6 +1225,18 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   if (!side) {
     // ---------------- chain wave: the serial projection, one step per iteration
     int seen_prod = 0, seen_cons = 0;
+#if MPPI_SC_SIDE
+    if constexpr (PROJ == 3) {
+      const int* cons[1] = {f_cons};
+      int seen_c[1] = {0};
+      WaitStat ws;
+      chain_wave_3d<TB, 1, DUMP>(a, dem, s, tj, valid, kl, ring_in, ring_out, f_prod, f_chain, cons, seen_prod,
+                                 seen_c, ws);
+#ifdef MPPI_STAMPS
+      st_wait += ws.wait;
+#endif
+    } else
+#endif
     for (int sc = 0; sc < H; ++sc) {
       wait_ge(f_prod, sc + 1, seen_prod);
       wait_ge(f_cons, sc - D + 1, seen_cons);
@@ -1186,6 +1346,7 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
           dm_sincosf(wp * a.dt, &sn, &cs);
           ri[TB] = sn;
           ri[2 * TB] = cs;
+          ri[3 * TB] = 1.0f - cs;
         }
 #else
         ri[TB] = wp;
@@ -1442,111 +1603,19 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const R
     }
     int seen_prod = 0, seen_wheel = 0, seen_cost = 0;
     if constexpr (PROJ == 3) {
-      // Software-pipelined: iteration t orients step t (its normal gathered during iteration
-      // t - 1), then advances the position of step t + 1 and issues that step's normal gather,
-      // which stays in flight while step t's outputs are published.  Register sets A / B
-      // alternate between steps (no loop-carried copy of a load in flight).
-      Head hd{f2{s.hx, s.hy}, s.hz};
-      f2 posA = f2{s.x, s.y}, posB = posA;
-      float4 nvA = make_float4(0.f, 0.f, 0.f, 0.f), nvB = nvA;
-      float snA = 0.f, csA = 0.f, omA = 0.f, snB = 0.f, csB = 0.f, omB = 0.f;
-      const f2 cell_off = f2{-a.x_min, a.y_min};
-      const float fi_hi = (float)(a.grid - 1), fj_lo = (float)(1 - a.rows);
-      const float4* ntab0 = dem.N + (a.grid + 2);  // entry (jj, ii) = (1 - tjj, ti + 1): offset ti - tjj * (grid + 1)
-      const int nrow = a.grid + 1;
-      // normal-table entry of the cell holding pos (Dem::cell + Dem::normal_cell)
-      auto gather = [&](f2 pos, float4& nv) __attribute__((always_inline)) {
-        f2 f;
-        if (dem.cdiv) {  // uniform: division by the verified reciprocal (cdiv_f), both axes at once
-          const f2 aa = pos + cell_off;
-          const f2 q0 = aa * bc2(dem.rinv);
-          const f2 r = pk_fma(-q0, bc2(dem.res), aa);
-          f = pk_fma(r, bc2(dem.rinv), q0);
-        } else {
-          f = f2{(pos.x - a.x_min) / a.res, (pos.y + a.y_min) / a.res};
-        }
-        const int ti = (int)__builtin_amdgcn_fmed3f(f.x, -1.0f, fi_hi);  // min(i, grid - 1)
-        const int tjj = (int)__builtin_amdgcn_fmed3f(f.y, fj_lo, 1.0f);  // -min(j, rows - 1)
-#if defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 1  // diagnostic builds only: one cell (L1 hits)
-        nv = ntab0[(ti - tjj * nrow) & 0];
-#elif defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 2  // diagnostic: no load
-        nv = make_float4(__builtin_bit_cast(float, ti) * 1e-30f, __builtin_bit_cast(float, tjj) * 1e-30f, 1.0f, 0.f);
+      const int* cons[2] = {f_wheel, f_cost};
+      int seen_cons[2] = {0, 0};
+#ifdef MPPI_STAMPS
+      WaitStat ws;
+      chain_wave_3d<TB, 2, DUMP>(a, dem, s, tj, valid, kl, ring_in, ring_out, f_prod, f_chain, cons, seen_prod,
+                                 seen_cons, ws);
+      st_wait += ws.wait;
+      st_n += ws.n;
 #else
-        nv = ntab0[ti - tjj * nrow];
+      WaitStat ws;
+      chain_wave_3d<TB, 2, DUMP>(a, dem, s, tj, valid, kl, ring_in, ring_out, f_prod, f_chain, cons, seen_prod,
+                                 seen_cons, ws);
 #endif
-      };
-      auto read_in = [&](int t, float& v, float& sn, float& cs, float& om, int need) __attribute__((always_inline)) {
-        if (need) wait_ge(f_prod, need, seen_prod);
-        const float* ri = ring_in + (t % D) * RI * TB + tj;
-        v = ri[0];
-        sn = ri[TB];
-        cs = ri[2 * TB];
-        om = ri[3 * TB];
-      };
-      {  // step 0's position and normal
-        float v0;
-        read_in(0, v0, snA, csA, omA, 1);
-        Lean l;
-        lean_init(l);
-        f2 p = advance_step<true>(hd, v0, a.dt, posA, l);
-        if (__builtin_expect(lean_bad(l), 0)) p = advance_step<false>(hd, v0, a.dt, posA, l);
-        posA = p;
-        gather(posA, nvA);
-      }
-      // step t in set X (pos, normal in flight, sin / cos / 1 - cos); step t + 1 into set Y.
-      // Even steps wait for two steps' worth of progress (the producer's steps t + 1, t + 2 and
-      // the consumers' ring slots of t, t + 1), odd steps are covered by them.
-      auto it = [&](auto even_tag, int t, f2& pX, float4& nX, float& snX, float& csX, float& omX, f2& pY,
-                    float4& nY, float& snY, float& csY, float& omY) __attribute__((always_inline)) {
-        constexpr bool EVEN = decltype(even_tag)::value;
-        const bool more = t + 1 < H;  // uniform
-        float v1 = 0.f;
-        if (more) read_in(t + 1, v1, snY, csY, omY, EVEN ? min(t + 3, H) : 0);
-        const f2 nxy = f2{nX.x, nX.y};
-        const float nz = nX.z;
-        Lean l;
-        lean_init(l);
-        Head ho = orient_step<true>(nxy, nz, hd, snX, csX, omX, l);
-        f2 p1 = pX;
-        if (more) p1 = advance_step<true>(ho, v1, a.dt, pX, l);
-        if (__builtin_expect(lean_bad(l), 0)) {  // operand outside the fast range: IEEE redo
-          ho = orient_step<false>(nxy, nz, hd, snX, csX, omX, l);
-          if (more) p1 = advance_step<false>(ho, v1, a.dt, pX, l);
-        }
-        if (more) {
-          pY = p1;
-          gather(pY, nY);
-        }
-        // wheel offset right = 0.2 * cross(normal, current_hv) (projection_warp.py:333)
-        const f2 cxy = bc2(a.off) * cross_xy(nxy, nz, ho.xy, ho.z);
-        if constexpr (EVEN) {
-          wait_ge(f_wheel, t - D + 2, seen_wheel);
-          wait_ge(f_cost, t - D + 2, seen_cost);
-        }
-        float* ro = ring_out + (t % D) * 4 * TB + tj;
-        ro[0] = pX.x;
-        ro[TB] = pX.y;
-        ro[2 * TB] = cxy.x;
-        ro[3 * TB] = cxy.y;
-        if constexpr (DUMP) {
-          if (valid) {
-            float q[4];
-            dem.template corners<false>(pX.x, pX.y, q, nobad);
-            const float z = bilinear<false>(pX.x, pX.y, q, dem.template rr<false>(), nobad);
-            const size_t o3 = ((size_t)kl * H + t) * 3;
-            if (a.d_traj) { a.d_traj[o3] = pX.x; a.d_traj[o3 + 1] = pX.y; a.d_traj[o3 + 2] = z; }
-            if (a.d_hv) { a.d_hv[o3] = ho.xy.x; a.d_hv[o3 + 1] = ho.xy.y; a.d_hv[o3 + 2] = ho.z; }
-          }
-        }
-        lds_store_release(f_chain, t + 1);
-        hd = ho;
-      };
-      int t = 0;
-      for (; t + 1 < H; t += 2) {
-        it(T_{}, t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
-        it(F_{}, t + 1, posB, nvB, snB, csB, omB, posA, nvA, snA, csA, omA);
-      }
-      if (t < H) it(T_{}, t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
     } else
     for (int sc = 0; sc < H; ++sc) {
       wait_ge(f_prod, sc + 1, seen_prod);
@@ -1813,6 +1882,9 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const R
 #define MPPI_FIN_PRIO 0
 #endif
 constexpr int FIN_THREADS = 1024;
+#ifndef MPPI_COLFIN_FENCED
+#define MPPI_COLFIN_FENCED 0  // 1: release / acquire at agent scope around the column-split handoff
+#endif
 constexpr int FIN_LDS_NODES = 16;
 constexpr int FIN_GROUP_CHUNK = 64;    // groups per scale-table fill (15 PairScale + 16 m each)
 
@@ -2440,13 +2512,24 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
     __syncthreads();
     int* flag = reinterpret_cast<int*>(mlev);
     if (tid == 0) {
+#if MPPI_COLFIN_FENCED
+      // HIP memory model: the workgroup's u_opt stores (ordered before this thread by the barrier)
+      // released at agent scope with the count; the last workgroup acquires before reading them
+      const unsigned prev = __hip_atomic_fetch_add(f.level1_cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#else
+      // the stores above are agent-scope atomics, written through the XCD's L2,
+      // and complete (vmcnt(0)) before the barrier, so a relaxed count suffices on gfx950
       const unsigned prev = __hip_atomic_fetch_add(f.level1_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
       const int last = prev == gridDim.x - 1;
       if (last) __hip_atomic_store(f.level1_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
       flag[0] = last;
     }
     __syncthreads();
     if (!flag[0]) return;
+#if MPPI_COLFIN_FENCED
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -11,8 +11,8 @@ timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/py
 echo "pytest exit=$?" >> $OUT/pytest_$TAG.log
 timeout -k 10 300 python bench.py --steps 200 --warmup 20 --cpu-baseline-seconds ${CPU_S:-0} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || exit 1
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o r01 --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 5 --cpu-baseline-seconds 0 --no-c5 --no-bilinear --no-costmap > /dev/null 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o r02 --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 5 --cpu-baseline-seconds 0 --no-c4 --no-c5 --no-bilinear --no-costmap > /dev/null 2>&1
 cd $GRAFT_REPO_ROOT
 tail -3 $OUT/pytest_$TAG.log
 cut -c1-400 $OUT/bench_$TAG.json
-cat $OUT/prof_$TAG/r01_kernel_stats.csv
+cat $OUT/prof_$TAG/r02_kernel_stats.csv

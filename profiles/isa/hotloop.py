@@ -43,7 +43,7 @@ def main():
         if piece:
             sub.append(piece)
         for ins in sub:
-            if any(x.startswith("s_sleep") for x in ins) or any("v_div_scale" in x for x in ins):
+            if any(x.startswith("s_sleep") for x in ins) or any(("v_div_scale" in x or "v_cmp_class" in x) for x in ins):
                 continue
             for x in ins:
                 op = x.split()[0]

@@ -6,6 +6,8 @@ Each toggle below changes only WHERE or WHEN work runs, never the arithmetic:
   MPPI_UCACHE=0     leaf reduction re-reads every normals row instead of the LDS-cached controls
   MPPI_NOISE_AT=1/2 noise of the steps ahead launched after the finish / beside the rollout
   MPPI_NOISE_AHEAD=1  normals generated one step ahead instead of two
+  MPPI_ROLES=0/1    the pair rollout kernel / the role-split one at any K
+  MPPI_NOISE_GPC=1  noise grid of one workgroup per CU
 The toggles are read when a context is created, so each variant gets its own engine.
 Sizes: n = 256 leaf records (C3 K) and n = 1024 (C5 K) at a short horizon.
 """
@@ -51,9 +53,10 @@ def _run(env, K, H, steps=3, info=None):
 
 @pytest.mark.parametrize("K,H", [(65536, 24), (262144, 16)])
 @pytest.mark.parametrize("env", [{"MPPI_COLFIN": "0"}, {"MPPI_UCACHE": "0"}, {"MPPI_NOISE_AT": "1"},
-                                 {"MPPI_NOISE_AT": "2"}, {"MPPI_NOISE_AHEAD": "1"}],
+                                 {"MPPI_NOISE_AT": "2"}, {"MPPI_NOISE_AHEAD": "1"}, {"MPPI_ROLES": "0"},
+                                 {"MPPI_ROLES": "1"}, {"MPPI_NOISE_GPC": "1"}],
                          ids=["record-tree", "no-ucache", "noise-after-finish", "noise-beside-rollout",
-                              "noise-one-ahead"])
+                              "noise-one-ahead", "pair-kernel", "role-split-kernel", "noise-1-per-cu"])
 def test_variant_bitwise_equal(K, H, env):
     ref, ref_costs = _run({}, K, H)
     got, got_costs = _run(env, K, H)

@@ -16,6 +16,15 @@ TOL = 1e-5
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["roles", "pair"])
+def rollout_kernel(request, monkeypatch):
+    """Every parity case runs on both rollout kernels: the role-split one (the default at one
+    workgroup per CU) and the pair kernel (the default at larger K), forced by MPPI_ROLES, which
+    a context reads when it is created."""
+    monkeypatch.setenv("MPPI_ROLES", "1" if request.param == "roles" else "0")
+    return request.param
+
+
 def _run_both(K, H, seed, st, proj="3d", step=0, nominal=None, scene=None, **pkw):
     Z, hw, cm = scene if scene is not None else hp.c3_scene()
     p = R.Params(K=K, H=H, seed=seed, **pkw)
