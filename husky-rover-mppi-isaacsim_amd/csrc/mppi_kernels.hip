@@ -2935,6 +2935,9 @@ hipError_t launch_normal_table(const float* Z, int rows, int grid, float res, fl
   return hipGetLastError();
 }
 
+#ifndef MPPI_NOISE_WT
+#define MPPI_NOISE_WT 1
+#endif
 // The step's sampling normals (sampling_warp.py:54-92 with the Philox noise of
 // DEFINED D1), precomputed so the rollout's side waves only load them: thread =
 // (block, Philox block n = t/2, trajectory); writes eps1/eps2 of steps t, t+1.
@@ -2951,12 +2954,23 @@ __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t
     const int t = 2 * n;
     float* e1 = eps + ((size_t)blk * 2 * H + t) * 256 + tj;
     float* e2 = e1 + (size_t)H * 256;
+#if MPPI_NOISE_WT
+    // write-through (agent-scope, sc1) stores: the rows do not sit dirty in the XCD's L2, where the
+    // next kernel boundary on any stream would have to write them back
+    __hip_atomic_store(e1, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(e2, a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t + 1 < H) {
+      __hip_atomic_store(e1 + 256, b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(e2 + 256, b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#else
     e1[0] = a1;
     e2[0] = a2;
     if (t + 1 < H) {
       e1[256] = b1;
       e2[256] = b2;
     }
+#endif
   }
 }
 
