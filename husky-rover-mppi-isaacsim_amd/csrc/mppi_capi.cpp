@@ -3,7 +3,9 @@
 // Host arithmetic that feeds the kernels (path-follow branch, intermediate
 // goal, window bounds) is float32 in the reference's operation order; this
 // file is compiled with -ffp-contract=off like the kernels.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: RCCL is opened with dlopen by mppi_group_create
 
 #include <algorithm>
 #include <chrono>
@@ -1623,6 +1625,228 @@ int mppi_rollout_python25d(mppi_ctx* c, int64_t n, int32_t H, const double* x0, 
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   hipFree(buf);
   if (e != hipSuccess) return fail(MPPI_EHIP, std::string("python25d: ") + hipGetErrorString(e));
+  return MPPI_OK;
+}
+
+// ---- multi-GPU group in one process ----
+// One context per member device over a contiguous, leaf-aligned shard of the global K (as
+// mppi_amd/distributed.shard_bounds), Philox keyed by the global index; per step every member
+// runs its partial step (rollout + its record), the records are all-gathered (RCCL, one
+// ncclAllGather per member inside one group call, on the members' streams; members sharing a
+// device exchange by device copies), and every member combines them in member order and runs the
+// finish (identical controls everywhere; member 0's outputs are returned).
+}  // extern "C"
+
+namespace {
+struct RcclApi {
+  void* h = nullptr;
+  ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+};
+// RCCL from the process (torch may already hold one) or librccl.so.1; nullptr if unavailable
+const RcclApi* rccl_api(std::string& why) {
+  static RcclApi api;
+  static bool tried = false;
+  static std::string err;
+  if (!tried) {
+    tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      err = std::string("RCCL not found: ") + dlerror();
+    } else {
+      api.h = h;
+      api.comm_init_all = reinterpret_cast<decltype(api.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+      api.comm_destroy = reinterpret_cast<decltype(api.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+      api.all_gather = reinterpret_cast<decltype(api.all_gather)>(dlsym(h, "ncclAllGather"));
+      api.group_start = reinterpret_cast<decltype(api.group_start)>(dlsym(h, "ncclGroupStart"));
+      api.group_end = reinterpret_cast<decltype(api.group_end)>(dlsym(h, "ncclGroupEnd"));
+      api.error_string = reinterpret_cast<decltype(api.error_string)>(dlsym(h, "ncclGetErrorString"));
+      if (!api.comm_init_all || !api.comm_destroy || !api.all_gather || !api.group_start || !api.group_end)
+        err = "RCCL lacks ncclCommInitAll / ncclAllGather / ncclGroupStart";
+    }
+  }
+  why = err;
+  return err.empty() ? &api : nullptr;
+}
+}  // namespace
+
+struct mppi_group {
+  int n = 0, E = 0;
+  std::vector<mppi_ctx*> ctx;
+  std::vector<int> dev;
+  std::vector<int64_t> begin, count;
+  std::vector<double*> rec;       // [E] this member's record (its device)
+  std::vector<double*> gathered;  // [n * E] every member's record, member order (its device)
+  std::vector<hipEvent_t> ev;     // copy exchange: this member's record is ready
+  std::vector<double> empty_rec;  // the empty record (m = +inf, S = V = 0) for empty shards
+  bool use_rccl = false;
+  std::vector<ncclComm_t> comm;
+};
+
+extern "C" {
+
+int mppi_group_create(const mppi_params* params, int32_t n, const int32_t* devices, mppi_group** out) {
+  if (!params || !devices || !out || n < 1) return fail(MPPI_EINVAL, "group: null argument or n < 1");
+  *out = nullptr;
+  const int64_t K = params->num_trajectories;
+  if (K < 1) return fail(MPPI_EINVAL, "group: num_trajectories must be >= 1");
+  auto* g = new mppi_group();
+  g->n = n;
+  g->E = 2 * params->num_iterations + 2;
+  const int64_t leaves = (K + 255) / 256, per = (leaves + n - 1) / n;
+  bool distinct = true;
+  for (int i = 0; i < n; ++i) {
+    const int64_t b = std::min<int64_t>(K, (int64_t)i * per * 256), e = std::min<int64_t>(K, (int64_t)(i + 1) * per * 256);
+    g->begin.push_back(b);
+    g->count.push_back(e - b);
+    g->dev.push_back(devices[i]);
+    for (int j = 0; j < i; ++j) distinct &= devices[j] != devices[i];
+  }
+  auto bail = [&](int rc) {
+    mppi_group_destroy(g);
+    return rc;
+  };
+  for (int i = 0; i < n; ++i) {
+    mppi_params p = *params;
+    p.num_trajectories = g->count[i] > 0 ? g->count[i] : 256;  // an empty shard's context serves the finish
+    p.k_offset = params->k_offset + g->begin[i];
+    mppi_ctx* c = nullptr;
+    int rc = mppi_create(&p, devices[i], &c);
+    if (rc) return bail(rc);
+    g->ctx.push_back(c);
+    double *r = nullptr, *ga = nullptr;
+    hipEvent_t e = nullptr;
+    if (hipSetDevice(devices[i]) != hipSuccess || hipMalloc(&r, (size_t)g->E * sizeof(double)) != hipSuccess ||
+        hipMalloc(&ga, (size_t)n * g->E * sizeof(double)) != hipSuccess ||
+        hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      if (r) hipFree(r);
+      if (ga) hipFree(ga);
+      return bail(fail(MPPI_EHIP, "group: device buffers"));
+    }
+    g->rec.push_back(r);
+    g->gathered.push_back(ga);
+    g->ev.push_back(e);
+  }
+  g->empty_rec.assign((size_t)g->E, 0.0);
+  g->empty_rec[0] = INFINITY;
+  // MPPI_GROUP_RCCL: unset = RCCL between distinct devices (n > 1); 1 = also for one member
+  // (exercises the RCCL exchange on a 1-GPU host); 0 = device copies only
+  const char* env = std::getenv("MPPI_GROUP_RCCL");
+  const int force = env ? std::atoi(env) : -1;
+  if (distinct && ((n > 1 && force != 0) || force == 1)) {
+    std::string why;
+    const RcclApi* api = rccl_api(why);
+    if (!api) return bail(fail(MPPI_EHIP, "group: " + why));
+    g->comm.assign(n, nullptr);
+    const ncclResult_t r = api->comm_init_all(g->comm.data(), n, g->dev.data());
+    if (r != ncclSuccess) {
+      g->comm.clear();
+      return bail(fail(MPPI_EHIP, std::string("group: ncclCommInitAll: ") +
+                                      (api->error_string ? api->error_string(r) : "error")));
+    }
+    g->use_rccl = true;
+  }
+  *out = g;
+  return MPPI_OK;
+}
+
+void mppi_group_destroy(mppi_group* g) {
+  if (!g) return;
+  std::string why;
+  const RcclApi* api = g->comm.empty() ? nullptr : rccl_api(why);
+  for (size_t i = 0; i < g->comm.size(); ++i)
+    if (g->comm[i] && api) api->comm_destroy(g->comm[i]);
+  for (size_t i = 0; i < g->ctx.size(); ++i) {
+    hipSetDevice(g->dev[i]);
+    if (i < g->rec.size() && g->rec[i]) hipFree(g->rec[i]);
+    if (i < g->gathered.size() && g->gathered[i]) hipFree(g->gathered[i]);
+    if (i < g->ev.size() && g->ev[i]) hipEventDestroy(g->ev[i]);
+    mppi_destroy(g->ctx[i]);
+  }
+  delete g;
+}
+
+int mppi_group_size(mppi_group* g) { return g ? g->n : -1; }
+
+int mppi_group_context(mppi_group* g, int32_t i, mppi_ctx** out) {
+  if (!g || !out || i < 0 || i >= g->n) return fail(MPPI_EINVAL, "group: bad member index");
+  *out = g->ctx[i];
+  return MPPI_OK;
+}
+
+int mppi_group_shard(mppi_group* g, int32_t i, int64_t* begin, int64_t* count) {
+  if (!g || i < 0 || i >= g->n) return fail(MPPI_EINVAL, "group: bad member index");
+  if (begin) *begin = g->begin[i];
+  if (count) *count = g->count[i];
+  return MPPI_OK;
+}
+
+int mppi_group_step(mppi_group* g, int32_t proj, uint64_t step, mppi_outputs* out) {
+  if (!g) return fail(MPPI_EINVAL, "null group");
+  if (g->n == 1 && !g->use_rccl) return mppi_step(g->ctx[0], proj, step, out);
+  const int n = g->n;
+  const size_t bytes = (size_t)g->E * sizeof(double);
+  for (int i = 0; i < n; ++i) {
+    const int rc = check_ready(g->ctx[i]);  // every member (an empty one runs the finish) needs its scene
+    if (rc) return rc;
+  }
+  // 1. every member's rollout and record, on its own stream
+  for (int i = 0; i < n; ++i) {
+    mppi_ctx* c = g->ctx[i];
+    HIP_TRY(hipSetDevice(g->dev[i]));
+    if (g->count[i] > 0) {
+      const int rc = mppi_step_partial(c, proj, step, g->rec[i]);
+      if (rc) return rc;
+    } else {
+      HIP_TRY(hipMemcpyAsync(g->rec[i], g->empty_rec.data(), bytes, hipMemcpyHostToDevice, c->stream));
+    }
+  }
+  // 2. the exchange
+  if (g->use_rccl) {
+    std::string why;
+    const RcclApi* api = rccl_api(why);
+    if (!api) return fail(MPPI_EHIP, "group: " + why);
+    ncclResult_t r = api->group_start();
+    for (int i = 0; i < n && r == ncclSuccess; ++i)
+      r = api->all_gather(g->rec[i], g->gathered[i], (size_t)g->E, ncclFloat64, g->comm[i], g->ctx[i]->stream);
+    const ncclResult_t r2 = api->group_end();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      return fail(MPPI_EHIP, std::string("group: ncclAllGather: ") +
+                                 (api->error_string ? api->error_string(r != ncclSuccess ? r : r2) : "error"));
+  } else {
+    for (int i = 0; i < n; ++i) {
+      HIP_TRY(hipSetDevice(g->dev[i]));
+      HIP_TRY(hipEventRecord(g->ev[i], g->ctx[i]->stream));
+    }
+    for (int i = 0; i < n; ++i) {
+      HIP_TRY(hipSetDevice(g->dev[i]));
+      for (int j = 0; j < n; ++j) {
+        HIP_TRY(hipStreamWaitEvent(g->ctx[i]->stream, g->ev[j], 0));
+        HIP_TRY(hipMemcpyPeerAsync(g->gathered[i] + (size_t)j * g->E, g->dev[i], g->rec[j], g->dev[j], bytes,
+                                   g->ctx[i]->stream));
+      }
+    }
+  }
+  // 3. every member combines the records in member order and runs the finish; then the outputs
+  for (int i = 0; i < n; ++i) {
+    mppi_ctx* c = g->ctx[i];
+    HIP_TRY(hipSetDevice(g->dev[i]));
+    const Plan pl = c->have_last ? c->last_plan : make_plan(c);
+    int rc = enqueue_finish(c, pl, c->st, g->gathered[i], n, 1, nullptr, true);
+    if (rc) return rc;
+    rc = flush_speculation(c);
+    if (rc) return rc;
+  }
+  for (int i = 0; i < n; ++i) {
+    HIP_TRY(hipSetDevice(g->dev[i]));
+    const int rc = copy_outputs(g->ctx[i], i == 0 ? out : nullptr);
+    if (rc) return rc;
+  }
   return MPPI_OK;
 }
 

@@ -105,6 +105,13 @@ _PROTOS = {
     "mppi_costmap_builder_build": (C.c_int, [C.c_void_p, _DP, C.c_int32, C.c_int32, C.c_double, C.c_double,
                                              C.c_double, C.c_double, C.c_int32, _FP, C.c_void_p, C.c_int32]),
     "mppi_costmap_builder_last_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
+    "mppi_group_create": (C.c_int, [C.POINTER(MppiParams), C.c_int32, C.POINTER(C.c_int32),
+                                    C.POINTER(C.c_void_p)]),
+    "mppi_group_destroy": (None, [C.c_void_p]),
+    "mppi_group_size": (C.c_int, [C.c_void_p]),
+    "mppi_group_context": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
+    "mppi_group_shard": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "mppi_group_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.POINTER(MppiOutputs)]),
     "mppi_rollout_python25d": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, _DP, _DP, _DP, _DP, _DP, C.c_double,
                                          C.c_double, C.c_double, C.c_double, _DP, C.POINTER(C.c_int32)]),
 }
@@ -253,14 +260,18 @@ class Engine:
     OUT_NAMES = ("u1_opt", "u2_opt", "lin_vel", "ang_vel", "traj_sim", "heading_sim",
                  "left_wheel_sim", "right_wheel_sim")
 
-    def __init__(self, params: MppiParams, device: int = 0):
+    def __init__(self, params: MppiParams, device: int = 0, _ctx=None):
         self.lib = load_library()
         self.params = params
         self.H = int(params.num_iterations)
         self.K = int(params.num_trajectories)
         self.device = int(device)
-        ctx = C.c_void_p()
-        _check(self.lib, self.lib.mppi_create(C.byref(params), self.device, C.byref(ctx)), "mppi_create")
+        self._owned = _ctx is None
+        if _ctx is None:
+            ctx = C.c_void_p()
+            _check(self.lib, self.lib.mppi_create(C.byref(params), self.device, C.byref(ctx)), "mppi_create")
+        else:
+            ctx = _ctx   # a group member: the group destroys it
         self.ctx = ctx
         H = self.H
         self._buf = {n: np.zeros(3 * H if n.endswith("_sim") else H, np.float32) for n in self.OUT_NAMES}
@@ -271,7 +282,8 @@ class Engine:
     # ------------------------------------------------------------ lifetime
     def close(self):
         if getattr(self, "ctx", None) and self.ctx.value:
-            self.lib.mppi_destroy(self.ctx)
+            if getattr(self, "_owned", True):
+                self.lib.mppi_destroy(self.ctx)
             self.ctx = C.c_void_p()
 
     def __del__(self):
@@ -474,3 +486,80 @@ class Engine:
     def bilinear_query(self, x_ptr, y_ptr, h_ptr, n):
         self._c(self.lib.mppi_bilinear_query(self.ctx, C.c_void_p(int(x_ptr)), C.c_void_p(int(y_ptr)),
                                              C.c_void_p(int(h_ptr)), int(n)), "mppi_bilinear_query")
+
+
+class Group:
+    """mppi_group (include/mppi.h): one controller over n GPUs from one process.
+
+    Member i is an Engine over the contiguous shard mppi_group_shard(i) of the K trajectories;
+    setters broadcast to every member; step() enqueues every member's rollout, all-gathers the
+    records (RCCL between distinct devices, device copies when members share one) and returns the
+    outputs, bitwise equal to one context over all K.
+    """
+
+    def __init__(self, params: MppiParams, devices):
+        self.lib = load_library()
+        self.params = params
+        self.H = int(params.num_iterations)
+        self.K = int(params.num_trajectories)
+        devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+        h = C.c_void_p()
+        _check(self.lib, self.lib.mppi_group_create(C.byref(params), len(devices), devs, C.byref(h)),
+               "mppi_group_create")
+        self.h = h
+        self.members = []
+        for i, d in enumerate(devices):
+            ctx = C.c_void_p()
+            _check(self.lib, self.lib.mppi_group_context(h, i, C.byref(ctx)), "mppi_group_context")
+            b, n = self.shard(i)
+            p = MppiParams.from_buffer_copy(params)
+            p.num_trajectories = n if n > 0 else 256
+            p.k_offset = int(params.k_offset) + b
+            self.members.append(Engine(p, d, _ctx=ctx))
+
+    def shard(self, i):
+        b, n = C.c_int64(), C.c_int64()
+        _check(self.lib, self.lib.mppi_group_shard(self.h, int(i), C.byref(b), C.byref(n)), "mppi_group_shard")
+        return b.value, n.value
+
+    def __len__(self):
+        return len(self.members)
+
+    def _each(self, name, *a, **kw):
+        for m in self.members:
+            getattr(m, name)(*a, **kw)
+
+    def set_dem(self, *a, **kw):
+        self._each("set_dem", *a, **kw)
+
+    def set_costmap(self, *a, **kw):
+        self._each("set_costmap", *a, **kw)
+
+    def set_state(self, state: MppiState):
+        self._each("set_state", state)
+
+    def set_nominal(self, u1, u2):
+        self._each("set_nominal", u1, u2)
+
+    def step(self, proj="3d", step=0, copy=True):
+        m0 = self.members[0]
+        _check(self.lib, self.lib.mppi_group_step(self.h, PROJ[proj], int(step), C.byref(m0._out)),
+               "mppi_group_step")
+        return m0._outputs() if copy else None
+
+    def costs(self):
+        """Every trajectory's cost in global order (the members' shards concatenated)."""
+        return np.concatenate([m.costs()[:self.shard(i)[1]] for i, m in enumerate(self.members)])
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            for m in self.members:
+                m.close()
+            self.lib.mppi_group_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

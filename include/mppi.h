@@ -215,6 +215,30 @@ int mppi_step_partial(mppi_ctx* ctx, int32_t proj, uint64_t step, double* record
 int mppi_step_finish(mppi_ctx* ctx, const double* records_dev, int32_t n_records,
                      mppi_outputs* out);
 
+/* ---- the same sharded step driven from ONE process ----
+ * For a host that owns several GPUs in one process (the reference's
+ * controller object, MPPI_isaac.py:397-470, is single-process; a caller that
+ * wants one controller over n GPUs without torch.distributed).  The group
+ * holds one context per member device, member i over trajectories
+ * [begin_i, begin_i + count_i) of params->num_trajectories (256-trajectory
+ * leaves split contiguously, as mppi_amd/distributed.shard_bounds), noise
+ * keyed by the global trajectory index, so a group step is bitwise equal to
+ * one context over all K.  mppi_group_step enqueues every member's rollout and
+ * record, all-gathers the records (RCCL ncclAllGather in one group call, RCCL
+ * opened with dlopen when the devices are distinct; device-to-device copies
+ * when members share a device), runs every member's finish and returns member
+ * 0's outputs; every member keeps the same nominal controls.  Scene, state,
+ * weights and warm starts are set on each member through mppi_group_context
+ * with the single-context calls above. */
+typedef struct mppi_group mppi_group;
+int mppi_group_create(const mppi_params* params, int32_t n, const int32_t* devices,
+                      mppi_group** out);
+void mppi_group_destroy(mppi_group* group);
+int mppi_group_size(mppi_group* group);
+int mppi_group_context(mppi_group* group, int32_t member, mppi_ctx** out);
+int mppi_group_shard(mppi_group* group, int32_t member, int64_t* begin, int64_t* count);
+int mppi_group_step(mppi_group* group, int32_t proj, uint64_t step, mppi_outputs* out);
+
 /* ---- introspection (self.costs_wp / self.trajectories .numpy(), MPPI_isaac.py:466-470) ---- */
 /* costs of the last step's trajectories of this context [n <= K] */
 int mppi_get_costs(mppi_ctx* ctx, float* costs_host, int64_t n);
