@@ -1919,6 +1919,109 @@ __device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>
   return s;
 }
 
+// The optimal rollout's serial chain (projection_warp.py:306-326 on one trajectory) on one
+// whole wave, every lane computing the same values: a lone lane waits out each step's
+// normal-table load (L2 / MALL latency, about half of a step).  Instead each step's normal comes
+// from the 8 x 8-cell neighbourhood of the position two steps earlier, loaded one cell per lane
+// while those two steps run, and is read from the lane holding it (v_readlane); a position more
+// than 3 cells from that centre loads its entry directly.  Arithmetic as the rollout chain
+// (advance_step / orient_step, correctly rounded, IEEE redo out of range), so every value is
+// chain3d_lean's.  Writes x, y (0, 1), n (6..8) and the new heading (9..11) of each step into
+// chain[12 t ..] (lane 0).
+constexpr int TAIL_WIN = 8, TAIL_WIN_LO = 3;  // neighbourhood cells [c - 3, c + 4] per axis
+__device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem<false>& dem, const float* vb,
+                                              const float* snb, const float* csb, float* chain, int H, int lane) {
+  const f2 cell_off = f2{-f.x_min, f.y_min};
+  const float fi_hi = (float)(f.grid - 1), fj_lo = (float)(1 - f.rows);
+  const float4* ntab0 = dem.N + (f.grid + 2);  // entry (jj, ii) = (1 - tjj, ti + 1): offset ti - tjj * (grid + 1)
+  const int nrow = f.grid + 1;
+  const int ldx = (lane % TAIL_WIN) - TAIL_WIN_LO, ldy = (lane / TAIL_WIN) - TAIL_WIN_LO;
+  // (ti, tjj) of the cell holding pos: min(i, grid - 1), -min(j, rows - 1) (Dem::cell)
+  auto cell_of = [&](f2 pos, int& ti, int& tjj) __attribute__((always_inline)) {
+    f2 q;
+    if (dem.cdiv) {
+      const f2 aa = pos + cell_off;
+      const f2 q0 = aa * bc2(dem.rinv);
+      const f2 r = pk_fma(-q0, bc2(dem.res), aa);
+      q = pk_fma(r, bc2(dem.rinv), q0);
+    } else {
+      q = f2{(pos.x - f.x_min) / f.res, (pos.y + f.y_min) / f.res};
+    }
+    ti = (int)__builtin_amdgcn_fmed3f(q.x, -1.0f, fi_hi);
+    tjj = (int)__builtin_amdgcn_fmed3f(q.y, fj_lo, 1.0f);
+  };
+  // this lane's cell of the neighbourhood centred on (ti, tjj): its table offset, load issued
+  auto issue = [&](int ti, int tjj, int& lo, float4& w) __attribute__((always_inline)) {
+    const int ci = min(max(ti + ldx, -1), f.grid - 1);
+    const int cj = min(max(tjj + ldy, 1 - f.rows), 1);
+    lo = ci - cj * nrow;
+    w = ntab0[lo];
+  };
+  // the normal of (ti, tjj) from the neighbourhood centred on (cti, ctjj)
+  auto pick = [&](int ti, int tjj, int cti, int ctjj, int lo, const float4& w) __attribute__((always_inline)) {
+    const int to = ti - tjj * nrow;
+    const int dx = ti - cti + TAIL_WIN_LO, dy = tjj - ctjj + TAIL_WIN_LO;
+    const int src = __builtin_amdgcn_readfirstlane(dy * TAIL_WIN + dx);
+    const bool in = ((unsigned)dx < (unsigned)TAIL_WIN) & ((unsigned)dy < (unsigned)TAIL_WIN);
+    float3 n;
+    if (in && __builtin_amdgcn_readlane(lo, src & 63) == to) {
+      n.x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w.x), src & 63));
+      n.y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w.y), src & 63));
+      n.z = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w.z), src & 63));
+    } else {
+      const float4 d = ntab0[to];
+      n = make_float3(d.x, d.y, d.z);
+    }
+    return n;
+  };
+  const Traj s0 = initial_pose(f, dem);
+  Head hd{f2{s0.hx, s0.hy}, s0.hz};
+  f2 pos = f2{s0.x, s0.y};
+  int tiA, tjjA, tiB, tjjB, loA, loB;
+  float4 wA, wB;
+  cell_of(pos, tiA, tjjA);  // the neighbourhoods of steps 0 and 1: around the start
+  tiB = tiA;
+  tjjB = tjjA;
+  issue(tiA, tjjA, loA, wA);
+  loB = loA;
+  wB = wA;
+  // step t: position, normal from neighbourhood X (centred two steps back), refill X around
+  // this step's cell for step t + 2, orientation, record
+  auto step = [&](int t, int& ctiX, int& ctjjX, int& loX, float4& wX) __attribute__((always_inline)) {
+    const float v = vb[t], sn = snb[t], cs = csb[t];
+    Lean la;
+    lean_init(la);
+    f2 p = advance_step<true>(hd, v, f.dt, pos, la);
+    if (__builtin_expect(lean_bad(la), 0)) p = advance_step<false>(hd, v, f.dt, pos, la);
+    pos = p;
+    int ti, tjj;
+    cell_of(pos, ti, tjj);
+    const float3 n = pick(ti, tjj, ctiX, ctjjX, loX, wX);
+    ctiX = ti;
+    ctjjX = tjj;
+    issue(ti, tjj, loX, wX);
+    const float omc = 1.0f - cs;
+    const f2 nxy = f2{n.x, n.y};
+    Lean l;
+    lean_init(l);
+    Head ho = orient_step<true>(nxy, n.z, hd, sn, cs, omc, l);
+    if (__builtin_expect(lean_bad(l), 0)) ho = orient_step<false>(nxy, n.z, hd, sn, cs, omc, l);
+    hd = ho;
+    if (lane == 0) {
+      float* ch = chain + 12 * t;
+      ch[0] = pos.x; ch[1] = pos.y;
+      ch[6] = n.x; ch[7] = n.y; ch[8] = n.z;
+      ch[9] = ho.xy.x; ch[10] = ho.xy.y; ch[11] = ho.z;
+    }
+  };
+  int t = 0;
+  for (; t + 1 < H; t += 2) {
+    step(t, tiA, tjjA, loA, wA);
+    step(t + 1, tiB, tjjB, loB, wB);
+  }
+  if (t < H) step(t, tiA, tjjA, loA, wA);
+}
+
 // Step 0 of the optimal rollout on one lane (no barrier): traj | hv | lw | rw of the
 // first step into out[0..12), the layout optimal_rollout uses for nsteps = 1.
 template <bool LDS>
@@ -1954,7 +2057,9 @@ __device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem<L
                                                 int nsteps, float* out, int tid, int nthreads) {
   const float res_half_neg = (-f.res) / 2.0f;
   const float res_sq = f.res * f.res;
-  if (tid == 0) {  // the serial chain (projection_warp.py:306-326)
+  if constexpr (!LDS && MPPI_LEAN_CHAIN) {  // the serial chain on wave 0 (tail_chain_3d)
+    if (tid < 64) tail_chain_3d(f, dem, vb, snb, csb, chain, nsteps, tid);
+  } else if (tid == 0) {  // the serial chain (projection_warp.py:306-326)
     Traj s = initial_pose(f, dem);
     float vn = vb[0], sn_n = snb[0], cs_n = csb[0];
     for (int t = 0; t < nsteps; ++t) {
