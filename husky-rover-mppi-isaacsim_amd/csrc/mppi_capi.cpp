@@ -42,6 +42,9 @@ int fail(int code, const std::string& msg) {
 
 constexpr size_t kLdsBytes = 160 * 1024;
 constexpr int kEpsSlots = 3;
+// deferred optimal rollouts in flight: the tail of step i may run until the finish of step i + 3
+// is enqueued (beside the next rollout it gets only the issue slots the rollout waves leave)
+constexpr int kTailSlots = 3;
 
 struct Plan {
   int traj_per_block = 256;
@@ -135,6 +138,10 @@ struct mppi_ctx {
   long tr_n = 0;
   int wave_prio = 1;  // rollout waves raise their issue priority (env MPPI_WAVE_PRIO=0: off)
   int roles = -1;     // rollout kernel: -1 auto (role split at <= 1 workgroup per CU), 0 pair, 1 roles (MPPI_ROLES)
+  int fused = 1;               // one launch per step (mppi_step_fused_kernel): 0 never, 1 synchronous steps,
+                               // 2 also with the deferred optimal rollout (MPPI_FUSED)
+  int fused_noise_groups = -1; // noise of step + 2 in the launch: -1 one workgroup per CU the finish leaves,
+                               // n > 0 n workgroups, 0 before the launch on the context stream (MPPI_FUSED_NOISE_GROUPS)
   int noise_gpc = 0;  // noise kernel workgroups per CU: 0 auto (2 beside the role split, else 4) (MPPI_NOISE_GPC)
   hipEvent_t ev_roll_done = nullptr;
   hipEvent_t ev_prev_roll = nullptr;  // recorded after the last rollout that read an eps slot
@@ -160,12 +167,12 @@ struct mppi_ctx {
   bool async_tail = false;
   hipStream_t tail_stream = nullptr;
   hipEvent_t ev_fin_done = nullptr;
-  hipEvent_t ev_tail[2] = {nullptr, nullptr};  // per parity: tail done
+  hipEvent_t ev_tail[kTailSlots] = {};  // per slot: tail done
   bool tail_pending = false;       // the latest tail's outputs are not merged into out_host yet
-  bool tail_inflight[2] = {false, false};  // the tail of that parity may still run
-  int tail_par = 0;                // parity of the latest tail
-  float* tail_in[2] = {nullptr, nullptr};    // device [3H] per parity
-  float* tail_host[2] = {nullptr, nullptr};  // pinned [12H] per parity (written by the kernel)
+  bool tail_inflight[kTailSlots] = {};  // the tail of that slot may still run
+  int tail_par = 0;                // slot of the latest tail
+  float* tail_in[kTailSlots] = {};    // device [3H] per slot
+  float* tail_host[kTailSlots] = {};  // pinned [12H] per slot (written by the kernel)
   // timing
   bool timing = false;
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -452,10 +459,12 @@ void collect_tail_timing(mppi_ctx* c) {
 // Wait until no deferred optimal rollout can still read tail_in or the DEM, and
 // merge the latest one's outputs into out_host[4H, 16H).
 int sync_tail(mppi_ctx* c) {
-  if (!c->tail_inflight[0] && !c->tail_inflight[1] && !c->tail_pending) return MPPI_OK;
+  bool any = c->tail_pending;
+  for (int i = 0; i < kTailSlots; ++i) any |= c->tail_inflight[i];
+  if (!any) return MPPI_OK;
   HIP_TRY(hipStreamSynchronize(c->tail_stream));
   collect_tail_timing(c);
-  c->tail_inflight[0] = c->tail_inflight[1] = false;
+  for (int i = 0; i < kTailSlots; ++i) c->tail_inflight[i] = false;
   if (c->tail_pending) {
     const int H = H_of(c);
     std::memcpy(c->out_host + 4 * H, c->tail_host[c->tail_par], (size_t)12 * H * sizeof(float));
@@ -668,7 +677,7 @@ int prepare_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, int mode, 
     f.done = c->done;
     f.seq = ++c->seq;
   }
-  par = c->tail_par ^ 1;
+  par = (c->tail_par + 1) % kTailSlots;
   if (mode == 2) {
     f.tail_in = c->tail_in[par];
     f.tail_out = c->tail_host[par];
@@ -825,19 +834,119 @@ void remember(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
   c->last_plan = pl;
 }
 
+// The fused step launch (mppi_step_fused_kernel): rollout, column-split finish and the noise of
+// step + noise_ahead in one kernel on the context stream.  Applies to sampled steps of the role-split
+// plan whose records fit the column-split finish and whose LDS fits one workgroup per CU.
+// By default only for synchronous steps (no deferred optimal rollout): there the finish (with the
+// ~50 us serial optimal rollout) covers the noise workgroups.  With the deferred tail the finish is
+// shorter than the noise (~25 us of the whole chip), which the three-launch schedule hides beside the
+// finish, the host round trip and the next rollout instead (measured: 8820 vs 8050 steps/s at C3).
+bool fused_shape(const mppi_ctx* c, const Plan& pl, int mode, int* P, int* ncol, int* groups, size_t* lds) {
+  if (!c->fused || (c->async_tail && c->fused < 2)) return false;
+  if (mode != 0 || !pl.roles || !c->colfin || c->noise_at != 0 || pl.blocks < 1) return false;
+  size_t cf_lds = 0;
+  if (!colfin_shape(pl.blocks, H_of(c), P, ncol, groups, &cf_lds)) return false;
+  *lds = std::max({pl.lds_bytes, cf_lds, pl.fin_lds_bytes});
+  return *lds <= 160 * 1024;
+}
+
+int enqueue_fused(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int ncol, int groups, size_t lds) {
+  if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
+  int rc = ensure_nodes(c, pl.blocks);
+  if (rc) return rc;
+  rc = flush_speculation(c);
+  if (rc) return rc;
+  int slot = -1;
+  rc = eps_for_step(c, pl, step, &slot);
+  if (rc) return rc;
+  RolloutArgs a;
+  fill_rollout(c, pl, c->st, step, c->u_nom[c->cur], a);
+  a.wave_prio = c->wave_prio;
+  a.eps = c->eps[slot];
+  FusedArgs z;
+  std::memset(&z, 0, sizeof(z));
+  // normals of steps step + 1 .. step + noise_ahead.  Steady state: the farthest (step + 2) inside
+  // the launch, on the CUs the rollout releases, beside the finish (MPPI_FUSED_NOISE_GROUPS = 0:
+  // before the launch on the context stream).  Any other missing step (first steps, a jump of the
+  // step counter) is generated before the launch on the context stream.
+  const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
+  for (int d = 1; d <= c->noise_ahead; ++d) {
+    const uint64_t target = step + (uint64_t)d;
+    bool have = false;
+    for (int i = 0; i < kEpsSlots; ++i) have |= c->eps_step[i] == (int64_t)target;
+    if (have) continue;
+    const bool last = d == c->noise_ahead;
+    const int v = eps_victim(c, slot, step, c->noise_ahead);
+    if (v < 0) return fail(MPPI_ESTATE, "no free noise slot");
+    if (c->eps_pending[v]) {  // a stale speculation still writing the victim slot on the noise stream
+      HIP_TRY(hipStreamWaitEvent(c->stream, c->eps_ev[v], 0));
+      c->eps_pending[v] = false;
+    }
+    if (last && c->fused_noise_groups != 0) {
+      z.noise_eps = c->eps[v];
+      z.noise_n_base = target * nb;
+      z.noise_groups = c->fused_noise_groups > 0 ? c->fused_noise_groups : std::max(c->num_cus - groups, 1);
+    } else {
+      HIP_TRY(launch_noise(c->p.seed, target * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[v], c->stream,
+                           noise_groups(c, pl)));
+    }
+    c->eps_step[v] = (int64_t)target;
+  }
+  int par = 0;
+  rc = prepare_finish(c, pl, c->st, 1, nullptr, z.f, par);
+  if (rc) return rc;
+  z.f.recs = c->nodes;
+  z.f.n_recs = pl.blocks;
+  if (c->level1_cap < 1 || c->level1_cap * (size_t)E_of(c) < (size_t)E_of(c)) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->level1) HIP_TRY(hipFree(c->level1));
+    c->level1 = nullptr;
+    HIP_TRY(hipMalloc(&c->level1, (size_t)E_of(c) * sizeof(double)));
+    c->level1_cap = 1;
+  }
+  z.f.level1 = c->level1;
+  z.f.level1_cnt = c->level1_cnt;
+  z.nroll = pl.blocks;
+  z.fin_P = P;
+  z.fin_ncol = ncol;
+  z.fin_groups = groups;
+  z.rec_cnt = c->level1_cnt + 16;
+  c->fin_kind = 1;
+  c->fin_P = P;
+  c->fin_ncol = ncol;
+  c->fin_groups = groups;
+  if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  HIP_TRY(launch_step_fused(a, z, lds, c->stream, proj));
+  if (c->timing) {
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    c->ev_roll_pending = true;
+  }
+  if (z.f.mode == 2) return enqueue_tail(c, z.f, par);
+  return MPPI_OK;
+}
+
 int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out) {
   if (c && c->trace) c->tr_t0 = now_us();
   int rc = check_ready(c);
   if (rc) return rc;
   const Plan pl = make_plan(c);
-  rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr);
-  if (rc) return rc;
-  if (c->trace) c->tr_t1 = now_us();
-  remember(c, proj, step, mode, pl);
-  rc = enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 1, nullptr, true);
-  if (rc) return rc;
-  rc = flush_speculation(c);
-  if (rc) return rc;
+  int fP = 0, fcol = 0, fgroups = 0;
+  size_t flds = 0;
+  if (fused_shape(c, pl, mode, &fP, &fcol, &fgroups, &flds)) {
+    rc = enqueue_fused(c, proj, step, pl, fP, fcol, fgroups, flds);
+    if (rc) return rc;
+    if (c->trace) c->tr_t1 = now_us();
+    remember(c, proj, step, mode, pl);
+  } else {
+    rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr);
+    if (rc) return rc;
+    if (c->trace) c->tr_t1 = now_us();
+    remember(c, proj, step, mode, pl);
+    rc = enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 1, nullptr, true);
+    if (rc) return rc;
+    rc = flush_speculation(c);
+    if (rc) return rc;
+  }
   if (!c->trace) return copy_outputs(c, out);
   const double t2 = now_us();
   rc = copy_outputs(c, out);
@@ -990,6 +1099,8 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   if (const char* e = std::getenv("MPPI_WAVE_PRIO")) c->wave_prio = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_ROLES")) c->roles = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_NOISE_GPC")) c->noise_gpc = std::max(std::atoi(e), 0);
+  if (const char* e = std::getenv("MPPI_FUSED")) c->fused = std::min(std::max(std::atoi(e), 0), 2);
+  if (const char* e = std::getenv("MPPI_FUSED_NOISE_GROUPS")) c->fused_noise_groups = std::max(std::atoi(e), -1);
   const char* ep = std::getenv("MPPI_STREAM_PRIO");
   const bool use_prio = !(ep && std::atoi(ep) == 0);
   const int H = p.num_iterations;
@@ -1010,12 +1121,14 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipHostMalloc(&c->stage, 16 * H * sizeof(float), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&c->done, 64, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->cdiv_bad, sizeof(unsigned)) != hipSuccess ||
-      hipMalloc(&c->level1_cnt, sizeof(unsigned)) != hipSuccess ||
+      hipMalloc(&c->level1_cnt, 128) != hipSuccess ||  // [0]: finish handoff, [16]: fused record count
       hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->tail_in[1], 3 * H * sizeof(float)) != hipSuccess ||
+      hipMalloc(&c->tail_in[2], 3 * H * sizeof(float)) != hipSuccess ||
       hipHostMalloc(&c->tail_host[0], 12 * H * sizeof(float), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&c->tail_host[1], 12 * H * sizeof(float), hipHostMallocDefault) != hipSuccess)
+      hipHostMalloc(&c->tail_host[1], 12 * H * sizeof(float), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&c->tail_host[2], 12 * H * sizeof(float), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "device allocation failed"));
   if (hipMemset(c->u_nom[0], 0, 2 * H * sizeof(float)) != hipSuccess ||
       hipMemset(c->u_nom[1], 0, 2 * H * sizeof(float)) != hipSuccess ||
@@ -1026,6 +1139,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   if (hipEventCreateWithFlags(&c->ev_fin_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_tail[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_tail[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_tail[2], hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->tail_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithPriority(&c->noise_stream, hipStreamNonBlocking, c->prio_least) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_roll_done, hipEventDisableTiming) != hipSuccess ||
@@ -1037,7 +1151,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   c->out_host = new float[16 * H]();
   std::memset(c->stage, 0, 16 * H * sizeof(float));
   *c->done = 0;
-  if (hipMemset(c->level1_cnt, 0, sizeof(unsigned)) != hipSuccess)
+  if (hipMemset(c->level1_cnt, 0, 128) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
   if (hipDeviceSynchronize() != hipSuccess) return cleanup(fail(MPPI_EHIP, "device sync failed"));
   *out = c;
@@ -1074,7 +1188,7 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->done) hipHostFree(c->done);
   if (c->cdiv_bad) hipFree(c->cdiv_bad);
   delete[] c->out_host;
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kTailSlots; ++i) {
     if (c->tail_in[i]) hipFree(c->tail_in[i]);
     if (c->tail_host[i]) hipHostFree(c->tail_host[i]);
     if (c->ev_tail[i]) hipEventDestroy(c->ev_tail[i]);

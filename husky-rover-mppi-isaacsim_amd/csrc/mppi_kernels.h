@@ -112,6 +112,19 @@ hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hip
 // workgroup over 1024 threads, one wave per role (chain, producer, wheel, cost) and 64
 // trajectories; rings [D][4 + 4][TB] + cost[TB] + slope[TB] in LDS.
 constexpr int ROLES_WAVES_PER_TRAJ_WAVE = 4;
+// One launch per step (mppi_step_fused_kernel): the role-split rollout's nroll workgroups, then
+// fin_groups column-split finish workgroups (colfin_shape; they wait for rec_cnt == nroll, records
+// written through), then noise_groups workgroups generating the normals of Philox block base
+// noise_n_base into noise_eps (none when noise_groups == 0).  rec_cnt: zeroed, re-armed in-kernel.
+struct FusedArgs {
+  FinishArgs f;
+  int nroll, fin_P, fin_ncol, fin_groups;
+  unsigned* rec_cnt;
+  float* noise_eps;
+  uint64_t noise_n_base;
+  int noise_groups;
+};
+hipError_t launch_step_fused(const RolloutArgs& a, const FusedArgs& z, size_t lds, hipStream_t st, int proj);
 // record tree finish (mppi_finish_kernel): the fallback where the column-split shape does not fit
 hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, int groups = 1);
 // column-split finish: every workgroup builds the pair-scale table and reduces ncol columns

@@ -790,7 +790,7 @@ __device__ __forceinline__ double group_apply(const PairScale* ps, const double 
 // LDS row stride (floats) of the pair kernel's control cache: 256 trajectories + one float4 of
 // skew, so the leaf's lanes (one row each) hit different banks
 constexpr int UCACHE_ROW = 256 + 4;
-template <int TB, int NT, bool EPS = false>
+template <int TB, int NT, bool EPS = false, bool WT = false>
 __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
                                              unsigned char* scratch, const float* ub_block,
                                              const float* ucache = nullptr, int uc_steps = 0);
@@ -804,8 +804,9 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
 //   pairwise tree in index order ((x0+x1)+(x2+x3)) + ... (float64);
 // then the workgroup's subtree over its TB/256 leaves (tree_reduce order).
 // Called by all NT threads; `scratch` is LDS of at least
-// TB*4 + TB/64*4 (rounded to 16) + TB/256*(2H+2)*8 bytes.
-template <int TB, int NT, bool EPS>
+// TB*4 + TB/64*4 (rounded to 16) + TB/256*(2H+2)*8 bytes.  WT: the record is stored
+// write-through (agent-scope atomic stores) for the finish workgroups of a fused launch.
+template <int TB, int NT, bool EPS, bool WT>
 __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
                                              unsigned char* scratch, const float* ub_block,
                                              const float* ucache, int uc_steps) {
@@ -921,7 +922,10 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
         lm[q] = ps.m;
       }
     }
-    a.nodes[(size_t)blockIdx.x * E + j] = val[0];
+    if constexpr (WT)
+      __hip_atomic_store(a.nodes + (size_t)blockIdx.x * E + j, val[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      a.nodes[(size_t)blockIdx.x * E + j] = val[0];
   }
 }
 
@@ -1510,8 +1514,8 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 // Deadlock-free: no wave waits on a later step of a wave that waits on it.
 constexpr int ROLE_CHAIN = 0, ROLE_PROD = 1, ROLE_WHEEL = 2, ROLE_COST = 3, NROLES = 4;
 
-template <int TB, int PROJ, int MODE, bool DUMP>
-__global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const RolloutArgs a) {
+template <int TB, int PROJ, int MODE, bool DUMP, bool FUSED>
+__device__ __forceinline__ void roles_body(const RolloutArgs& a, unsigned* rec_cnt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   constexpr int NT = NROLES * TB;
   constexpr int NG = TB / 64;  // trajectory groups (waves per role)
@@ -1864,10 +1868,20 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const R
   }
   __syncthreads();
   if constexpr (MODE == 0)  // rows hold the normals; the leaf recomputes the sampled controls
-    leaf_records<TB, NT, true>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB, ucache,
-                               a.ucache_steps);
+    leaf_records<TB, NT, true, FUSED>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB, ucache,
+                                      a.ucache_steps);
   else
-    leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
+    leaf_records<TB, NT, false, FUSED>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
+  if constexpr (FUSED) {  // the record is written through: count it (D8: complete, then a relaxed count)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(rec_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <int TB, int PROJ, int MODE, bool DUMP>
+__global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const RolloutArgs a) {
+  roles_body<TB, PROJ, MODE, DUMP, false>(a, nullptr);
 }
 
 // =====================================================================  finish kernel
@@ -2499,13 +2513,26 @@ root_ready:
 constexpr int COLFIN_PMAX = 4096;  // leaf records (K <= 1,048,576 per context)
 __device__ __forceinline__ int colfin_level_base(int P, int l) { return P - (P >> l); }
 
-__global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishArgs f, int P, int ncol) {
+// Records written by this launch's own rollout blocks (fused launch, RECS_WT) are read with
+// agent-scope atomic loads: they bypass a stale line of the previous step's records in this XCD's
+// L2 (the rollout blocks store them write-through).
+template <bool RECS_WT>
+__device__ __forceinline__ double rec_load(const double* p) {
+  if constexpr (RECS_WT) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+
+// The column-split finish of workgroup `blk` of `nblk` (mppi_colfin_kernel, or the finish
+// workgroups of a fused launch, which also re-arm the fused launch's record counter).
+template <bool RECS_WT>
+__device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol, int blk, int nblk,
+                                            unsigned* rec_cnt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
 #if MPPI_FIN_PRIO
   __builtin_amdgcn_s_setprio(3);  // the serial step path outranks the next step's noise waves
 #endif
 #ifdef MPPI_STAMPS
-  if (blockIdx.x == 0) FIN_STAMP(0);
+  if (blk == 0) FIN_STAMP(0);
 #endif
   const int tid = threadIdx.x;
   const int H = f.H;
@@ -2516,7 +2543,7 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
   float* mlev = reinterpret_cast<float*>(lps + (P - 1));  // node minima, level l at 2P - (2P >> l)
   double* part = reinterpret_cast<double*>(mlev + 2 * P);  // [ncol + 1][P / 16], 8-byte aligned (P >= 16)
   // this workgroup's columns: [c0, c1) plus column 1 (S) as slot ncol when c0 > 1
-  const int c0 = (int)blockIdx.x * ncol;
+  const int c0 = blk * ncol;
   const int c1 = min(E, c0 + ncol);
   const int nc = c1 - c0;
   const bool extra_s = c0 > 1;
@@ -2533,10 +2560,11 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int r = min(16 * it_g + i, n - 1);
-      v[i] = recs[(size_t)r * E + col];
+      v[i] = rec_load<RECS_WT>(recs + (size_t)r * E + col);
     }
   }
-  for (int i = tid; i < P; i += FIN_THREADS) mlev[i] = (i < n) ? (float)recs[(size_t)i * E] : INFINITY;
+  for (int i = tid; i < P; i += FIN_THREADS)
+    mlev[i] = (i < n) ? (float)rec_load<RECS_WT>(recs + (size_t)i * E) : INFINITY;
   __syncthreads();
   // (2) pair scales: first the node minima level by level (one fminf per node, the m that
   //     pair_scale forms), then every node's pair scale in one pass, so the exponentials of
@@ -2557,7 +2585,7 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
   }
   __syncthreads();
 #ifdef MPPI_STAMPS
-  if (blockIdx.x == 0) FIN_STAMP(9);
+  if (blk == 0) FIN_STAMP(9);
 #endif
   // (3) the 4 lowest levels of every item in registers
   double v0 = 0.0;
@@ -2595,7 +2623,7 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
     __syncthreads();
   }
 #ifdef MPPI_STAMPS
-  if (blockIdx.x == 0) FIN_STAMP(10);
+  if (blk == 0) FIN_STAMP(10);
 #endif
   // root of slot c: part[c * NG]
   if (f.mode == 0) {
@@ -2612,7 +2640,7 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
                          __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (gridDim.x > 1) {
+  if (nblk > 1) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* flag = reinterpret_cast<int*>(mlev);
@@ -2626,8 +2654,11 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
       // and complete (vmcnt(0)) before the barrier, so a relaxed count suffices on gfx950
       const unsigned prev = __hip_atomic_fetch_add(f.level1_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
-      const int last = prev == gridDim.x - 1;
-      if (last) __hip_atomic_store(f.level1_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+      const int last = prev == (unsigned)nblk - 1;
+      if (last) {  // re-armed; every finish workgroup has passed its record wait (fused launch)
+        __hip_atomic_store(f.level1_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (RECS_WT) __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       flag[0] = last;
     }
     __syncthreads();
@@ -2638,6 +2669,7 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (RECS_WT && tid == 0) __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #ifdef MPPI_STAMPS
   FIN_STAMP(13);
@@ -2652,6 +2684,10 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
   FIN_STAMP(1);
 #endif
   finish_phase2<false>(f, ures, smem_raw, tid, FIN_THREADS);
+}
+
+__global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishArgs f, int P, int ncol) {
+  colfin_body<false>(f, P, ncol, (int)blockIdx.x, (int)gridDim.x, nullptr);
 }
 
 // Deferred optimal rollout (MPPI_isaac.py:696-720) of the sequence a mode-2
@@ -3046,11 +3082,11 @@ hipError_t launch_normal_table(const float* Z, int rows, int grid, float res, fl
 // The step's sampling normals (sampling_warp.py:54-92 with the Philox noise of
 // DEFINED D1), precomputed so the rollout's side waves only load them: thread =
 // (block, Philox block n = t/2, trajectory); writes eps1/eps2 of steps t, t+1.
-__global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t n_base, int64_t k_offset,
-                                                         int H, int n_blocks, float* __restrict__ eps) {
-  const int tj = threadIdx.x;
+// Rows g = g0, g0 + gstride, ... of (block, Philox block n) for trajectory tj of each block.
+__device__ __forceinline__ void noise_rows(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int n_blocks,
+                                           float* __restrict__ eps, int64_t g0, int64_t gstride, int tj) {
   const int NB = (H + 1) >> 1;
-  for (int64_t g = blockIdx.x; g < (int64_t)n_blocks * NB; g += gridDim.x) {
+  for (int64_t g = g0; g < (int64_t)n_blocks * NB; g += gstride) {
     const int n = (int)(g % NB);
     const int64_t blk = g / NB;
     const uint64_t kg = (uint64_t)(k_offset + blk * 256 + tj);
@@ -3077,6 +3113,53 @@ __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t
     }
 #endif
   }
+}
+__global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t n_base, int64_t k_offset,
+                                                         int H, int n_blocks, float* __restrict__ eps) {
+  noise_rows(seed, n_base, k_offset, H, n_blocks, eps, blockIdx.x, gridDim.x, threadIdx.x);
+}
+
+// =====================================================================  fused step launch
+// One launch per MPPI step: workgroups [0, nroll) are the role-split rollout (each counts its
+// record once it is written through), [nroll, nroll + fin_groups) the column-split finish
+// (each waits for the count, then reduces its columns; the last runs phase 2 and re-arms the
+// count), and the rest generate the normals of a later step (noise_rows, four 256-trajectory
+// rows per workgroup).  Workgroups are dispatched in index order, so the finish and noise
+// workgroups take CUs as rollout workgroups retire: no kernel boundary between rollout and
+// finish, no event between the rollout and the noise, the noise beside the finish as before.
+// A finish workgroup only waits on rollout workgroups dispatched before it (no deadlock).
+template <int TB, int PROJ>
+__global__ __launch_bounds__(NROLES * TB) void mppi_step_fused_kernel(const RolloutArgs a, const FusedArgs z) {
+  const int b = (int)blockIdx.x;
+  if (b < z.nroll) {
+    roles_body<TB, PROJ, 0, false, true>(a, z.rec_cnt);
+    return;
+  }
+  if (b < z.nroll + z.fin_groups) {
+    if (threadIdx.x == 0) {  // bounded (2 s of the 100 MHz clock): a lost count cannot hang the device
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(z.rec_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)z.nroll &&
+             __builtin_amdgcn_s_memrealtime() - t0 < 200000000ull)
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __syncthreads();
+    colfin_body<true>(z.f, z.fin_P, z.fin_ncol, b - z.nroll, z.fin_groups, z.rec_cnt);
+    return;
+  }
+  const int nb = (int)gridDim.x - z.nroll - z.fin_groups;
+  const int sub = threadIdx.x >> 8;  // NROLES * TB / 256 rows in flight per workgroup
+  noise_rows(a.seed, z.noise_n_base, a.k_offset, a.H, z.nroll, z.noise_eps,
+             (int64_t)(b - z.nroll - z.fin_groups) * (NROLES * TB / 256) + sub, (int64_t)nb * (NROLES * TB / 256),
+             threadIdx.x & 255);
+}
+
+hipError_t launch_step_fused(const RolloutArgs& a, const FusedArgs& z, size_t lds, hipStream_t st, int proj) {
+  const dim3 g((unsigned)(z.nroll + z.fin_groups + z.noise_groups)), b(NROLES * 256);
+  if (proj == 3)
+    hipLaunchKernelGGL((mppi_step_fused_kernel<256, 3>), g, b, lds, st, a, z);
+  else
+    hipLaunchKernelGGL((mppi_step_fused_kernel<256, 2>), g, b, lds, st, a, z);
+  return hipGetLastError();
 }
 
 hipError_t launch_noise(uint64_t seed, uint64_t n_base, int64_t k_offset, int blocks, int H, float* eps,

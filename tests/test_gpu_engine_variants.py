@@ -8,6 +8,8 @@ Each toggle below changes only WHERE or WHEN work runs, never the arithmetic:
   MPPI_NOISE_AHEAD=1  normals generated one step ahead instead of two
   MPPI_ROLES=0/1    the pair rollout kernel / the role-split one at any K
   MPPI_NOISE_GPC=1  noise grid of one workgroup per CU
+  MPPI_FUSED=0      rollout, finish and noise as three launches instead of the fused step launch
+  MPPI_FUSED_NOISE_GROUPS=0/7  the fused launch without its noise workgroups / with only 7
 The toggles are read when a context is created, so each variant gets its own engine.
 Sizes: n = 256 leaf records (C3 K) and n = 1024 (C5 K) at a short horizon.
 """
@@ -21,7 +23,7 @@ pytestmark = pytest.mark.gpu
 KEYS = ("u1_opt", "u2_opt", "lin_vel", "ang_vel")
 
 
-def _run(env, K, H, steps=3, info=None):
+def _run(env, K, H, steps=3, info=None, step_ids=None):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
@@ -41,7 +43,7 @@ def _run(env, K, H, steps=3, info=None):
     eng.set_costmap(cm, hw)
     eng.set_state(_lib.make_state(-60.0, -5.0, (1.0, 0.0, 0.0), goal_x=65.0, goal_y=10.0))
     outs = []
-    for i in range(steps):
+    for i in (step_ids if step_ids is not None else range(steps)):
         o = eng.step("3d", i)
         outs.append({k: o[k].copy() for k in KEYS})
     costs = eng.costs()
@@ -54,9 +56,11 @@ def _run(env, K, H, steps=3, info=None):
 @pytest.mark.parametrize("K,H", [(65536, 24), (262144, 16)])
 @pytest.mark.parametrize("env", [{"MPPI_COLFIN": "0"}, {"MPPI_UCACHE": "0"}, {"MPPI_NOISE_AT": "1"},
                                  {"MPPI_NOISE_AT": "2"}, {"MPPI_NOISE_AHEAD": "1"}, {"MPPI_ROLES": "0"},
-                                 {"MPPI_ROLES": "1"}, {"MPPI_NOISE_GPC": "1"}],
+                                 {"MPPI_ROLES": "1"}, {"MPPI_NOISE_GPC": "1"}, {"MPPI_FUSED": "0"},
+                                 {"MPPI_FUSED_NOISE_GROUPS": "0"}, {"MPPI_FUSED_NOISE_GROUPS": "7"}],
                          ids=["record-tree", "no-ucache", "noise-after-finish", "noise-beside-rollout",
-                              "noise-one-ahead", "pair-kernel", "role-split-kernel", "noise-1-per-cu"])
+                              "noise-one-ahead", "pair-kernel", "role-split-kernel", "noise-1-per-cu",
+                              "unfused", "fused-noise-separate", "fused-7-noise-groups"])
 def test_variant_bitwise_equal(K, H, env):
     ref, ref_costs = _run({}, K, H)
     got, got_costs = _run(env, K, H)
@@ -82,3 +86,16 @@ def test_column_split_finish_at_4096_records(K, H):
     for i, (a, b) in enumerate(zip(got, ref)):
         for k in KEYS:
             np.testing.assert_array_equal(a[k], b[k], err_msg=f"step {i} {k}")
+
+
+@pytest.mark.parametrize("env", [{"MPPI_FUSED": "0"}, {"MPPI_FUSED": "1"}], ids=["unfused", "fused"])
+def test_step_counter_jumps(env):
+    """Step counters that skip and repeat (normals generated out of order, slots reused) give the
+    same results with and without the fused launch."""
+    ids = [0, 1, 5, 6, 6, 2]
+    ref, ref_costs = _run({"MPPI_FUSED": "0", "MPPI_ROLES": "0"}, 65536, 24, step_ids=ids)
+    got, got_costs = _run(env, 65536, 24, step_ids=ids)
+    np.testing.assert_array_equal(got_costs, ref_costs)
+    for i, (a, b) in enumerate(zip(got, ref)):
+        for k in KEYS:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=f"call {i} {k} {env}")
