@@ -1512,6 +1512,9 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 //   PROD  step p : cost > p - D   (ring_in slot p % D read by CHAIN and COST; COST waited on CHAIN)
 //   WHEEL / COST step s : chained > s
 // Deadlock-free: no wave waits on a later step of a wave that waits on it.
+#ifndef MPPI_COLFIN_FENCED
+#define MPPI_COLFIN_FENCED 0  // 1: release / acquire at agent scope around the finish handoffs (D8)
+#endif
 constexpr int ROLE_CHAIN = 0, ROLE_PROD = 1, ROLE_WHEEL = 2, ROLE_COST = 3, NROLES = 4;
 
 template <int TB, int PROJ, int MODE, bool DUMP, bool FUSED>
@@ -1875,7 +1878,11 @@ __device__ __forceinline__ void roles_body(const RolloutArgs& a, unsigned* rec_c
   if constexpr (FUSED) {  // the record is written through: count it (D8: complete, then a relaxed count)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#if MPPI_COLFIN_FENCED
+    if (tid == 0) __hip_atomic_fetch_add(rec_cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#else
     if (tid == 0) __hip_atomic_fetch_add(rec_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
   }
 }
 
@@ -1896,9 +1903,6 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const R
 #define MPPI_FIN_PRIO 0
 #endif
 constexpr int FIN_THREADS = 1024;
-#ifndef MPPI_COLFIN_FENCED
-#define MPPI_COLFIN_FENCED 0  // 1: release / acquire at agent scope around the column-split handoff
-#endif
 constexpr int FIN_LDS_NODES = 16;
 constexpr int FIN_GROUP_CHUNK = 64;    // groups per scale-table fill (15 PairScale + 16 m each)
 
@@ -3143,6 +3147,9 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_fused_kernel(const Roll
         __builtin_amdgcn_s_sleep(2);
     }
     __syncthreads();
+#if MPPI_COLFIN_FENCED
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
     colfin_body<true>(z.f, z.fin_P, z.fin_ncol, b - z.nroll, z.fin_groups, z.rec_cnt);
     return;
   }
