@@ -2166,7 +2166,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
     ostage[tid] = ures;
     // optimal-sequence wheel filter (sampling_warp.py:120-138, k=3.0, a=0.92): the
     // inputs (u*k)*(1-a) in parallel, only the recurrence L = L*a + in on lane 0
-    uo[tid] = (ures * f.ok) * one_m_a;
+    uo[tid < H ? 2 * tid : 2 * (tid - H) + 1] = (ures * f.ok) * one_m_a;  // (L, R) input pairs
   }
   float* win = reinterpret_cast<float*>(smem + f.win_offset);
   if constexpr (LDS) {
@@ -2185,69 +2185,46 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
   dem.init(f.Z, win, f.rows, f.grid, f.wx0, f.wy0, f.W, f.Wr, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
   dem.N = f.ntab;
   const int lane = tid & 63, wave = tid >> 6;
+  // the recurrence L = L a + in_L, R = R a + in_R on lane 0 of wave 0 with (L, R) packed: one
+  // v_pk_mul and one v_pk_add per step (IEEE per component: the reference's two roundings), the
+  // input pairs read four steps ahead, each step's (L, R) stored to LDS (no per-step select)
+  f2* lr = reinterpret_cast<f2*>(chain);  // [H] (L, R) pairs; chain is free until the optimal rollout
   if (wave == 0) {
-    // the recurrence on every lane of wave 0 (identical values), inputs read 8 at a time
-    // as LDS broadcasts; lane t%64 keeps L_t, R_t and stores them once per 64 steps
-    float L = f.wl, R = f.wr;
-    float myL = 0.0f, myR = 0.0f;
-    int t = 0;
-    // the next block's inputs are read while this block's recurrence runs (one LDS latency
-    // per block would otherwise sit on the serial path)
-    float i1[8], i2[8];
-    if (H >= 8) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        i1[k] = uo[k];
-        i2[k] = uo[H + k];
-      }
-    }
-    for (; t + 8 <= H; t += 8) {
-      float n1[8], n2[8];
-      const bool more = t + 16 <= H;  // wave-uniform
-      if (more) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          n1[k] = uo[t + 8 + k];
-          n2[k] = uo[H + t + 8 + k];
+    if (lane == 0) {
+      const f2* in2 = reinterpret_cast<const f2*>(uo);
+      const f2 a2 = bc2(f.oa);
+      f2 LR = f2{f.wl, f.wr};
+      int t = 0;
+      if (H >= 4) {
+        f2 i0 = in2[0], i1 = in2[1], i2 = in2[2], i3 = in2[3];
+        for (; t + 4 <= H; t += 4) {
+          const int tn = min(t + 4, H - 4);  // the next four pairs (clamped: re-read at the end)
+          const f2 n0 = in2[tn], n1 = in2[tn + 1], n2 = in2[tn + 2], n3 = in2[tn + 3];
+          LR = LR * a2 + i0;
+          lr[t] = LR;
+          LR = LR * a2 + i1;
+          lr[t + 1] = LR;
+          LR = LR * a2 + i2;
+          lr[t + 2] = LR;
+          LR = LR * a2 + i3;
+          lr[t + 3] = LR;
+          i0 = n0;
+          i1 = n1;
+          i2 = n2;
+          i3 = n3;
         }
       }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        L = L * f.oa + i1[k];
-        R = R * f.oa + i2[k];
-        const bool mine = lane == ((t + k) & 63);
-        myL = mine ? L : myL;
-        myR = mine ? R : myR;
+      for (; t < H; ++t) {
+        LR = LR * a2 + in2[t];
+        lr[t] = LR;
       }
-      if (((t + 8) & 63) == 0) {
-        vb[t + 8 - 64 + lane] = myL;
-        wb[t + 8 - 64 + lane] = myR;
-      }
-      if (more) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          i1[k] = n1[k];
-          i2[k] = n2[k];
-        }
-      }
-    }
-    for (; t < H; ++t) {
-      L = L * f.oa + uo[t];
-      R = R * f.oa + uo[H + t];
-      const bool mine = lane == (t & 63);
-      myL = mine ? L : myL;
-      myR = mine ? R : myR;
-    }
-    if ((H & 63) != 0 && lane < (H & 63)) {  // the last, partial 64-step block
-      vb[(H & ~63) + lane] = myL;
-      wb[(H & ~63) + lane] = myR;
     }
 #ifdef MPPI_STAMPS
     FIN_STAMP(12);
 #endif
   } else if (wave == 1 && f.mode == 2) {
     if (lane == 0) {  // step 0 of the optimal rollout needs only the first filter step
-      const float L0 = f.wl * f.oa + uo[0], R0 = f.wr * f.oa + uo[H];
+      const float L0 = f.wl * f.oa + uo[0], R0 = f.wr * f.oa + uo[1];
       const float v0 = clampf((L0 + R0) / 2.0f, f.vmin, f.vmax);
       const float w0 = clampf(((-L0) + R0) / f.rwheel, f.wmin, f.wmax);
       float sn0, cs0;
@@ -2257,7 +2234,8 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
   }
   __syncthreads();
   for (int t = tid; t < H; t += nthreads) {
-    const float L = vb[t], R = wb[t];
+    const f2 LRt = lr[t];
+    const float L = LRt.x, R = LRt.y;
     const float v = clampf((L + R) / 2.0f, f.vmin, f.vmax);
     const float w = clampf(((-L) + R) / f.rwheel, f.wmin, f.wmax);
     float sn, cs;

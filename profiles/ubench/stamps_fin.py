@@ -1,0 +1,51 @@
+"""Diagnostic: phase breakdown of the column-split finish (FIN_STAMP slots, s_memrealtime 100 MHz).
+
+Uses a separate library built with -DMPPI_STAMPS (never the product .so):
+  make -C husky-rover-mppi-isaacsim_amd/csrc OUT=$PWD/ab/stamps.so EXTRA=-DMPPI_STAMPS
+Usage (GPU box): python profiles/ubench/stamps_fin.py ab/stamps.so [K] [H] [async 0|1]
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "husky-rover-mppi-isaacsim_amd")]
+
+
+def main():
+    so = os.path.abspath(sys.argv[1])
+    K = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+    H = int(sys.argv[3]) if len(sys.argv) > 3 else 100
+    asyn = (sys.argv[4] != "0") if len(sys.argv) > 4 else True
+    os.environ["MPPI_LIB_PATH"] = so
+    from mppi_amd import _lib, scene
+    lib = _lib.load_library(so)
+    lib.mppi_debug_stamps.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+    Z, hw, cm = scene.scene_c3()
+    eng = _lib.Engine(_lib.make_params(K, H), 0)
+    eng.set_async_tail(asyn)
+    eng.set_dem(Z, hw)
+    eng.set_costmap(cm, hw)
+    eng.set_state(_lib.make_state(-60.0, -5.0, goal_x=65.0, goal_y=10.0))
+    n = 64 * 16 * 6 + 1024 * 2 + 64 * 8 + 16
+    rows = []
+    for i in range(12):
+        eng.step("3d", i)
+        if i >= 4:
+            eng.outputs()
+            buf = (C.c_uint64 * n)()
+            assert lib.mppi_debug_stamps(buf, n) == 0
+            rows.append(np.array(buf, dtype=np.float64)[-16:])
+    fs = np.median(np.array(rows), axis=0)
+    us = lambda a, b: (fs[b] - fs[a]) / 100.0  # noqa: E731
+    print(f"K={K} H={H} async={asyn}: finish phases (us, median of {len(rows)} steps, workgroup 0 / last)")
+    print(f"  start -> scale table {us(0, 9):.2f}  -> columns reduced {us(9, 10):.2f}  -> counted (last) {us(10, 13):.2f}")
+    print(f"  u_opt read {us(13, 1):.2f}  phase2 setup {us(1, 2):.2f}  filter {us(2, 12):.2f}  "
+          f"v/w/sincos {us(12, 3):.2f}  outputs {us(3, 4):.2f}  signal {us(4, 5):.2f}")
+    print(f"  total start -> signal {us(0, 5):.2f}")
+
+
+if __name__ == "__main__":
+    main()
