@@ -1915,7 +1915,7 @@ __device__ __forceinline__ double group8_apply(const PairScale* ps, const double
 
 // Robot pose with the heading projected on the DEM (projection_warp.py:306-310).
 template <bool LDS>
-__device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>& dem) {
+__device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>& dem, const float* qpre = nullptr) {
   const float res_half_neg = (-f.res) / 2.0f;
   const float res_sq = f.res * f.res;
   Traj s;
@@ -1923,7 +1923,14 @@ __device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>
   s.y = f.y0;
   bool unused = false;
   float q[4];
-  dem.template corners<false>(s.x, s.y, q, unused);
+  if (qpre) {  // the corners, loaded when the finish started (same cell: corners<false> of (x0, y0))
+    q[0] = qpre[0];
+    q[1] = qpre[1];
+    q[2] = qpre[2];
+    q[3] = qpre[3];
+  } else {
+    dem.template corners<false>(s.x, s.y, q, unused);
+  }
   const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
   const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
   const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
@@ -1948,7 +1955,8 @@ __device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>
 // chain[12 t ..] (lane 0).
 constexpr int TAIL_WIN = 8, TAIL_WIN_LO = 3;  // neighbourhood cells [c - 3, c + 4] per axis
 __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem<false>& dem, const float* vb,
-                                              const float* snb, const float* csb, float* chain, int H, int lane) {
+                                              const float* snb, const float* csb, float* chain, int H, int lane,
+                                              const float* qpre) {
   const f2 cell_off = f2{-f.x_min, f.y_min};
   const float fi_hi = (float)(f.grid - 1), fj_lo = (float)(1 - f.rows);
   const float4* ntab0 = dem.N + (f.grid + 2);  // entry (jj, ii) = (1 - tjj, ti + 1): offset ti - tjj * (grid + 1)
@@ -1992,7 +2000,7 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem<fal
     }
     return n;
   };
-  const Traj s0 = initial_pose(f, dem);
+  const Traj s0 = initial_pose(f, dem, qpre);
   Head hd{f2{s0.hx, s0.hy}, s0.hz};
   f2 pos = f2{s0.x, s0.y};
   int tiA, tjjA, tiB, tjjB, loA, loB;
@@ -2044,10 +2052,10 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem<fal
 // first step into out[0..12), the layout optimal_rollout uses for nsteps = 1.
 template <bool LDS>
 __device__ __forceinline__ void first_step(const FinishArgs& f, const Dem<LDS>& dem, float v, float sn, float cs,
-                                           float* out) {
+                                           float* out, const float* qpre) {
   const float res_half_neg = (-f.res) / 2.0f;
   const float res_sq = f.res * f.res;
-  Traj s = initial_pose(f, dem);
+  Traj s = initial_pose(f, dem, qpre);
   const Traj saved = s;
   float q[4], nx, ny, nz;
   bool bad = false;
@@ -2072,11 +2080,12 @@ __device__ __forceinline__ void first_step(const FinishArgs& f, const Dem<LDS>& 
 template <bool LDS>
 __device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem<LDS>& dem, const float* vb,
                                                 const float* snb, const float* csb, float* chain,
-                                                int nsteps, float* out, int tid, int nthreads) {
+                                                int nsteps, float* out, int tid, int nthreads,
+                                                const float* qpre = nullptr) {
   const float res_half_neg = (-f.res) / 2.0f;
   const float res_sq = f.res * f.res;
   if constexpr (!LDS && MPPI_LEAN_CHAIN) {  // the serial chain on wave 0 (tail_chain_3d)
-    if (tid < 64) tail_chain_3d(f, dem, vb, snb, csb, chain, nsteps, tid);
+    if (tid < 64) tail_chain_3d(f, dem, vb, snb, csb, chain, nsteps, tid, qpre);
   } else if (tid == 0) {  // the serial chain (projection_warp.py:306-326)
     Traj s = initial_pose(f, dem);
     float vn = vb[0], sn_n = snb[0], cs_n = csb[0];
@@ -2147,8 +2156,10 @@ __device__ __forceinline__ void signal_done(const FinishArgs& f) {
 // completion word.  Called by all `nthreads` threads of one workgroup; smem holds
 // uo[2H] v[H] w[H] sn[H] cs[H] chain[12H] out[16H] floats (+ the DEM window for LDS).
 template <bool LDS>
+// qpre: the DEM corners of the robot's cell, loaded at the start of the finish by waves 0 and
+// nthreads / 64 - 1 (the waves that use them here), or nullptr.
 __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, unsigned char* smem, int tid,
-                                              int nthreads) {
+                                              int nthreads, const float* qpre = nullptr) {
   const int H = f.H;
   float* uo = reinterpret_cast<float*>(smem);
   float* vb = uo + 2 * H;
@@ -2222,14 +2233,14 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
 #ifdef MPPI_STAMPS
     FIN_STAMP(12);
 #endif
-  } else if (wave == 1 && f.mode == 2) {
+  } else if (wave == nthreads / 64 - 1 && f.mode == 2) {
     if (lane == 0) {  // step 0 of the optimal rollout needs only the first filter step
       const float L0 = f.wl * f.oa + uo[0], R0 = f.wr * f.oa + uo[1];
       const float v0 = clampf((L0 + R0) / 2.0f, f.vmin, f.vmax);
       const float w0 = clampf(((-L0) + R0) / f.rwheel, f.wmin, f.wmax);
       float sn0, cs0;
       dm_sincosf(w0 * f.dt, &sn0, &cs0);
-      first_step<LDS>(f, dem, v0, sn0, cs0, ostage + 4 * H);
+      first_step<LDS>(f, dem, v0, sn0, cs0, ostage + 4 * H, qpre);
     }
   }
   __syncthreads();
@@ -2258,7 +2269,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
 #endif
   // mode 1: the whole optimal rollout; mode 2: its first step only (the pose the
   // closed loop needs now), the rest runs in mppi_tail_kernel on a side stream
-  if (f.mode != 2) optimal_rollout<LDS>(f, dem, vb, snb, csb, chain, H, ostage + 4 * H, tid, nthreads);
+  if (f.mode != 2) optimal_rollout<LDS>(f, dem, vb, snb, csb, chain, H, ostage + 4 * H, tid, nthreads, qpre);
   __syncthreads();
   for (int i = tid; i < nout; i += nthreads) store_out(f.out + i, ostage[i]);
 #ifdef MPPI_STAMPS
@@ -2521,6 +2532,18 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
   const int E = 2 * H + 2;
   const int n = f.n_recs;
   const double* recs = f.recs;
+  // the robot cell's DEM corners for phase 2's initial pose, loaded now by the two waves that use
+  // them there (only the last workgroup does), so that load is off phase 2's serial path
+  float qpre[4] = {0.f, 0.f, 0.f, 0.f};
+  {
+    const int w = tid >> 6;
+    if (f.mode != 0 && (w == 0 || w == FIN_THREADS / 64 - 1)) {
+      Dem<false> d0;
+      d0.init(f.Z, nullptr, f.rows, f.grid, 0, 0, 1, 1, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
+      bool unused = false;
+      d0.template corners<false>(f.x0, f.y0, qpre, unused);
+    }
+  }
   PairScale* lps = reinterpret_cast<PairScale*>(smem_raw);
   float* mlev = reinterpret_cast<float*>(lps + (P - 1));  // node minima, level l at 2P - (2P >> l)
   double* part = reinterpret_cast<double*>(mlev + 2 * P);  // [ncol + 1][P / 16], 8-byte aligned (P >= 16)
@@ -2665,7 +2688,7 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
   FIN_STAMP(6);
   FIN_STAMP(1);
 #endif
-  finish_phase2<false>(f, ures, smem_raw, tid, FIN_THREADS);
+  finish_phase2<false>(f, ures, smem_raw, tid, FIN_THREADS, qpre);
 }
 
 __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishArgs f, int P, int ncol) {
