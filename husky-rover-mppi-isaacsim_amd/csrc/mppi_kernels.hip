@@ -3141,13 +3141,23 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_fused_kernel(const Roll
     return;
   }
   if (b < z.nroll + z.fin_groups) {
+    __shared__ int timed_out;
     if (threadIdx.x == 0) {  // bounded (2 s of the 100 MHz clock): a lost count cannot hang the device
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(z.rec_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)z.nroll &&
-             __builtin_amdgcn_s_memrealtime() - t0 < 200000000ull)
+      int late = 0;
+      while (__hip_atomic_load(z.rec_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)z.nroll) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 >= 200000000ull) {
+          late = 1;
+          break;
+        }
         __builtin_amdgcn_s_sleep(2);
+      }
+      timed_out = late;
     }
     __syncthreads();
+    // a finish without all records publishes nothing: the host's wait reports the step as failed
+    // ("finish kernel retired without publishing its outputs") instead of returning wrong controls
+    if (timed_out) return;
 #if MPPI_COLFIN_FENCED
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #endif
