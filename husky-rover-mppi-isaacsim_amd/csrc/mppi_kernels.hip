@@ -226,11 +226,29 @@ struct Dem {
     return N[(uint32_t)(jj * (grid + 1) + ii)];
 #endif
   }
+  // cell() + at() in two instructions per index: clamp(trunc(clamp(f, -1, grid)), 0, grid - 1)
+  // == trunc(med3(f, 0, grid - 1)) and clamp(-trunc(clamp(f, -rows, 1)), 0, rows - 1)
+  // == -trunc(med3(f, 1 - rows, 0)); a NaN lands on the same bound (v_med3_f32 with a NaN
+  // operand returns the min3 of the others)
   template <bool F>
   __device__ __forceinline__ float point(float x, float y, bool& bad) const {
-    int i, j;
-    cell<F>(x, y, i, j, bad);
-    return at(j, i);
+    float fi, fj;
+    if (cdiv) {  // uniform branch
+      fi = cdiv_f(x - x_min, res, rinv);
+      fj = cdiv_f(y + y_min, res, rinv);
+    } else {
+      fi = dv<F>(x - x_min, rr<F>(), bad);
+      fj = dv<F>(y + y_min, rr<F>(), bad);
+    }
+    const int col = (int)__builtin_amdgcn_fmed3f(fi, 0.0f, (float)(grid - 1));
+    const int row = -(int)__builtin_amdgcn_fmed3f(fj, (float)(1 - rows), 0.0f);
+    if constexpr (LDS) {
+      const int r = clampi(row - wy0, 0, Wr - 1);
+      const int c = clampi(col - wx0, 0, W - 1);
+      return win[r * W + c];
+    } else {
+      return Z[(size_t)row * grid + col];
+    }
   }
 };
 
@@ -689,8 +707,9 @@ __device__ __forceinline__ int costmap_index(int size, float hw, const Recip& rr
     fx = dv<F>(x + hw, rres_c, bad);
     fy = dv<F>((-y) + hw, rres_c, bad);
   }
-  const int ix = clampi(trunc_clamped(fx, -1.0f, (float)size), 0, size - 1);
-  const int iy = clampi(trunc_clamped(fy, -1.0f, (float)size), 0, size - 1);
+  // clamp(trunc(clamp(f, -1, size)), 0, size - 1) == trunc(med3(f, 0, size - 1)) (as Dem::point)
+  const int ix = (int)__builtin_amdgcn_fmed3f(fx, 0.0f, (float)(size - 1));
+  const int iy = (int)__builtin_amdgcn_fmed3f(fy, 0.0f, (float)(size - 1));
   return ix + size * iy;
 }
 
