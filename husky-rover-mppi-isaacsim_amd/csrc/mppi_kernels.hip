@@ -1631,44 +1631,24 @@ __device__ __forceinline__ void roles_body(const RolloutArgs& a, unsigned* rec_c
     if constexpr (PROJ == 3) {
       const int* cons[2] = {f_wheel, f_cost};
       int seen_cons[2] = {0, 0};
-#ifdef MPPI_STAMPS
       WaitStat ws;
       chain_wave_3d<TB, 2, DUMP>(a, dem, s, tj, valid, kl, ring_in, ring_out, f_prod, f_chain, cons, seen_prod,
                                  seen_cons, ws);
+#ifdef MPPI_STAMPS
       st_wait += ws.wait;
       st_n += ws.n;
-#else
-      WaitStat ws;
-      chain_wave_3d<TB, 2, DUMP>(a, dem, s, tj, valid, kl, ring_in, ring_out, f_prod, f_chain, cons, seen_prod,
-                                 seen_cons, ws);
 #endif
     } else
-    for (int sc = 0; sc < H; ++sc) {
+    for (int sc = 0; sc < H; ++sc) {  // 2D (projection_warp.py:373-382): no normal, wheels zero
       wait_ge(f_prod, sc + 1, seen_prod);
       wait_ge(f_wheel, sc - D + 1, seen_wheel);
       wait_ge(f_cost, sc - D + 1, seen_cost);
       const float* ri = ring_in + (sc % D) * RI * TB + tj;
       const float v = ri[0], sn = ri[TB], cs = ri[2 * TB];
-      float cx = 0.f, cy = 0.f, z = 0.f;
-      float q[4];
-      if constexpr (PROJ == 3) {
-        float nx, ny, nz;
-        bool bad = false;
-        const Traj saved = s;
-        chain3d_lean<true>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-        if constexpr (DUMP) dem.template corners<false>(s.x, s.y, q, nobad);  // heights: dump only
-        if (__builtin_expect(bad, 0)) {  // operand outside the fast range: IEEE redo
-          s = saved;
-          chain3d<false, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-        }
-        cx = a.off * (ny * s.hz - nz * s.hy);
-        cy = a.off * (nz * s.hx - nx * s.hz);
-        if constexpr (DUMP) z = bilinear<false>(s.x, s.y, q, dem.template rr<false>(), nobad);
-      } else {
-        StepOut o;
-        step2d<false, false>(dem, a.dt, v, sn, cs, s, o, nobad);
-        z = o.z;
-      }
+      const float cx = 0.f, cy = 0.f;
+      StepOut o;
+      step2d<false, false>(dem, a.dt, v, sn, cs, s, o, nobad);
+      const float z = o.z;
       float* ro = ring_out + (sc % D) * 4 * TB + tj;
       ro[0] = s.x;
       ro[TB] = s.y;

@@ -57,10 +57,14 @@ class ShardedMPPI:
     with no host synchronisation in between.
     """
 
-    def __init__(self, K_global: int, H: int, device, group=None, engine_factory=None, **params_kw):
+    def __init__(self, K_global: int, H: int, device, group=None, engine_factory=None, always_exchange=False,
+                 **params_kw):
         """``engine_factory(K, H, k_offset, device)`` replaces the HIP engine (CPU protocol tests
         drive the same exchange with an oracle-backed stand-in); ``device="cpu"`` then skips the
-        HIP stream and keeps the exchange buffers in host memory (gloo)."""
+        HIP stream and keeps the exchange buffers in host memory (gloo).  ``always_exchange``
+        runs the partial step, the collective and the finish even at world size 1 (tests of the
+        RCCL path on a one-GPU host)."""
+        self.always_exchange = bool(always_exchange)
         import contextlib
 
         import torch
@@ -99,7 +103,7 @@ class ShardedMPPI:
     def step(self, proj="3d", step=0, copy=True):
         """One MPPI_step over K_global trajectories; outputs (identical on all ranks) in host memory."""
         with self._ctx():
-            if self.world == 1:
+            if self.world == 1 and not self.always_exchange:
                 return self.engine.step(proj, step, copy)
             if self.empty:
                 self.record.zero_()
