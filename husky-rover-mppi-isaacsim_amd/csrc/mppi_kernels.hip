@@ -1534,6 +1534,9 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 #ifndef MPPI_COLFIN_FENCED
 #define MPPI_COLFIN_FENCED 0  // 1: release / acquire at agent scope around the finish handoffs (D8)
 #endif
+#ifndef MPPI_SIDE_PRIO
+#define MPPI_SIDE_PRIO 2  // issue priority of the producer / wheel / cost waves (the chain's is 3)
+#endif
 constexpr int ROLE_CHAIN = 0, ROLE_PROD = 1, ROLE_WHEEL = 2, ROLE_COST = 3, NROLES = 4;
 
 template <int TB, int PROJ, int MODE, bool DUMP, bool FUSED>
@@ -1561,7 +1564,7 @@ __device__ __forceinline__ void roles_body(const RolloutArgs& a, unsigned* rec_c
   const int tj = grp * 64 + (tid & 63);  // trajectory within the workgroup
   if (a.wave_prio) {  // above the deferred optimal rollout (priority 0); the chain above all
     if (role == ROLE_CHAIN) __builtin_amdgcn_s_setprio(3);
-    else __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(MPPI_SIDE_PRIO);
   }
   int* f_prod = flags + grp;
   int* f_chain = flags + NG + grp;
