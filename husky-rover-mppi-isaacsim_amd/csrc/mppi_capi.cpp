@@ -1237,6 +1237,8 @@ static int check_grid(int32_t rows, int32_t cols, float res) {
   if (!(res > 0.0f)) return fail(MPPI_EINVAL, "DEM resolution must be > 0");
   if ((int64_t)rows * cols >= ((int64_t)1 << 29))  // kernels address cells with 32-bit byte offsets
     return fail(MPPI_EINVAL, "DEM larger than 2^29 cells");
+  if (rows > (1 << 24) || cols > (1 << 24))  // cell bounds are clamped as exact floats
+    return fail(MPPI_EINVAL, "DEM dimension above 2^24");
   return MPPI_OK;
 }
 
