@@ -554,6 +554,24 @@ __device__ __forceinline__ f2 lean_div2(f2 a, const Recip& r, Lean& l) {
   const f2 e1 = pk_fma(b, q1, -a);
   return pk_fma(-e1, y, q1);
 }
+// (a.x, a.y, az) / r.b: lean_div2 and lean_div_s with their dependent steps interleaved, so the
+// scalar chain's instructions fill the wait states between the packed chain's dependent steps
+// (same operations, same results)
+__device__ __forceinline__ void lean_div3(f2 a, float az, const Recip& r, Lean& l, f2& qxy, float& qz) {
+  l.emin = min(l.emin, min(min(__builtin_amdgcn_frexp_expf(a.x), __builtin_amdgcn_frexp_expf(a.y)),
+                           __builtin_amdgcn_frexp_expf(az)));
+  const f2 b = bc2(r.b), y = bc2(r.y);
+  const f2 q0 = a * y;
+  const float q0z = az * r.y;
+  const f2 e0 = pk_fma(b, q0, -a);
+  const float e0z = __builtin_fmaf(r.b, q0z, -az);
+  const f2 q1 = pk_fma(-e0, y, q0);
+  const float q1z = __builtin_fmaf(-e0z, r.y, q0z);
+  const f2 e1 = pk_fma(b, q1, -a);
+  const float e1z = __builtin_fmaf(r.b, q1z, -az);
+  qxy = pk_fma(-e1, y, q1);
+  qz = __builtin_fmaf(-e1z, r.y, q1z);
+}
 // cross(n, o).xy = (ny oz - nz oy, nz ox - nx oz), as (ny oz, -nx oz) + (-nz oy, nz ox)
 __device__ __forceinline__ f2 cross_xy(f2 nxy, float nz, f2 oxy, float oz) {
   const f2 p1 = nxy.yx * f2{oz, -oz};
@@ -580,12 +598,10 @@ __device__ __forceinline__ Head orient_step(f2 nxy, float nz, const Head& h, flo
   if constexpr (F) {
     const f2 p2 = pxy * pxy;
     const Recip r = lean_norm2((p2.x + p2.y) + pz * pz, l);
-    txy = lean_div2(pxy, r, l);
-    tz = lean_div_s(pz, r, l);
+    lean_div3(pxy, pz, r, l, txy, tz);
     const f2 t2 = txy * txy;
     const Recip ro = lean_norm_near1((t2.x + t2.y) + tz * tz, l);
-    oxy = lean_div2(txy, ro, l);
-    oz = lean_div_s(tz, ro, l);
+    lean_div3(txy, tz, ro, l, oxy, oz);
   } else {
     const float pn = sqrtf((pxy.x * pxy.x + pxy.y * pxy.y) + pz * pz);
     txy = f2{pxy.x / pn, pxy.y / pn};
@@ -605,8 +621,7 @@ __device__ __forceinline__ Head orient_step(f2 nxy, float nz, const Head& h, flo
   if constexpr (F) {
     const f2 r2 = rxy * rxy;
     const Recip r = lean_norm_near1((r2.x + r2.y) + rz * rz, l);
-    o.xy = lean_div2(rxy, r, l);
-    o.z = lean_div_s(rz, r, l);
+    lean_div3(rxy, rz, r, l, o.xy, o.z);
   } else {
     const float rn = sqrtf((rxy.x * rxy.x + rxy.y * rxy.y) + rz * rz);
     o.xy = f2{rxy.x / rn, rxy.y / rn};
@@ -1077,24 +1092,26 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
       // step t in set X (pos, normal in flight, sin / cos / 1 - cos); step t + 1 into set Y.
       // Even steps wait for two steps' worth of progress (the producer's steps t + 1, t + 2 and
       // the consumers' ring slots of t, t + 1), odd steps are covered by them.
-      auto it = [&](auto even_tag, int t, f2& pX, float4& nX, float& snX, float& csX, float& omX, f2& pY,
-                    float4& nY, float& snY, float& csY, float& omY) __attribute__((always_inline)) {
+      // more = t + 1 < H as a compile-time tag: the loop body has no branch around the next
+      // step's advance and gather, so the scheduler can interleave them with step t's outputs
+      auto it = [&](auto even_tag, auto more_tag, int t, f2& pX, float4& nX, float& snX, float& csX, float& omX,
+                    f2& pY, float4& nY, float& snY, float& csY, float& omY) __attribute__((always_inline)) {
         constexpr bool EVEN = decltype(even_tag)::value;
-        const bool more = t + 1 < H;  // uniform
+        constexpr bool more = decltype(more_tag)::value;
         float v1 = 0.f;
-        if (more) read_in(t + 1, v1, snY, csY, omY, EVEN ? min(t + 3, H) : 0);
+        if constexpr (more) read_in(t + 1, v1, snY, csY, omY, EVEN ? min(t + 3, H) : 0);
         const f2 nxy = f2{nX.x, nX.y};
         const float nz = nX.z;
         Lean l;
         lean_init(l);
         Head ho = orient_step<true>(nxy, nz, hd, snX, csX, omX, l);
         f2 p1 = pX;
-        if (more) p1 = advance_step<true>(ho, v1, a.dt, pX, l);
+        if constexpr (more) p1 = advance_step<true>(ho, v1, a.dt, pX, l);
         if (__builtin_expect(lean_bad(l), 0)) {  // operand outside the fast range: IEEE redo
           ho = orient_step<false>(nxy, nz, hd, snX, csX, omX, l);
-          if (more) p1 = advance_step<false>(ho, v1, a.dt, pX, l);
+          if constexpr (more) p1 = advance_step<false>(ho, v1, a.dt, pX, l);
         }
-        if (more) {
+        if constexpr (more) {
           pY = p1;
           gather(pY, nY);
         }
@@ -1123,11 +1140,16 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
         hd = ho;
       };
       int t = 0;
-      for (; t + 1 < H; t += 2) {
-        it(T_{}, t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
-        it(F_{}, t + 1, posB, nvB, snB, csB, omB, posA, nvA, snA, csA, omA);
+      for (; t + 2 < H; t += 2) {
+        it(T_{}, T_{}, t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
+        it(F_{}, T_{}, t + 1, posB, nvB, snB, csB, omB, posA, nvA, snA, csA, omA);
       }
-      if (t < H) it(T_{}, t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
+      if (t + 1 < H) {  // the last two steps
+        it(T_{}, T_{}, t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
+        it(F_{}, F_{}, t + 1, posB, nvB, snB, csB, omB, posA, nvA, snA, csA, omA);
+      } else {  // the last step (H odd)
+        it(T_{}, F_{}, t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
+      }
   }
 }
 
