@@ -1037,7 +1037,10 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
   using F_ = std::false_type;
   const int H = a.H;
   bool nobad = false;
-  {
+  // dem.cdiv (uniform) as a compile-time tag: one copy of the loop per cell-division path, so
+  // no branch inside a step separates the gather from the work around it
+  auto body = [&](auto cd_tag) __attribute__((always_inline)) {
+      constexpr bool CD = decltype(cd_tag)::value;
       // Software-pipelined: iteration t orients step t (its normal gathered during iteration
       // t - 1), then advances the position of step t + 1 and issues that step's normal gather,
       // which stays in flight while step t's outputs are published.  Register sets A / B
@@ -1053,7 +1056,7 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
       // normal-table entry of the cell holding pos (Dem::cell + Dem::normal_cell)
       auto gather = [&](f2 pos, float4& nv) __attribute__((always_inline)) {
         f2 f;
-        if (dem.cdiv) {  // uniform: division by the verified reciprocal (cdiv_f), both axes at once
+        if constexpr (CD) {  // division by the verified reciprocal (cdiv_f), both axes at once
           const f2 aa = pos + cell_off;
           const f2 q0 = aa * bc2(dem.rinv);
           const f2 r = pk_fma(-q0, bc2(dem.res), aa);
@@ -1111,12 +1114,12 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
           ho = orient_step<false>(nxy, nz, hd, snX, csX, omX, l);
           if constexpr (more) p1 = advance_step<false>(ho, v1, a.dt, pX, l);
         }
+        // wheel offset right = 0.2 * cross(normal, current_hv) (projection_warp.py:333)
+        const f2 cxy = bc2(a.off) * cross_xy(nxy, nz, ho.xy, ho.z);
         if constexpr (more) {
           pY = p1;
           gather(pY, nY);
         }
-        // wheel offset right = 0.2 * cross(normal, current_hv) (projection_warp.py:333)
-        const f2 cxy = bc2(a.off) * cross_xy(nxy, nz, ho.xy, ho.z);
         if constexpr (EVEN) {
 #pragma unroll
           for (int c = 0; c < NC; ++c) lds_wait_ge(f_cons[c], t - D + 2, seen_cons[c], ws);
@@ -1150,7 +1153,11 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
       } else {  // the last step (H odd)
         it(T_{}, F_{}, t, posA, nvA, snA, csA, omA, posB, nvB, snB, csB, omB);
       }
-  }
+  };
+  if (dem.cdiv)
+    body(T_{});
+  else
+    body(F_{});
 }
 
 template <int TB, int PROJ, int MODE, bool DUMP>
