@@ -3,7 +3,7 @@
 # Usage (on the box): bash profiles/ab_env2.sh "MPPI_X=0" "MPPI_X=1" ...
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-for round in 1 2; do
+for round in ${ROUNDS:-1 2}; do
   for v in "$@"; do
     timeout -k 10 200 env $v python bench.py --cpu-baseline-seconds 0 --no-bilinear --no-costmap --no-c5 --no-c4 $BENCH_ARGS > $R/gpurun_out/ab.json 2>$R/gpurun_out/ab.err || { tail -5 $R/gpurun_out/ab.err; exit 1; }
     python3 -c "import json; d=json.load(open('$R/gpurun_out/ab.json')); c=d['config']; print('$v', round(d['value']), 'sync', round(c['sync_steps_per_s']), 'fin', c['finish_kernel_avg_ms'], 'roll', d['roofline']['kernel_avg_ms'])"
