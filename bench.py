@@ -400,10 +400,13 @@ def main():
     # every step's outputs still reach pinned host memory inside the timed region
     s0 = args.warmup + args.steps
     el = timed_run(torch, dist, run, args.proj, args.warmup, args.steps, s0, not args.sync)
-    # per-kernel HIP-event times in a separate pass (events add stream work of their own)
-    timed_run(torch, dist, run, args.proj, args.warmup, max(args.steps // 4, 10), 2 * s0, not args.sync,
-              kernel_timing=True)
+    # per-kernel HIP-event times in separate passes (events add stream work of their own): the
+    # rollout and finish with the tail untimed (timing a tail waits for it on the host, which
+    # moves it against the next rollout), then the tail
+    nt = max(args.steps // 4, 10)
+    timed_run(torch, dist, run, args.proj, args.warmup, nt, 2 * s0, not args.sync, kernel_timing=2)
     roll_ms, fin_ms, n_roll = run.eng.timing()
+    timed_run(torch, dist, run, args.proj, args.warmup, nt, 3 * s0, not args.sync, kernel_timing=1)
     tail_ms, n_tail = run.eng.tail_timing()
     info = run.eng.launch_info()
     record_bytes = run.eng.record_len() * 8

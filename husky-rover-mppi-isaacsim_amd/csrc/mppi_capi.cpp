@@ -174,7 +174,7 @@ struct mppi_ctx {
   float* tail_in[kTailSlots] = {};    // device [3H] per slot
   float* tail_host[kTailSlots] = {};  // pinned [12H] per slot (written by the kernel)
   // timing
-  bool timing = false;
+  int timing = 0;  // 1: rollout, finish and tail events; 2: rollout and finish only (mppi_set_timing)
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   bool ev_roll_pending = false, ev_fin_pending = false, ev_tail_pending = false;
   double t_roll = 0, t_fin = 0, t_tail = 0;
@@ -697,12 +697,12 @@ int prepare_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, int mode, 
 int enqueue_tail(mppi_ctx* c, const FinishArgs& f, int par) {
   HIP_TRY(hipEventRecord(c->ev_fin_done, c->stream));
   HIP_TRY(hipStreamWaitEvent(c->tail_stream, c->ev_fin_done, 0));
-  if (c->timing) {
+  if (c->timing == 1) {  // (collecting waits for the previous tail: mode 2 leaves the tail untimed)
     collect_tail_timing(c);
     HIP_TRY(hipEventRecord(c->ev[4], c->tail_stream));
   }
   HIP_TRY(launch_tail(f, c->tail_stream));
-  if (c->timing) {
+  if (c->timing == 1) {
     HIP_TRY(hipEventRecord(c->ev[5], c->tail_stream));
     c->ev_tail_pending = true;
   }
@@ -1466,7 +1466,8 @@ int mppi_set_timing(mppi_ctx* c, int32_t enable) {
   if (!c) return fail(MPPI_EINVAL, "null context");
   int rc = sync_tail(c);
   if (rc) return rc;
-  c->timing = enable != 0;
+  if (enable < 0 || enable > 2) return fail(MPPI_EINVAL, "timing mode must be 0, 1 or 2");
+  c->timing = enable;
   c->t_roll = c->t_fin = c->t_tail = 0.0;
   c->launches = c->tail_launches = 0;
   c->ev_roll_pending = c->ev_fin_pending = c->ev_tail_pending = false;

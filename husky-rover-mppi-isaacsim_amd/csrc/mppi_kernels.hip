@@ -1564,7 +1564,11 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 #define MPPI_COLFIN_FENCED 0  // 1: release / acquire at agent scope around the finish handoffs (D8)
 #endif
 #ifndef MPPI_SIDE_PRIO
-#define MPPI_SIDE_PRIO 2  // issue priority of the producer / wheel / cost waves (the chain's is 3)
+// issue priority of the producer / wheel / cost waves (the chain's is 3).  0, level with the
+// deferred optimal rollout of the previous step (mppi_tail_kernel) on the CU they share: at 2 the
+// tail, starved, ran ~105 us and into the next finish, and pipelined C3 steps alternated between
+// ~98 and ~120 us (profiles/r02_notes.md); 0: ~9900 against ~9200 steps/s
+#define MPPI_SIDE_PRIO 0
 #endif
 constexpr int ROLE_CHAIN = 0, ROLE_PROD = 1, ROLE_WHEEL = 2, ROLE_COST = 3, NROLES = 4;
 

@@ -437,7 +437,9 @@ class Engine:
         return arrs
 
     def set_timing(self, on=True):
-        self._c(self.lib.mppi_set_timing(self.ctx, 1 if on else 0), "mppi_set_timing")
+        """on: False / True (rollout, finish and tail events) or 2 (rollout and finish only)."""
+        mode = on if isinstance(on, int) and not isinstance(on, bool) else (1 if on else 0)
+        self._c(self.lib.mppi_set_timing(self.ctx, mode), "mppi_set_timing")
 
     def timing(self):
         r = C.c_double()

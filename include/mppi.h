@@ -248,7 +248,9 @@ int mppi_dump_rollouts(mppi_ctx* ctx, float* traj, float* heading, float* left_w
                        float* right_wheel, float* lin_vel, float* ang_vel, float* u1, float* u2);
 
 /* HIP-event timing of the rollout kernel and of the combine/optimal-rollout
- * kernel, measured on the context stream around each launch. */
+ * kernel, measured on the context stream around each launch.  enable: 0 off,
+ * 1 rollout, finish and deferred-tail events (collecting a tail's time waits for
+ * it on the host), 2 rollout and finish only (the pipelined schedule undisturbed). */
 int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
 int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_t* launches);
 /* HIP-event time of the deferred optimal-rollout kernels (side stream). */
