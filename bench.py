@@ -401,12 +401,13 @@ def main():
     s0 = args.warmup + args.steps
     el = timed_run(torch, dist, run, args.proj, args.warmup, args.steps, s0, not args.sync)
     # per-kernel HIP-event times in separate passes (events add stream work of their own): the
-    # rollout and finish with the tail untimed (timing a tail waits for it on the host, which
-    # moves it against the next rollout), then the tail
+    # rollout alone with no host wait (mode 2; waiting for the finish / tail events moved the tail
+    # onto the next rollout and inflated it by ~15 us), then the finish and the tail (mode 1)
     nt = max(args.steps // 4, 10)
     timed_run(torch, dist, run, args.proj, args.warmup, nt, 2 * s0, not args.sync, kernel_timing=2)
-    roll_ms, fin_ms, n_roll = run.eng.timing()
+    roll_ms, _, n_roll = run.eng.timing()
     timed_run(torch, dist, run, args.proj, args.warmup, nt, 3 * s0, not args.sync, kernel_timing=1)
+    _, fin_ms, n_fin = run.eng.timing()
     tail_ms, n_tail = run.eng.tail_timing()
     info = run.eng.launch_info()
     record_bytes = run.eng.record_len() * 8
@@ -481,7 +482,7 @@ def main():
                 "pipelined_tail": not args.sync,
                 "sync_steps_per_s": round(args.steps / el_sync, 3),
                 "sync_ms_per_step": round(el_sync / args.steps * 1e3, 4),
-                "finish_kernel_avg_ms": round(fin_ms / max(n_roll, 1), 5),
+                "finish_kernel_avg_ms": round(fin_ms / max(n_fin, 1), 5),
                 "tail_kernel_avg_ms": round(tail_ms / n_tail, 5) if n_tail else None,
                 "src_sha256": source_hash(),
             },

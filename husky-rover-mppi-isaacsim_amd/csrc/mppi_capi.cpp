@@ -174,7 +174,7 @@ struct mppi_ctx {
   float* tail_in[kTailSlots] = {};    // device [3H] per slot
   float* tail_host[kTailSlots] = {};  // pinned [12H] per slot (written by the kernel)
   // timing
-  int timing = 0;  // 1: rollout, finish and tail events; 2: rollout and finish only (mppi_set_timing)
+  int timing = 0;  // 1: rollout, finish and tail events; 2: rollout only, no host wait (mppi_set_timing)
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   bool ev_roll_pending = false, ev_fin_pending = false, ev_tail_pending = false;
   double t_roll = 0, t_fin = 0, t_tail = 0;
@@ -437,7 +437,10 @@ void fill_finish(const mppi_ctx* c, const Plan& pl, const mppi_state& st, Finish
 
 void collect_timing(mppi_ctx* c) {
   float ms = 0.f;
-  if (c->ev_roll_pending && hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) {
+  // mode 2: the host spun on the completion word, which the finish (enqueued after ev[1])
+  // publishes, so ev[1] has retired already (a fused launch publishes before its end: wait)
+  if (c->ev_roll_pending && hipEventSynchronize(c->ev[1]) == hipSuccess &&
+      hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) {
     c->t_roll += ms;
     c->launches += 1;
   }
@@ -476,7 +479,7 @@ int sync_tail(mppi_ctx* c) {
 // Spin until the finish kernel has published c->seq (all outputs in pinned host
 // memory); a fault surfaces through hipStreamQuery.
 int wait_done(mppi_ctx* c) {
-  if (c->timing) {  // timing events need the stream to retire
+  if (c->timing == 1) {  // the finish's timing events need the stream to retire
     HIP_TRY(hipStreamSynchronize(c->stream));
   }
   for (uint64_t i = 0;; ++i) {
@@ -746,9 +749,9 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
     c->fin_ncol = cf_ncol;
     c->fin_groups = cf_groups;
     const size_t lds = std::max(cf_lds, f.mode == 0 ? (size_t)0 : pl.fin_lds_bytes);
-    if (timed && c->timing) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    if (timed && c->timing == 1) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     HIP_TRY(launch_colfin(f, lds, c->stream, cf_P, cf_ncol, cf_groups));
-    if (timed && c->timing) {
+    if (timed && c->timing == 1) {
       HIP_TRY(hipEventRecord(c->ev[3], c->stream));
       c->ev_fin_pending = true;
     }
@@ -772,9 +775,9 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
   c->fin_P = n;
   c->fin_ncol = 0;
   c->fin_groups = groups;
-  if (timed && c->timing) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  if (timed && c->timing == 1) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   HIP_TRY(launch_finish(f, f.mode == 0 ? pl.fin_tree_bytes : pl.fin_lds_bytes, c->stream, groups));
-  if (timed && c->timing) {
+  if (timed && c->timing == 1) {
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     c->ev_fin_pending = true;
   }

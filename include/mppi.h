@@ -249,8 +249,9 @@ int mppi_dump_rollouts(mppi_ctx* ctx, float* traj, float* heading, float* left_w
 
 /* HIP-event timing of the rollout kernel and of the combine/optimal-rollout
  * kernel, measured on the context stream around each launch.  enable: 0 off,
- * 1 rollout, finish and deferred-tail events (collecting a tail's time waits for
- * it on the host), 2 rollout and finish only (the pipelined schedule undisturbed). */
+ * 1 rollout, finish and deferred-tail events (the host waits for the stream and
+ * for each tail to collect them), 2 rollout events only (no host wait: the
+ * pipelined schedule undisturbed; the finish time reads 0). */
 int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
 int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_t* launches);
 /* HIP-event time of the deferred optimal-rollout kernels (side stream). */
