@@ -142,7 +142,7 @@ struct mppi_ctx {
                                // 2 also with the deferred optimal rollout (MPPI_FUSED)
   int fused_noise_groups = -1; // noise of step + 2 in the launch: -1 one workgroup per CU the finish leaves,
                                // n > 0 n workgroups, 0 before the launch on the context stream (MPPI_FUSED_NOISE_GROUPS)
-  int noise_gpc = 0;  // noise kernel workgroups per CU: 0 auto (3 beside the role split, else 4; measured) (MPPI_NOISE_GPC)
+  int noise_gpc = 0;  // noise kernel workgroups per CU: 0 auto = 4 (measured: profiles/r02_notes.md) (MPPI_NOISE_GPC)
   hipEvent_t ev_roll_done = nullptr;
   hipEvent_t ev_prev_roll = nullptr;  // recorded after the last rollout that read an eps slot
   // finish: column-split u_opt slice records / first tree level, arrival counter
@@ -296,10 +296,11 @@ Plan make_plan(const mppi_ctx* c) {
 }
 
 // Noise grid: a few 4-wave workgroups per CU.  The noise of step i+2 runs beside the finish of
-// step i and the start of rollout i+1; beside the role-split rollout (16 waves) and the deferred
-// optimal rollout (4 waves) only 2 per CU leave the rollout's wave slots free.
+// step i and the start of rollout i+1.  4 per CU measured best at C3 with the rollout's side roles
+// at priority 0 (10095 steps/s against 9920 at 3 and 9730 at 2, alternating runs:
+// profiles/r02_notes.md); MPPI_NOISE_GPC overrides.
 int noise_groups(const mppi_ctx* c, const Plan& pl) {
-  const int gpc = c->noise_gpc > 0 ? c->noise_gpc : (pl.roles ? 3 : 4);
+  const int gpc = c->noise_gpc > 0 ? c->noise_gpc : 4;
   return std::max(c->num_cus, 1) * gpc;
 }
 

@@ -10,6 +10,7 @@ Each toggle below changes only WHERE or WHEN work runs, never the arithmetic:
   MPPI_NOISE_GPC=1  noise grid of one workgroup per CU
   MPPI_FUSED=0      rollout, finish and noise as three launches instead of the fused step launch
   MPPI_FUSED_NOISE_GROUPS=0/7  the fused launch without its noise workgroups / with only 7
+  MPPI_WAVE_PRIO=0  rollout waves at the default issue priority (no s_setprio)
 The toggles are read when a context is created, so each variant gets its own engine.
 Sizes: n = 256 leaf records (C3 K) and n = 1024 (C5 K) at a short horizon.
 """
@@ -57,10 +58,11 @@ def _run(env, K, H, steps=3, info=None, step_ids=None):
 @pytest.mark.parametrize("env", [{"MPPI_COLFIN": "0"}, {"MPPI_UCACHE": "0"}, {"MPPI_NOISE_AT": "1"},
                                  {"MPPI_NOISE_AT": "2"}, {"MPPI_NOISE_AHEAD": "1"}, {"MPPI_ROLES": "0"},
                                  {"MPPI_ROLES": "1"}, {"MPPI_NOISE_GPC": "1"}, {"MPPI_FUSED": "0"},
-                                 {"MPPI_FUSED_NOISE_GROUPS": "0"}, {"MPPI_FUSED_NOISE_GROUPS": "7"}],
+                                 {"MPPI_FUSED_NOISE_GROUPS": "0"}, {"MPPI_FUSED_NOISE_GROUPS": "7"},
+                                 {"MPPI_WAVE_PRIO": "0"}],
                          ids=["record-tree", "no-ucache", "noise-after-finish", "noise-beside-rollout",
                               "noise-one-ahead", "pair-kernel", "role-split-kernel", "noise-1-per-cu",
-                              "unfused", "fused-noise-separate", "fused-7-noise-groups"])
+                              "unfused", "fused-noise-separate", "fused-7-noise-groups", "no-wave-priority"])
 def test_variant_bitwise_equal(K, H, env):
     ref, ref_costs = _run({}, K, H)
     got, got_costs = _run(env, K, H)
@@ -99,3 +101,35 @@ def test_step_counter_jumps(env):
     for i, (a, b) in enumerate(zip(got, ref)):
         for k in KEYS:
             np.testing.assert_array_equal(a[k], b[k], err_msg=f"call {i} {k} {env}")
+
+
+def test_timing_modes():
+    """mppi_set_timing: mode 2 times the rollout only (no host wait), mode 1 also the finish and
+    the deferred tail; other modes are refused."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from mppi_amd import _lib, scene
+    eng = _lib.Engine(_lib.make_params(65536, 24), 0)
+    Z, hw, cm = scene.scene_c3()
+    eng.set_dem(Z, hw)
+    eng.set_costmap(cm, hw)
+    eng.set_state(_lib.make_state(-60.0, -5.0, (1.0, 0.0, 0.0), goal_x=65.0, goal_y=10.0))
+    try:
+        eng.set_async_tail(True)
+        eng.set_timing(2)
+        for i in range(4):
+            eng.step("3d", i, copy=False)
+        roll, fin, n = eng.timing()
+        assert n == 4 and roll > 0.0 and fin == 0.0
+        assert eng.tail_timing()[1] == 0
+        eng.set_timing(True)
+        for i in range(4, 8):
+            eng.step("3d", i, copy=False)
+        roll, fin, n = eng.timing()
+        assert n == 4 and roll > 0.0 and fin > 0.0
+        assert eng.tail_timing()[1] >= 3
+        with pytest.raises(Exception):
+            eng.set_timing(3)
+    finally:
+        eng.close()
