@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     ap.add_argument("--no-bilinear", action="store_true", help="skip the C5 tiled-lookup roofline leg")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (K=1048576) strong-scaling leg")
+    ap.add_argument("--timed-events", action="store_true",
+                    help="record the rollout kernel's HIP events inside the timed region (not a separate pass)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 full-step leg (N=1)")
     ap.add_argument("--no-costmap", action="store_true", help="skip the obstacle-costmap builder leg")
     ap.add_argument("--sync", action="store_true",
@@ -399,13 +401,17 @@ def main():
     # headline: the optimal rollout of step i (it only feeds trajectories_sim) overlaps step i+1;
     # every step's outputs still reach pinned host memory inside the timed region
     s0 = args.warmup + args.steps
-    el = timed_run(torch, dist, run, args.proj, args.warmup, args.steps, s0, not args.sync)
-    # per-kernel HIP-event times in separate passes (events add stream work of their own): the
-    # rollout alone with no host wait (mode 2; waiting for the finish / tail events moved the tail
-    # onto the next rollout and inflated it by ~15 us), then the finish and the tail (mode 1)
+    # the rollout kernel's HIP events (mode 2: two event records per step on the engine stream,
+    # no host wait) in a pass of their own; --timed-events records them inside the timed region
+    # (same kernel time within 0.5 %, but ~6 % fewer steps/s: profiles/r02_notes.md)
     nt = max(args.steps // 4, 10)
-    timed_run(torch, dist, run, args.proj, args.warmup, nt, 2 * s0, not args.sync, kernel_timing=2)
+    el = timed_run(torch, dist, run, args.proj, args.warmup, args.steps, s0, not args.sync,
+                   kernel_timing=2 if args.timed_events else 0)
+    if not args.timed_events:
+        timed_run(torch, dist, run, args.proj, args.warmup, nt, 2 * s0, not args.sync, kernel_timing=2)
     roll_ms, _, n_roll = run.eng.timing()
+    # the finish and the tail in a pass of their own (mode 1 waits for the stream and for each tail
+    # on the host, which moves the tail onto the next rollout)
     timed_run(torch, dist, run, args.proj, args.warmup, nt, 3 * s0, not args.sync, kernel_timing=1)
     _, fin_ms, n_fin = run.eng.timing()
     tail_ms, n_tail = run.eng.tail_timing()
