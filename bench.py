@@ -16,8 +16,14 @@ exchange one (2H+2)-double softmax record per step with one RCCL all-gather.
 same config on its own GPU alone (`speedup_vs_1`), and the `c4` leg (K=1,048,576,
 the north-star scaling config) is run beside the headline at every N.
 
-Launch: python bench.py [--config c3|c4|c5] [--steps K --warmup W]  (N=1), or
-        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Launch: python bench.py [--config c3|c4|c5] [--steps K --warmup W]  (N=1);
+        python bench.py --gpus N: one process drives GPUs 0..N-1 through the C-ABI group
+        (mppi_group_create: one context per GPU, ncclCommInitAll, one ncclAllGather per member
+        per step, each member's launches enqueued by its own thread; SURVEY.md §8(e));
+        python bench.py --group-devices 0,0,0,0,0,0,0,0: the same group code path with members
+        sharing one GPU (records exchanged by device copies: a 1-GPU rehearsal of the 8-way split);
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N: one process per
+        GPU (torch.distributed over RCCL, mppi_amd/distributed.ShardedMPPI).
 """
 from __future__ import annotations
 
@@ -73,6 +79,9 @@ def parse():
     ap.add_argument("--no-costmap", action="store_true", help="skip the obstacle-costmap builder leg")
     ap.add_argument("--sync", action="store_true",
                     help="report the synchronous mode (no deferred optimal rollout) as the headline")
+    ap.add_argument("--group-devices", default=None,
+                    help="comma-separated device of each group member (default with --gpus N>1 and no "
+                         "torch.distributed launcher: 0,1,...,N-1)")
     return ap.parse_args()
 
 
@@ -97,14 +106,34 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def host_cores():
-    """CPUs this process may use (the GPU box grants a share of a larger machine), at most 16."""
+def cgroup_cpus():
+    """CPU quota of this process's cgroup (cgroup v2 cpu.max or v1 cfs quota), in CPUs; None if unlimited."""
     try:
-        n = len(os.sched_getaffinity(0))
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def host_cores():
+    """CPUs this process is granted: its affinity set, bounded by its cgroup's CPU quota (the GPU
+    box grants a share of a larger machine; os.cpu_count() reports the whole machine)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
-    return max(1, min(n, cap, 16))
+        aff = os.cpu_count() or 1
+    quota = cgroup_cpus()
+    n = aff if quota is None else max(1, min(aff, int(quota)))
+    return n, aff, quota
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle, numpy)
@@ -139,7 +168,7 @@ def cpu_baseline(Z, hw, cm, start, goal, budget_s):
     from oracle import mppi_ref as R
     _CPU["sc"] = R.Scene(Z, hw, cm)
     _CPU["st"] = R.State(x=start[0], y=start[1], goal_x=goal[0], goal_y=goal[1])
-    nw = host_cores()
+    nw, aff, quota = host_cores()
     table = {}
     t_all = time.perf_counter()
     ctx = mp.get_context("fork")
@@ -171,8 +200,9 @@ def cpu_baseline(Z, hw, cm, start, goal, budget_s):
             "sample": (f"oracle/mppi_ref.py (numpy f32), C3 K=65536 H=100 on {c3['workers']} worker "
                        f"processes (leaf-aligned K shards, same record tree), median of "
                        f"{c3['steps_timed']} steps; host {cpu_model()}, os.cpu_count()={os.cpu_count()}, "
-                       f"granted cores={nw}"),
-            "table": table, "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(), "granted_cores": nw}
+                       f"affinity={aff}, cgroup quota={quota} CPUs -> {nw} workers"),
+            "table": table, "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(), "granted_cores": nw,
+            "affinity_cpus": aff, "cgroup_quota_cpus": quota}
 
 
 # ------------------------------------------------------------------ side legs (N=1)
@@ -294,36 +324,56 @@ def get_scene(fn):
 
 
 class Runner:
-    """One rank's controller for one config: the sharded engine (N>1) or a single-GPU engine."""
+    """One rank's controller for one config: the sharded engine (torch.distributed, N>1), a C-ABI
+    group over `devices` (one process, N>1) or a single-GPU engine."""
 
-    def __init__(self, cfg, device, world, solo=False):
+    def __init__(self, cfg, device, world, solo=False, devices=None):
         from mppi_amd import _lib
         from mppi_amd.distributed import ShardedMPPI
         K, H, scene_fn, start, goal, desc = CONFIGS[cfg]
         self.K, self.H, self.desc = K, H, desc
         self.world = 1 if solo else world
+        self.sharded = self.group = None
         Z, hw, cm = get_scene(scene_fn)
-        if self.world > 1:
+        state = _lib.make_state(start[0], start[1], (1.0, 0.0, 0.0), goal_x=goal[0], goal_y=goal[1])
+        if devices is not None and not solo:
+            self.group = _lib.Group(_lib.make_params(K, H), devices)
+            self.engines = self.group.members
+            self.eng = self.engines[0]
+            self.k_local = self.group.shard(0)[1]
+        elif self.world > 1:
             self.sharded = ShardedMPPI(K, H, device)
             self.eng = self.sharded.engine
+            self.engines = [self.eng]
             self.k_local = self.sharded.k_count
         else:
-            self.sharded = None
             self.eng = _lib.Engine(_lib.make_params(K, H), device)
+            self.engines = [self.eng]
             self.k_local = K
-        self.eng.set_dem(Z, hw)
-        self.eng.set_costmap(cm, hw)
-        self.eng.set_state(_lib.make_state(start[0], start[1], (1.0, 0.0, 0.0), goal_x=goal[0],
-                                           goal_y=goal[1]))
+        for e in self.engines:
+            e.set_dem(Z, hw)
+            e.set_costmap(cm, hw)
+            e.set_state(state)
+
+    def set_async_tail(self, on):
+        for e in self.engines:
+            e.set_async_tail(on)
+
+    def outputs(self):
+        return self.group.outputs() if self.group is not None else self.eng.outputs()
 
     def step(self, proj, i):
-        if self.sharded is not None:
+        if self.group is not None:
+            self.group.step(proj, i, copy=False)
+        elif self.sharded is not None:
             self.sharded.step(proj, i, copy=False)
         else:
             self.eng.step(proj, i, copy=False)
 
     def close(self):
-        if self.sharded is not None:
+        if self.group is not None:
+            self.group.close()
+        elif self.sharded is not None:
             self.sharded.close()
         else:
             self.eng.close()
@@ -331,25 +381,27 @@ class Runner:
 
 def timed_run(torch, dist, run, proj, warmup, steps, step0, async_tail, kernel_timing=False):
     """`warmup` untimed + `steps` timed MPPI steps, barrier + synchronize on both sides; returns
-    the max-over-ranks wall time of the timed steps."""
+    the max-over-ranks wall time of the timed steps.  Kernel timing (if any) on the first
+    member's / rank's engine."""
     eng = run.eng
-    eng.set_async_tail(async_tail)
+    run.set_async_tail(async_tail)
     eng.set_timing(False)
     for i in range(warmup):
         run.step(proj, step0 + i)
 
     def barrier():
-        torch.cuda.synchronize()
+        for d in sorted({e.device for e in run.engines}):
+            torch.cuda.synchronize(d)
         if dist is not None and run.world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
 
     eng.set_timing(kernel_timing)
     barrier()
     t0 = time.perf_counter()
     for i in range(steps):
         run.step(proj, step0 + warmup + i)
-    eng.outputs()          # the last step's deferred optimal rollout is in host memory too
+    run.outputs()          # the last step's deferred optimal rollout is in host memory too
     barrier()
     el = time.perf_counter() - t0
     if dist is not None and run.world > 1:
@@ -380,10 +432,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world == 1 and args.gpus > 1:
-        raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    devices = None   # the in-process group (mppi_group_create) over these devices
+    if args.group_devices:
+        devices = [int(d) for d in args.group_devices.split(",") if d.strip()]
+    elif world == 1 and args.gpus > 1:
+        devices = list(range(args.gpus))
+    if devices is not None and world > 1:
+        raise SystemExit("--group-devices / an in-process group is for a single process (no torch.distributed)")
+    n_gpus = len(set(devices)) if devices is not None else world
+    members = len(devices) if devices is not None else world
     cpu = None
-    if world == 1 and args.cpu_baseline_seconds > 0:
+    if world == 1 and devices is None and args.cpu_baseline_seconds > 0:
         # before anything touches the GPU: the fork pool's workers must not inherit a HIP context
         Z, hw, cm = get_scene("scene_c3")
         cpu = cpu_baseline(Z, hw, cm, CONFIGS["c3"][3], CONFIGS["c3"][4], args.cpu_baseline_seconds)
@@ -394,7 +453,8 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    run = Runner(args.config, local_rank, world)
+    run = Runner(args.config, local_rank, world, devices=devices)
+    group_info = run.group.info() if run.group is not None else None
     K, H = run.K, run.H
     # synchronous MPPI_step semantics first (every output in host memory when step() returns)
     el_sync = timed_run(torch, dist, run, args.proj, args.warmup, args.steps, 0, False)
@@ -421,8 +481,8 @@ def main():
     run.close()
 
     def solo_rate(cfg, steps):
-        """rank 0 alone, the whole config on its GPU (the N=1 reference of this job)."""
-        r = Runner(cfg, local_rank, 1, solo=True)
+        """rank 0 / member 0 alone, the whole config on its GPU (the N=1 reference of this job)."""
+        r = Runner(cfg, devices[0] if devices is not None else local_rank, 1, solo=True)
         t = timed_run(torch, None, r, args.proj, args.warmup, steps, 0, not args.sync)
         r.close()
         return steps / t
@@ -433,10 +493,12 @@ def main():
         if rank == 0:
             speedup = (args.steps / el) / solo_rate(args.config, args.steps)
         dist.barrier()
+    elif members > 1:
+        speedup = (args.steps / el) / solo_rate(args.config, args.steps)
 
     c4 = None
     if not args.no_c4 and args.config != "c4":
-        r4 = Runner("c4", local_rank, world)
+        r4 = Runner("c4", local_rank, world, devices=devices)
         c4_steps = max(10, args.steps // 8)
         t4 = timed_run(torch, dist, r4, args.proj, min(args.warmup, 5), c4_steps, 0, not args.sync)
         r4.eng.set_timing(False)
@@ -444,16 +506,31 @@ def main():
         r4.close()
         if world > 1:
             dist.barrier()
-        c4 = {"workload": CONFIGS["c4"][5] + f", K-sharded over {world} GPU(s)", "global_K": CONFIGS["c4"][0],
-              "k_per_gpu": kl4, "steps": c4_steps, "steps_per_s": round(c4_steps / t4, 3),
-              "ms_per_step": round(t4 / c4_steps * 1e3, 4)}
+        c4 = {"workload": CONFIGS["c4"][5] + f", K-sharded over {members} member(s) on {n_gpus} GPU(s)",
+              "global_K": CONFIGS["c4"][0], "k_per_gpu": kl4, "steps": c4_steps,
+              "steps_per_s": round(c4_steps / t4, 3), "ms_per_step": round(t4 / c4_steps * 1e3, 4)}
         if world > 1:
             sp = None
             if rank == 0:
                 sp = (c4_steps / t4) / solo_rate("c4", c4_steps)
                 c4["speedup_vs_1"] = round(sp, 3)
             dist.barrier()
+        elif members > 1:
+            c4["speedup_vs_1"] = round((c4_steps / t4) / solo_rate("c4", c4_steps), 3)
 
+    if world > 1:
+        launcher = "torch.distributed.run: one process per GPU, ShardedMPPI, all_gather_into_tensor over RCCL"
+        parallelism = (f"K-sharded dp{world}, one RCCL all_gather of a {record_bytes}-byte record per rank "
+                       f"per step")
+    elif devices is not None:
+        launcher = ("one process, C-ABI group (mppi_group_create), member threads" +
+                    (", ncclCommInitAll + ncclAllGather" if group_info and group_info["rccl"] else
+                     ", device-copy record exchange (members share a GPU)"))
+        parallelism = (f"K-sharded over {members} members on {n_gpus} GPU(s), one all-gather of a "
+                       f"{record_bytes}-byte record per member per step")
+    else:
+        launcher = "single process"
+        parallelism = "single GPU"
     if rank == 0:
         steps_per_s = args.steps / el
         k_avg_ms = roll_ms / max(n_roll, 1)
@@ -466,7 +543,7 @@ def main():
             "metric": "MPPI steps/sec at K=65536 H=100 on 750x750 costmap; 1/2/4/8-GPU scaling",
             "value": round(steps_per_s, 3),
             "unit": "MPPI steps/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 4),
@@ -480,8 +557,9 @@ def main():
                 "global_K": K,
                 "k_per_gpu": k_local,
                 "H": H,
-                "parallelism": (f"K-sharded dp{world}, one RCCL all_gather of a {record_bytes}-byte record "
-                                f"per rank per step") if world > 1 else "single GPU",
+                "parallelism": parallelism,
+                "launcher": launcher,
+                "group": group_info,
                 "record_bytes_per_rank": record_bytes,
                 "speedup_vs_1": round(speedup, 3) if speedup is not None else None,
                 "rollout_kernel": info,
@@ -507,9 +585,9 @@ def main():
         }
         if c4 is not None:
             rec["c4"] = c4
-        if world == 1 and not args.no_bilinear:
+        if world == 1 and devices is None and not args.no_bilinear:
             rec["bilinear_roofline"] = bilinear_bench(torch, torch.device("cuda", local_rank))
-        if world == 1 and not args.no_c5 and args.config != "c5":
+        if world == 1 and devices is None and not args.no_c5 and args.config != "c5":
             r5 = Runner("c5", local_rank, 1, solo=True)
             t5 = timed_run(torch, None, r5, args.proj, 10, 50, 0, not args.sync)
             timed_run(torch, None, r5, args.proj, 2, 10, 100, not args.sync, kernel_timing=True)
@@ -522,7 +600,7 @@ def main():
                          "finish_kernel_avg_ms": round(fin5 / max(n5, 1), 4),
                          "rollout_achieved_GBs": round(alg5 / (k5 * 1e-3) / 1e9, 1),
                          "rollout_frac_of_hbm_peak": round(alg5 / (k5 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-        if world == 1 and not args.no_costmap:
+        if world == 1 and devices is None and not args.no_costmap:
             rec["costmap_builder"] = costmap_bench(local_rank, cpu=args.cpu_baseline_seconds > 0)
         if cpu is not None:
             rec["cpu_baseline"] = cpu

@@ -8,12 +8,16 @@
 #include <rccl/rccl.h>  // types only: RCCL is opened with dlopen by mppi_group_create
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -142,6 +146,7 @@ struct mppi_ctx {
                                // 2 also with the deferred optimal rollout (MPPI_FUSED)
   int fused_noise_groups = -1; // noise of step + 2 in the launch: -1 one workgroup per CU the finish leaves,
                                // n > 0 n workgroups, 0 before the launch on the context stream (MPPI_FUSED_NOISE_GROUPS)
+  uint64_t fused_wait_ticks = 200000000ull;  // fused finish's record wait bound (2 s at 100 MHz; mppi_set_option)
   int noise_gpc = 0;  // noise kernel workgroups per CU: 0 auto = 4 (measured: profiles/r02_notes.md) (MPPI_NOISE_GPC)
   hipEvent_t ev_roll_done = nullptr;
   hipEvent_t ev_prev_roll = nullptr;  // recorded after the last rollout that read an eps slot
@@ -157,6 +162,7 @@ struct mppi_ctx {
   size_t bin_t_cap = 0;
   // the finish the last step ran (mppi_get_launch_info): 1 column-split, 0 record tree
   int fin_kind = -1, fin_P = 0, fin_ncol = 0, fin_groups = 0;
+  bool last_fused = false;  // the last step ran as one fused launch (mppi_get_launch_info info[11])
   // last step (for dump)
   bool have_last = false;
   int last_proj = 3, last_mode = 0;
@@ -477,6 +483,12 @@ int sync_tail(mppi_ctx* c) {
   return MPPI_OK;
 }
 
+// Zero the finish handoff counters (level1_cnt[0]) and the fused launch's record counter
+// ([16]) after a step that did not complete them; the context stream must be idle.
+void rearm_counters(mppi_ctx* c) {
+  if (hipMemsetAsync(c->level1_cnt, 0, 128, c->stream) == hipSuccess) hipStreamSynchronize(c->stream);
+}
+
 // Spin until the finish kernel has published c->seq (all outputs in pinned host
 // memory); a fault surfaces through hipStreamQuery.
 int wait_done(mppi_ctx* c) {
@@ -489,6 +501,9 @@ int wait_done(mppi_ctx* c) {
       const hipError_t e = hipStreamQuery(c->stream);
       if (e == hipSuccess) {
         if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == c->seq) return MPPI_OK;
+        // a finish that gave up waiting for records (fused launch) left its counters mid-count:
+        // re-arm them (the stream is idle) so that the next step starts from zero
+        rearm_counters(c);
         return fail(MPPI_EHIP, "finish kernel retired without publishing its outputs");
       }
       if (e != hipErrorNotReady) return fail(MPPI_EHIP, std::string("step failed: ") + hipGetErrorString(e));
@@ -849,9 +864,10 @@ bool fused_shape(const mppi_ctx* c, const Plan& pl, int mode, int* P, int* ncol,
   if (!c->fused || (c->async_tail && c->fused < 2)) return false;
   if (mode != 0 || !pl.roles || !c->colfin || c->noise_at != 0 || pl.blocks < 1) return false;
   size_t cf_lds = 0;
-  if (!colfin_shape(pl.blocks, H_of(c), P, ncol, groups, &cf_lds)) return false;
+  // the finish runs in the workgroups holding the last `groups` tickets: at most one per rollout workgroup
+  if (!colfin_shape(pl.blocks, H_of(c), P, ncol, groups, &cf_lds, pl.blocks)) return false;
   *lds = std::max({pl.lds_bytes, cf_lds, pl.fin_lds_bytes});
-  return *lds <= 160 * 1024;
+  return *lds + 64 <= kLdsBytes;  // + the kernel's static ticket words
 }
 
 int enqueue_fused(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int ncol, int groups, size_t lds) {
@@ -915,6 +931,7 @@ int enqueue_fused(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, i
   z.fin_ncol = ncol;
   z.fin_groups = groups;
   z.rec_cnt = c->level1_cnt + 16;
+  z.wait_ticks = c->fused_wait_ticks;
   c->fin_kind = 1;
   c->fin_P = P;
   c->fin_ncol = ncol;
@@ -936,7 +953,8 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   const Plan pl = make_plan(c);
   int fP = 0, fcol = 0, fgroups = 0;
   size_t flds = 0;
-  if (fused_shape(c, pl, mode, &fP, &fcol, &fgroups, &flds)) {
+  c->last_fused = fused_shape(c, pl, mode, &fP, &fcol, &fgroups, &flds);
+  if (c->last_fused) {
     rc = enqueue_fused(c, proj, step, pl, fP, fcol, fgroups, flds);
     if (rc) return rc;
     if (c->trace) c->tr_t1 = now_us();
@@ -1399,6 +1417,7 @@ int mppi_step_partial(mppi_ctx* c, int32_t proj, uint64_t step, double* record_d
   if (rc) return rc;
   if (!record_dev) return fail(MPPI_EINVAL, "null record buffer");
   const Plan pl = make_plan(c);
+  c->last_fused = false;
   rc = enqueue_rollout(c, proj, step, 0, pl, c->u_nom[c->cur], c->st, nullptr);
   if (rc) return rc;
   remember(c, proj, step, 0, pl);
@@ -1466,6 +1485,17 @@ int mppi_dump_rollouts(mppi_ctx* c, float* traj, float* hv, float* lw, float* rw
   return out_rc;
 }
 
+int mppi_set_option(mppi_ctx* c, const char* name, int64_t value) {
+  if (!c || !name) return fail(MPPI_EINVAL, "null argument");
+  const std::string n(name);
+  if (n == "fused_wait_ticks") {
+    if (value < 0) return fail(MPPI_EINVAL, "fused_wait_ticks must be >= 0");
+    c->fused_wait_ticks = (uint64_t)value;
+    return MPPI_OK;
+  }
+  return fail(MPPI_EINVAL, "unknown option '" + n + "'");
+}
+
 int mppi_set_timing(mppi_ctx* c, int32_t enable) {
   if (!c) return fail(MPPI_EINVAL, "null context");
   int rc = sync_tail(c);
@@ -1516,9 +1546,9 @@ int mppi_get_timing(mppi_ctx* c, double* roll, double* fin, int64_t* n) {
 int mppi_get_launch_info(mppi_ctx* c, int64_t* info, int32_t n) {
   if (!c || !info) return fail(MPPI_EINVAL, "null argument");
   const Plan& pl = c->last_plan;
-  const int64_t v[11] = {0, pl.block, pl.blocks, pl.W, pl.Wr, (int64_t)pl.lds_bytes, c->fin_kind,
-                         c->fin_P, c->fin_ncol, c->fin_groups, pl.ucache_steps};
-  for (int i = 0; i < n && i < 11; ++i) info[i] = v[i];
+  const int64_t v[12] = {0, pl.block, pl.blocks, pl.W, pl.Wr, (int64_t)pl.lds_bytes, c->fin_kind,
+                         c->fin_P, c->fin_ncol, c->fin_groups, pl.ucache_steps, c->last_fused ? 1 : 0};
+  for (int i = 0; i < n && i < 12; ++i) info[i] = v[i];
   return MPPI_OK;
 }
 
@@ -1767,6 +1797,7 @@ struct RcclApi {
   ncclResult_t (*group_start)() = nullptr;
   ncclResult_t (*group_end)() = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
+  ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
 };
 // RCCL from the process (torch may already hold one) or librccl.so.1; nullptr if unavailable
 const RcclApi* rccl_api(std::string& why) {
@@ -1787,6 +1818,7 @@ const RcclApi* rccl_api(std::string& why) {
       api.group_start = reinterpret_cast<decltype(api.group_start)>(dlsym(h, "ncclGroupStart"));
       api.group_end = reinterpret_cast<decltype(api.group_end)>(dlsym(h, "ncclGroupEnd"));
       api.error_string = reinterpret_cast<decltype(api.error_string)>(dlsym(h, "ncclGetErrorString"));
+      api.comm_count = reinterpret_cast<decltype(api.comm_count)>(dlsym(h, "ncclCommCount"));
       if (!api.comm_init_all || !api.comm_destroy || !api.all_gather || !api.group_start || !api.group_end)
         err = "RCCL lacks ncclCommInitAll / ncclAllGather / ncclGroupStart";
     }
@@ -1807,7 +1839,141 @@ struct mppi_group {
   std::vector<double> empty_rec;  // the empty record (m = +inf, S = V = 0) for empty shards
   bool use_rccl = false;
   std::vector<ncclComm_t> comm;
+  // Member threads (members 1..n-1; member 0 runs on the caller's thread).  Every member
+  // enqueues its own partial step, exchange and finish and waits for its own completion word,
+  // so the n enqueue paths (a few kernel launches + events each) run side by side instead of
+  // one after another on the caller's thread (which skewed member n-1's rollout start by n
+  // enqueue paths).  Handshake: the caller publishes the step (proj, step, out) and bumps `gen`;
+  // each worker runs its member and decrements `pending`.  Workers spin for a short while after
+  // each step (a control loop calls again within microseconds) and then sleep on the condition
+  // variable.  One RCCL communicator per member, each driven only by its member's thread (the
+  // one-thread-per-device use of ncclCommInitAll communicators: no group call needed).
+  bool threaded = false;
+  std::vector<std::thread> workers;
+  std::atomic<uint64_t> gen{0};
+  std::atomic<int> pending{0};
+  std::atomic<int> recorded{0};   // copy exchange: members whose record event is recorded
+  std::atomic<int> sleepers{0};
+  std::atomic<bool> stop{false};
+  std::mutex mu;
+  std::condition_variable cv;
+  int cur_proj = 3;
+  uint64_t cur_step = 0;
+  mppi_outputs* cur_out = nullptr;
+  std::vector<int> rc;
+  std::vector<std::string> err;
 };
+
+namespace {
+
+// Member i's partial step: rollout + its record (an empty member contributes the empty record).
+int group_partial(mppi_group* g, int i, int proj, uint64_t step) {
+  mppi_ctx* c = g->ctx[i];
+  HIP_TRY(hipSetDevice(g->dev[i]));
+  if (g->count[i] > 0) return mppi_step_partial(c, proj, step, g->rec[i]);
+  HIP_TRY(hipMemcpyAsync(g->rec[i], g->empty_rec.data(), (size_t)g->E * sizeof(double), hipMemcpyHostToDevice,
+                         c->stream));
+  return MPPI_OK;
+}
+
+// Member i receives every member's record into gathered[i] (device copies, members that share
+// a device or the device-copy mode): wait for each record's event, then a peer copy.
+int group_copy_in(mppi_group* g, int i) {
+  const size_t bytes = (size_t)g->E * sizeof(double);
+  HIP_TRY(hipSetDevice(g->dev[i]));
+  for (int j = 0; j < g->n; ++j) {
+    HIP_TRY(hipStreamWaitEvent(g->ctx[i]->stream, g->ev[j], 0));
+    HIP_TRY(hipMemcpyPeerAsync(g->gathered[i] + (size_t)j * g->E, g->dev[i], g->rec[j], g->dev[j], bytes,
+                               g->ctx[i]->stream));
+  }
+  return MPPI_OK;
+}
+
+// Member i combines the n records in member order, runs the finish and waits for its outputs.
+int group_finish(mppi_group* g, int i, mppi_outputs* out) {
+  mppi_ctx* c = g->ctx[i];
+  HIP_TRY(hipSetDevice(g->dev[i]));
+  const Plan pl = c->have_last ? c->last_plan : make_plan(c);
+  int rc = enqueue_finish(c, pl, c->st, g->gathered[i], g->n, 1, nullptr, true);
+  if (rc) return rc;
+  rc = flush_speculation(c);
+  if (rc) return rc;
+  return copy_outputs(c, out);
+}
+
+// One member's whole step on its own thread (threaded groups).
+int group_member_step(mppi_group* g, int i) {
+  int rc = group_partial(g, i, g->cur_proj, g->cur_step);
+  if (!g->use_rccl) {  // every member's record event must be recorded before anyone waits on it
+    if (rc == MPPI_OK && hipEventRecord(g->ev[i], g->ctx[i]->stream) != hipSuccess)
+      rc = fail(MPPI_EHIP, "group: hipEventRecord failed");
+    g->recorded.fetch_add(1, std::memory_order_acq_rel);
+    while (g->recorded.load(std::memory_order_acquire) < g->n) __builtin_ia32_pause();
+    if (rc) return rc;
+    rc = group_copy_in(g, i);
+  } else if (rc == MPPI_OK) {
+    std::string why;
+    const RcclApi* api = rccl_api(why);
+    if (!api) return fail(MPPI_EHIP, "group: " + why);
+    const ncclResult_t r = api->all_gather(g->rec[i], g->gathered[i], (size_t)g->E, ncclFloat64, g->comm[i],
+                                           g->ctx[i]->stream);
+    if (r != ncclSuccess)
+      return fail(MPPI_EHIP, std::string("group: ncclAllGather: ") + (api->error_string ? api->error_string(r) : "error"));
+  }
+  if (rc) return rc;
+  return group_finish(g, i, i == 0 ? g->cur_out : nullptr);
+}
+
+void group_worker(mppi_group* g, int i) {
+  hipSetDevice(g->dev[i]);
+  uint64_t seen = g->gen.load(std::memory_order_acquire);
+  for (;;) {
+    const auto t0 = std::chrono::steady_clock::now();
+    uint64_t now;
+    for (int spin = 0; (now = g->gen.load(std::memory_order_acquire)) == seen && !g->stop.load(); ++spin) {
+      if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) {
+        std::unique_lock<std::mutex> lk(g->mu);
+        g->sleepers.fetch_add(1);
+        g->cv.wait(lk, [&] { return g->gen.load() != seen || g->stop.load(); });
+        g->sleepers.fetch_sub(1);
+      } else {
+        __builtin_ia32_pause();
+      }
+    }
+    if (g->stop.load()) return;
+    seen = now;
+    const int rc = group_member_step(g, i);
+    g->rc[i] = rc;
+    if (rc) g->err[i] = g_err;
+    g->pending.fetch_sub(1, std::memory_order_acq_rel);
+  }
+}
+
+// The caller's thread: publish the step, run member 0, wait for the others.
+int group_step_threaded(mppi_group* g, int proj, uint64_t step, mppi_outputs* out) {
+  g->cur_proj = proj;
+  g->cur_step = step;
+  g->cur_out = out;
+  for (int i = 0; i < g->n; ++i) {
+    g->rc[i] = MPPI_OK;
+    g->err[i].clear();
+  }
+  g->recorded.store(0, std::memory_order_relaxed);
+  g->pending.store(g->n - 1, std::memory_order_relaxed);
+  {
+    std::lock_guard<std::mutex> lk(g->mu);  // a worker about to sleep sees the new generation
+    g->gen.fetch_add(1, std::memory_order_acq_rel);
+  }
+  if (g->sleepers.load() > 0) g->cv.notify_all();
+  g->rc[0] = group_member_step(g, 0);
+  if (g->rc[0]) g->err[0] = g_err;
+  while (g->pending.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
+  for (int i = 0; i < g->n; ++i)
+    if (g->rc[i]) return fail(g->rc[i], "group member " + std::to_string(i) + ": " + g->err[i]);
+  return MPPI_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -1872,12 +2038,33 @@ int mppi_group_create(const mppi_params* params, int32_t n, const int32_t* devic
     }
     g->use_rccl = true;
   }
+  // member threads (MPPI_GROUP_THREADS=0: every member enqueued from the caller's thread)
+  const char* et = std::getenv("MPPI_GROUP_THREADS");
+  g->threaded = n > 1 && !(et && std::atoi(et) == 0);
+  g->rc.assign(n, MPPI_OK);
+  g->err.assign(n, std::string());
+  if (g->threaded) {
+    try {
+      for (int i = 1; i < n; ++i) g->workers.emplace_back(group_worker, g, i);
+    } catch (const std::exception& ex) {
+      return bail(fail(MPPI_EHIP, std::string("group: worker threads: ") + ex.what()));
+    }
+  }
   *out = g;
   return MPPI_OK;
 }
 
 void mppi_group_destroy(mppi_group* g) {
   if (!g) return;
+  if (!g->workers.empty()) {
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      g->stop.store(true);
+    }
+    g->cv.notify_all();
+    for (auto& t : g->workers)
+      if (t.joinable()) t.join();
+  }
   std::string why;
   const RcclApi* api = g->comm.empty() ? nullptr : rccl_api(why);
   for (size_t i = 0; i < g->comm.size(); ++i)
@@ -1907,27 +2094,37 @@ int mppi_group_shard(mppi_group* g, int32_t i, int64_t* begin, int64_t* count) {
   return MPPI_OK;
 }
 
+int mppi_group_info(mppi_group* g, int64_t* info, int32_t n) {
+  if (!g || !info) return fail(MPPI_EINVAL, "null argument");
+  int ranks = 0;
+  if (g->use_rccl && !g->comm.empty()) {
+    std::string why;
+    const RcclApi* api = rccl_api(why);
+    if (api && api->comm_count) api->comm_count(g->comm[0], &ranks);
+  }
+  std::vector<int> devs(g->dev);
+  std::sort(devs.begin(), devs.end());
+  const int64_t distinct = std::unique(devs.begin(), devs.end()) - devs.begin();
+  const int64_t v[5] = {g->n, distinct, g->use_rccl ? 1 : 0, ranks, g->threaded ? 1 : 0};
+  for (int i = 0; i < n && i < 5; ++i) info[i] = v[i];
+  return MPPI_OK;
+}
+
 int mppi_group_step(mppi_group* g, int32_t proj, uint64_t step, mppi_outputs* out) {
   if (!g) return fail(MPPI_EINVAL, "null group");
   if (g->n == 1 && !g->use_rccl) return mppi_step(g->ctx[0], proj, step, out);
+  if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
   const int n = g->n;
-  const size_t bytes = (size_t)g->E * sizeof(double);
   for (int i = 0; i < n; ++i) {
     const int rc = check_ready(g->ctx[i]);  // every member (an empty one runs the finish) needs its scene
     if (rc) return rc;
   }
-  // 1. every member's rollout and record, on its own stream
+  if (g->threaded) return group_step_threaded(g, proj, step, out);
+  // one thread: every member's rollout and record, the exchange, every member's finish
   for (int i = 0; i < n; ++i) {
-    mppi_ctx* c = g->ctx[i];
-    HIP_TRY(hipSetDevice(g->dev[i]));
-    if (g->count[i] > 0) {
-      const int rc = mppi_step_partial(c, proj, step, g->rec[i]);
-      if (rc) return rc;
-    } else {
-      HIP_TRY(hipMemcpyAsync(g->rec[i], g->empty_rec.data(), bytes, hipMemcpyHostToDevice, c->stream));
-    }
+    const int rc = group_partial(g, i, proj, step);
+    if (rc) return rc;
   }
-  // 2. the exchange
   if (g->use_rccl) {
     std::string why;
     const RcclApi* api = rccl_api(why);
@@ -1945,15 +2142,10 @@ int mppi_group_step(mppi_group* g, int32_t proj, uint64_t step, mppi_outputs* ou
       HIP_TRY(hipEventRecord(g->ev[i], g->ctx[i]->stream));
     }
     for (int i = 0; i < n; ++i) {
-      HIP_TRY(hipSetDevice(g->dev[i]));
-      for (int j = 0; j < n; ++j) {
-        HIP_TRY(hipStreamWaitEvent(g->ctx[i]->stream, g->ev[j], 0));
-        HIP_TRY(hipMemcpyPeerAsync(g->gathered[i] + (size_t)j * g->E, g->dev[i], g->rec[j], g->dev[j], bytes,
-                                   g->ctx[i]->stream));
-      }
+      const int rc = group_copy_in(g, i);
+      if (rc) return rc;
     }
   }
-  // 3. every member combines the records in member order and runs the finish; then the outputs
   for (int i = 0; i < n; ++i) {
     mppi_ctx* c = g->ctx[i];
     HIP_TRY(hipSetDevice(g->dev[i]));

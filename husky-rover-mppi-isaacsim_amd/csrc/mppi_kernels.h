@@ -113,9 +113,11 @@ hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hip
 // trajectories; rings [D][4 + 4][TB] + cost[TB] + slope[TB] in LDS.
 constexpr int ROLES_WAVES_PER_TRAJ_WAVE = 4;
 // One launch per step (mppi_step_fused_kernel): the role-split rollout's nroll workgroups, then
-// fin_groups column-split finish workgroups (colfin_shape; they wait for rec_cnt == nroll, records
-// written through), then noise_groups workgroups generating the normals of Philox block base
-// noise_n_base into noise_eps (none when noise_groups == 0).  rec_cnt: zeroed, re-armed in-kernel.
+// noise_groups workgroups generating the normals of Philox block base noise_n_base into noise_eps
+// (none when noise_groups == 0).  The rollout workgroups holding the last fin_groups tickets of
+// rec_cnt (fin_groups <= nroll) then run the column-split finish (colfin_shape), each after
+// rec_cnt reaches nroll (records written through) or wait_ticks of the 100 MHz clock (then it
+// publishes nothing).  rec_cnt: zeroed, re-armed in-kernel (and by the host after a failed step).
 struct FusedArgs {
   FinishArgs f;
   int nroll, fin_P, fin_ncol, fin_groups;
@@ -123,6 +125,7 @@ struct FusedArgs {
   float* noise_eps;
   uint64_t noise_n_base;
   int noise_groups;
+  uint64_t wait_ticks;
 };
 hipError_t launch_step_fused(const RolloutArgs& a, const FusedArgs& z, size_t lds, hipStream_t st, int proj);
 // record tree finish (mppi_finish_kernel): the fallback where the column-split shape does not fit
@@ -130,7 +133,8 @@ hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, int gr
 // column-split finish: every workgroup builds the pair-scale table and reduces ncol columns
 // over all n records; the last to arrive runs phase 2 (f.level1 holds >= 2H floats, f.level1_cnt
 // a zeroed counter).  colfin_shape returns 0 when n is outside the kernel's range.
-int colfin_shape(int n, int H, int* P, int* ncol, int* groups, size_t* lds_tree);
+// (at most max_groups workgroups: more columns each).
+int colfin_shape(int n, int H, int* P, int* ncol, int* groups, size_t* lds_tree, int max_groups = 1 << 30);
 hipError_t launch_colfin(const FinishArgs& f, size_t lds, hipStream_t st, int P, int ncol, int groups);
 // optimal rollout of the sequence a mode-2 finish left in f.tail_in (one workgroup)
 constexpr int TAIL_THREADS = 256;

@@ -1572,8 +1572,10 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 #endif
 constexpr int ROLE_CHAIN = 0, ROLE_PROD = 1, ROLE_WHEEL = 2, ROLE_COST = 3, NROLES = 4;
 
+// FUSED: returns the workgroup's ticket (its rank among the workgroups that have completed their
+// records, from the record counter rec_cnt); otherwise -1.
 template <int TB, int PROJ, int MODE, bool DUMP, bool FUSED>
-__device__ __forceinline__ void roles_body(const RolloutArgs& a, unsigned* rec_cnt) {
+__device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cnt, int* ticket_lds = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   constexpr int NT = NROLES * TB;
   constexpr int NG = TB / 64;  // trajectory groups (waves per role)
@@ -1913,12 +1915,17 @@ __device__ __forceinline__ void roles_body(const RolloutArgs& a, unsigned* rec_c
   if constexpr (FUSED) {  // the record is written through: count it (D8: complete, then a relaxed count)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (tid == 0) {
 #if MPPI_COLFIN_FENCED
-    if (tid == 0) __hip_atomic_fetch_add(rec_cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      *ticket_lds = (int)__hip_atomic_fetch_add(rec_cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 #else
-    if (tid == 0) __hip_atomic_fetch_add(rec_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *ticket_lds = (int)__hip_atomic_fetch_add(rec_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
+    }
+    __syncthreads();
+    return *ticket_lds;
   }
+  return -1;
 }
 
 template <int TB, int PROJ, int MODE, bool DUMP>
@@ -3054,13 +3061,13 @@ hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, int gr
 
 // Column-split finish (mppi_colfin_kernel): P = leaves padded to a power of two >= 16,
 // ncol columns per workgroup; returns the LDS bytes the tree needs in *lds_tree.
-int colfin_shape(int n, int H, int* P_out, int* ncol_out, int* groups_out, size_t* lds_tree) {
-  if (n < 1 || n > COLFIN_PMAX) return 0;
+int colfin_shape(int n, int H, int* P_out, int* ncol_out, int* groups_out, size_t* lds_tree, int max_groups) {
+  if (n < 1 || n > COLFIN_PMAX || max_groups < 1) return 0;
   int P = 16;
   while (P < n) P *= 2;
   const int E = 2 * H + 2;
-  // about 64 workgroups, at least 2 columns each
-  const int ncol = std::max(2, (E + 63) / 64);
+  // about 64 workgroups, at least 2 columns each (at most max_groups workgroups)
+  const int ncol = std::max({2, (E + 63) / 64, (E + max_groups - 1) / max_groups});
   if ((ncol + 1) * (P / 16) > FIN_THREADS) return 0;  // one (column, group) item per thread
   const int groups = (E + ncol - 1) / ncol;
   *P_out = P;
@@ -3160,54 +3167,56 @@ __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t
 }
 
 // =====================================================================  fused step launch
-// One launch per MPPI step: workgroups [0, nroll) are the role-split rollout (each counts its
-// record once it is written through), [nroll, nroll + fin_groups) the column-split finish
-// (each waits for the count, then reduces its columns; the last runs phase 2 and re-arms the
-// count), and the rest generate the normals of a later step (noise_rows, four 256-trajectory
-// rows per workgroup).  Workgroups are dispatched in index order, so the finish and noise
-// workgroups take CUs as rollout workgroups retire: no kernel boundary between rollout and
-// finish, no event between the rollout and the noise, the noise beside the finish as before.
-// A finish workgroup only waits on rollout workgroups dispatched before it (no deadlock).
+// One launch per MPPI step: workgroups [0, nroll) are the role-split rollout, the rest generate
+// the normals of a later step (noise_rows, four 256-trajectory rows per workgroup).  Each rollout
+// workgroup writes its record through, completes it and takes a ticket from the record counter
+// (its rank among the finished rollout workgroups).  The workgroups holding the last fin_groups
+// tickets stay on as the column-split finish: finish workgroup t - (nroll - fin_groups) waits
+// until all nroll records are counted, reduces its columns, and the last of them runs phase 2
+// and re-arms the counters.  No assumption on the dispatch order: a waiting finish workgroup has
+// finished its own rollout, at most fin_groups - 1 < (workgroup slots of the device) of them wait
+// at once, and every rollout workgroup not yet counted either runs or gets a slot as others
+// retire.  No kernel boundary between rollout and finish, no event between rollout and noise.
 template <int TB, int PROJ>
 __global__ __launch_bounds__(NROLES * TB) void mppi_step_fused_kernel(const RolloutArgs a, const FusedArgs z) {
   const int b = (int)blockIdx.x;
   if (b < z.nroll) {
-    roles_body<TB, PROJ, 0, false, true>(a, z.rec_cnt);
-    return;
-  }
-  if (b < z.nroll + z.fin_groups) {
-    __shared__ int timed_out;
-    if (threadIdx.x == 0) {  // bounded (2 s of the 100 MHz clock): a lost count cannot hang the device
+    __shared__ int sh[2];
+    const int ticket = roles_body<TB, PROJ, 0, false, true>(a, z.rec_cnt, sh);
+    const int blk = ticket - (z.nroll - z.fin_groups);
+    if (blk < 0) return;
+    __builtin_amdgcn_s_setprio(0);  // the rollout waves' priorities do not carry into the finish
+    if (threadIdx.x == 0) {  // bounded (z.wait_ticks of the 100 MHz clock): a lost count cannot hang the device
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      int late = 0;
-      while (__hip_atomic_load(z.rec_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)z.nroll) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 >= 200000000ull) {
+      int late = z.wait_ticks == 0;  // 0: give up at once (the test hook of mppi_set_option)
+      while (!late && __hip_atomic_load(z.rec_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)z.nroll) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 >= z.wait_ticks) {
           late = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(2);
       }
-      timed_out = late;
+      sh[1] = late;
     }
     __syncthreads();
     // a finish without all records publishes nothing: the host's wait reports the step as failed
-    // ("finish kernel retired without publishing its outputs") instead of returning wrong controls
-    if (timed_out) return;
+    // ("finish kernel retired without publishing its outputs") and re-arms the counters
+    if (sh[1]) return;
 #if MPPI_COLFIN_FENCED
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #endif
-    colfin_body<true>(z.f, z.fin_P, z.fin_ncol, b - z.nroll, z.fin_groups, z.rec_cnt);
+    colfin_body<true>(z.f, z.fin_P, z.fin_ncol, blk, z.fin_groups, z.rec_cnt);
     return;
   }
-  const int nb = (int)gridDim.x - z.nroll - z.fin_groups;
+  const int nb = (int)gridDim.x - z.nroll;
   const int sub = threadIdx.x >> 8;  // NROLES * TB / 256 rows in flight per workgroup
   noise_rows(a.seed, z.noise_n_base, a.k_offset, a.H, z.nroll, z.noise_eps,
-             (int64_t)(b - z.nroll - z.fin_groups) * (NROLES * TB / 256) + sub, (int64_t)nb * (NROLES * TB / 256),
+             (int64_t)(b - z.nroll) * (NROLES * TB / 256) + sub, (int64_t)nb * (NROLES * TB / 256),
              threadIdx.x & 255);
 }
 
 hipError_t launch_step_fused(const RolloutArgs& a, const FusedArgs& z, size_t lds, hipStream_t st, int proj) {
-  const dim3 g((unsigned)(z.nroll + z.fin_groups + z.noise_groups)), b(NROLES * 256);
+  const dim3 g((unsigned)(z.nroll + z.noise_groups)), b(NROLES * 256);
   if (proj == 3)
     hipLaunchKernelGGL((mppi_step_fused_kernel<256, 3>), g, b, lds, st, a, z);
   else

@@ -87,6 +87,7 @@ _PROTOS = {
     "mppi_get_costs": (C.c_int, [C.c_void_p, _FP, C.c_int64]),
     "mppi_dump_rollouts": (C.c_int, [C.c_void_p] + [_FP] * 8),
     "mppi_set_timing": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mppi_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
     "mppi_get_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_int64)]),
     "mppi_get_tail_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
@@ -112,6 +113,7 @@ _PROTOS = {
     "mppi_group_context": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
     "mppi_group_shard": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "mppi_group_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.POINTER(MppiOutputs)]),
+    "mppi_group_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]),
     "mppi_rollout_python25d": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, _DP, _DP, _DP, _DP, _DP, C.c_double,
                                          C.c_double, C.c_double, C.c_double, _DP, C.POINTER(C.c_int32)]),
 }
@@ -436,6 +438,10 @@ class Engine:
                 "mppi_dump_rollouts")
         return arrs
 
+    def set_option(self, name, value):
+        """mppi_set_option (include/mppi.h): per-context tuning / test hooks by name."""
+        self._c(self.lib.mppi_set_option(self.ctx, name.encode(), int(value)), "mppi_set_option")
+
     def set_timing(self, on=True):
         """on: False / True (rollout, finish and tail events) or 2 (rollout and finish only)."""
         mode = on if isinstance(on, int) and not isinstance(on, bool) else (1 if on else 0)
@@ -455,10 +461,10 @@ class Engine:
         return t.value, n.value
 
     def launch_info(self):
-        info = (C.c_int64 * 11)()
-        self._c(self.lib.mppi_get_launch_info(self.ctx, info, 11), "mppi_get_launch_info")
+        info = (C.c_int64 * 12)()
+        self._c(self.lib.mppi_get_launch_info(self.ctx, info, 12), "mppi_get_launch_info")
         keys = ("reserved", "block", "blocks", "window_cols", "window_rows", "lds_bytes", "finish_kind",
-                "finish_records", "finish_ncol", "finish_groups", "ucache_steps")
+                "finish_records", "finish_ncol", "finish_groups", "ucache_steps", "fused")
         return dict(zip(keys, [int(v) for v in info]))
 
     def selftest(self, what, n=1 << 24, seed=1):
@@ -494,9 +500,12 @@ class Group:
     """mppi_group (include/mppi.h): one controller over n GPUs from one process.
 
     Member i is an Engine over the contiguous shard mppi_group_shard(i) of the K trajectories;
-    setters broadcast to every member; step() enqueues every member's rollout, all-gathers the
-    records (RCCL between distinct devices, device copies when members share one) and returns the
-    outputs, bitwise equal to one context over all K.
+    setters broadcast to every member; step() runs every member's rollout (each member's launches
+    enqueued by its own thread), all-gathers the records (RCCL between distinct devices, device
+    copies when members share one) and returns the outputs.  When every member's shard is a
+    power-of-two number of 256-trajectory leaves the member roots are subtrees of the one-context
+    tree and the step is bitwise equal to one context over all K; other splits (e.g. 3 members,
+    ragged K) run the same float64 combine with a different pairing.
     """
 
     def __init__(self, params: MppiParams, devices):
@@ -527,6 +536,12 @@ class Group:
     def __len__(self):
         return len(self.members)
 
+    def info(self):
+        """mppi_group_info: members, distinct devices, RCCL in use, RCCL ranks, member threads."""
+        v = (C.c_int64 * 5)()
+        _check(self.lib, self.lib.mppi_group_info(self.h, v, 5), "mppi_group_info")
+        return dict(zip(("members", "devices", "rccl", "rccl_ranks", "threaded"), [int(x) for x in v]))
+
     def _each(self, name, *a, **kw):
         for m in self.members:
             getattr(m, name)(*a, **kw)
@@ -543,11 +558,21 @@ class Group:
     def set_nominal(self, u1, u2):
         self._each("set_nominal", u1, u2)
 
+    def set_async_tail(self, on=True):
+        """Deferred optimal rollout on every member (Engine.set_async_tail)."""
+        self._each("set_async_tail", on)
+
     def step(self, proj="3d", step=0, copy=True):
         m0 = self.members[0]
         _check(self.lib, self.lib.mppi_group_step(self.h, PROJ[proj], int(step), C.byref(m0._out)),
                "mppi_group_step")
         return m0._outputs() if copy else None
+
+    def outputs(self):
+        """All outputs of the last step (every member's deferred optimal rollout waited for)."""
+        for m in self.members[1:]:
+            m.outputs()
+        return self.members[0].outputs()
 
     def costs(self):
         """Every trajectory's cost in global order (the members' shards concatenated)."""

@@ -222,14 +222,20 @@ int mppi_step_finish(mppi_ctx* ctx, const double* records_dev, int32_t n_records
  * holds one context per member device, member i over trajectories
  * [begin_i, begin_i + count_i) of params->num_trajectories (256-trajectory
  * leaves split contiguously, as mppi_amd/distributed.shard_bounds), noise
- * keyed by the global trajectory index, so a group step is bitwise equal to
- * one context over all K.  mppi_group_step enqueues every member's rollout and
- * record, all-gathers the records (RCCL ncclAllGather in one group call, RCCL
- * opened with dlopen when the devices are distinct; device-to-device copies
- * when members share a device), runs every member's finish and returns member
- * 0's outputs; every member keeps the same nominal controls.  Scene, state,
- * weights and warm starts are set on each member through mppi_group_context
- * with the single-context calls above. */
+ * keyed by the global trajectory index.  When every member's shard is a
+ * power-of-two number of leaves (e.g. C4's 8 x 512) the member roots are
+ * subtrees of the one-context record tree and a group step is bitwise equal
+ * to one context over all K; other splits (3 members, ragged K) run the same
+ * float64 combine with a different pairing (D2 in DESIGN.md).
+ * mppi_group_step runs every member's rollout and record (members 1..n-1 on
+ * threads of the group, member 0 on the caller's), all-gathers the records
+ * (RCCL ncclAllGather, one communicator per member from ncclCommInitAll,
+ * RCCL opened with dlopen, when the devices are distinct; device-to-device
+ * copies when members share a device), runs every member's finish and
+ * returns member 0's outputs; every member keeps the same nominal controls.
+ * Scene, state, weights and warm starts are set on each member through
+ * mppi_group_context with the single-context calls above (not while a
+ * group step runs). */
 typedef struct mppi_group mppi_group;
 int mppi_group_create(const mppi_params* params, int32_t n, const int32_t* devices,
                       mppi_group** out);
@@ -238,6 +244,10 @@ int mppi_group_size(mppi_group* group);
 int mppi_group_context(mppi_group* group, int32_t member, mppi_ctx** out);
 int mppi_group_shard(mppi_group* group, int32_t member, int64_t* begin, int64_t* count);
 int mppi_group_step(mppi_group* group, int32_t proj, uint64_t step, mppi_outputs* out);
+/* Group facts, up to 5 values: info[0] = members, [1] = distinct devices, [2] = 1 if the records
+ * travel by RCCL (else device copies), [3] = ranks of the RCCL communicator (ncclCommCount; 0
+ * without RCCL), [4] = 1 if members 1..n-1 run on group threads. */
+int mppi_group_info(mppi_group* group, int64_t* info, int32_t n);
 
 /* ---- introspection (self.costs_wp / self.trajectories .numpy(), MPPI_isaac.py:466-470) ---- */
 /* costs of the last step's trajectories of this context [n <= K] */
@@ -251,18 +261,30 @@ int mppi_dump_rollouts(mppi_ctx* ctx, float* traj, float* heading, float* left_w
  * kernel, measured on the context stream around each launch.  enable: 0 off,
  * 1 rollout, finish and deferred-tail events (the host waits for the stream and
  * for each tail to collect them), 2 rollout events only (no host wait: the
- * pipelined schedule undisturbed; the finish time reads 0). */
+ * pipelined schedule undisturbed; the finish time reads 0).  A synchronous
+ * step that ran as ONE fused launch (rollout + finish + optimal rollout,
+ * mppi_get_launch_info info[11] = 1) is counted whole as rollout time and
+ * adds nothing to the finish time. */
 int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
+
+/* Per-context tuning and test hooks, by name (MPPI_EINVAL for an unknown name):
+ *   "fused_wait_ticks"  bound, in ticks of the 100 MHz s_memrealtime clock, on how long a
+ *                       finish workgroup of the fused step launch waits for the rollout
+ *                       records (default 2e8 = 2 s).  A finish that gives up publishes
+ *                       nothing: the step returns MPPI_EHIP and the counters are re-armed,
+ *                       so the next step is correct (0: give up at once, the test hook). */
+int mppi_set_option(mppi_ctx* ctx, const char* name, int64_t value);
 int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_t* launches);
 /* HIP-event time of the deferred optimal-rollout kernels (side stream). */
 int mppi_get_tail_timing(mppi_ctx* ctx, double* tail_ms, int64_t* launches);
 
-/* Layout/launch facts for the last step (for tests and the bench), up to 11 values:
+/* Layout/launch facts for the last step (for tests and the bench), up to 12 values:
  * info[0]=0 (reserved), [1]=rollout block threads, [2]=rollout blocks, [3]/[4]=cols/rows of
  * the DEM window the step's lanes can touch, [5]=rollout LDS bytes, [6]=finish kind (1 =
  * column-split mppi_colfin_kernel, 0 = record tree mppi_finish_kernel), [7]=records padded
  * (column-split) or records (tree), [8]=columns per finish workgroup, [9]=finish workgroups,
- * [10]=steps whose sampled controls the rollout keeps in LDS. */
+ * [10]=steps whose sampled controls the rollout keeps in LDS, [11]=1 if the step ran as one
+ * fused launch (mppi_step_fused_kernel), else 0. */
 int mppi_get_launch_info(mppi_ctx* ctx, int64_t* info, int32_t n);
 
 /* Standalone DEM bilinear kernel: for n query points

@@ -133,3 +133,40 @@ def test_timing_modes():
             eng.set_timing(3)
     finally:
         eng.close()
+
+
+def test_fused_finish_gives_up_then_recovers():
+    """A fused finish that stops waiting for the records (mppi_set_option("fused_wait_ticks", 0):
+    give up at once) publishes nothing: the step raises, the host re-arms the record and handoff
+    counters, and the next step is bitwise equal to a fresh context's (the nominal controls were
+    not touched by the failed step)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from mppi_amd import _lib, scene
+    Z, hw, cm = scene.scene_c3()
+
+    def make():
+        e = _lib.Engine(_lib.make_params(65536, 24), 0)
+        e.set_dem(Z, hw)
+        e.set_costmap(cm, hw)
+        e.set_state(_lib.make_state(-60.0, -5.0, (1.0, 0.0, 0.0), goal_x=65.0, goal_y=10.0))
+        return e
+
+    eng, ref = make(), make()
+    try:
+        eng.set_option("fused_wait_ticks", 0)
+        with pytest.raises(RuntimeError, match="without publishing"):
+            eng.step("3d", 0)
+        assert eng.launch_info()["fused"] == 1
+        eng.set_option("fused_wait_ticks", 200000000)
+        for i in (1, 2):
+            a, b = eng.step("3d", i), ref.step("3d", i)
+            for k in KEYS:
+                np.testing.assert_array_equal(a[k], b[k], err_msg=f"step {i} {k}")
+        np.testing.assert_array_equal(eng.costs(), ref.costs())
+        with pytest.raises(RuntimeError, match="unknown option"):
+            eng.set_option("no_such_option", 1)
+    finally:
+        eng.close()
+        ref.close()
