@@ -1175,6 +1175,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   *c->done = 0;
   if (hipMemset(c->level1_cnt, 0, 128) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
+
   if (hipDeviceSynchronize() != hipSuccess) return cleanup(fail(MPPI_EHIP, "device sync failed"));
   *out = c;
   return MPPI_OK;
@@ -1259,6 +1260,8 @@ static int check_grid(int32_t rows, int32_t cols, float res) {
   if (!(res > 0.0f)) return fail(MPPI_EINVAL, "DEM resolution must be > 0");
   if ((int64_t)rows * cols >= ((int64_t)1 << 29))  // kernels address cells with 32-bit byte offsets
     return fail(MPPI_EINVAL, "DEM larger than 2^29 cells");
+  if (((int64_t)rows + 1) * ((int64_t)cols + 1) * 16 >= ((int64_t)1 << 32))  // the normal table, ditto
+    return fail(MPPI_EINVAL, "DEM normal table above 4 GiB ((rows+1)*(cols+1) >= 2^28)");
   if (rows > (1 << 24) || cols > (1 << 24))  // cell bounds are clamped as exact floats
     return fail(MPPI_EINVAL, "DEM dimension above 2^24");
   return MPPI_OK;

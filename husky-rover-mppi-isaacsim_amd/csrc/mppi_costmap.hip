@@ -260,21 +260,43 @@ __device__ inline uint32_t wave_excl_min_scan_down(uint32_t v, int lane) {
   return (uint32_t)__shfl((int)x, 63 - lane, 64);
 }
 
-// CM = columns per lane (a power of two >= ceil(W / 64)): a lane's chunk of a row stays in
-// registers from its chain to its final value.
+// One workgroup of CH_T threads walks the rows of both passes; thread t owns the contiguous
+// columns [t C, t C + C) (C = ceil(W / CH_T) <= CM), so a 1024^2 map has one column per thread.
+// Per row: the thread's chunk from the three LDS rows (7 mask taps per column), its in-chunk
+// chain, then the carry of the row chain across chunks as an exclusive min-scan over the
+// workgroup (a 64-lane DPP scan inside each wave, the waves' totals through LDS), the row written
+// to LDS and global memory; two barriers per row (totals visible / row visible).  Round 2 ran the
+// same arithmetic on one wave (C = W / 64 columns per lane): 3.96 ms per 1024^2 map.
+constexpr int CH_T = 1024;
+constexpr int CH_W = CH_T / 64;  // waves
+
+// min over the waves strictly before (UP) / after (!UP) wave w of their totals tot[0..CH_W)
+template <bool UP>
+__device__ inline uint32_t waves_prefix_min(const uint32_t* tot, int w, int lane) {
+  uint32_t x = 0xFFFFFFFFu;
+  if (lane < CH_W && (UP ? lane < w : lane > w)) x = tot[lane];
+  // min over lanes 0..15 (row 0 of the wave): row_shr 1, 2, 4, 8, then lane 15 holds it
+  x = dpp_min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x111, 0xF, 0xF, false));
+  x = dpp_min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x112, 0xF, 0xF, false));
+  x = dpp_min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x114, 0xF, 0xF, false));
+  x = dpp_min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, 0x118, 0xF, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+}
+
 template <int CM>
-__global__ __launch_bounds__(64) void costmap_chamfer_kernel(const uint8_t* __restrict__ occ, int H, int W,
-                                                             uint32_t* __restrict__ tmp, float* __restrict__ dist,
-                                                             int32_t* __restrict__ range) {
-  extern __shared__ uint32_t srows[];  // [3][W + 4]
-  const int lane = threadIdx.x;
+__global__ __launch_bounds__(CH_T) void costmap_chamfer_kernel(const uint8_t* __restrict__ occ, int H, int W,
+                                                               uint32_t* __restrict__ tmp, float* __restrict__ dist,
+                                                               int32_t* __restrict__ range) {
+  extern __shared__ uint32_t srows[];  // [3][W + 4] rows, then [2][CH_W] wave totals
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int S = W + 2 * CH_B;
-  const int C = (W + 63) / 64;
-  const int j0 = min(W, lane * C), j1 = min(W, j0 + C);
-  for (int k = lane; k < 3 * S; k += 64) srows[k] = CV_INIT;
+  uint32_t* tot = srows + 3 * S;
+  const int C = (W + CH_T - 1) / CH_T;
+  const int j0 = min(W, tid * C), j1 = min(W, j0 + C);
+  for (int k = tid; k < 3 * S; k += CH_T) srows[k] = CV_INIT;
   __syncthreads();
   uint32_t loc[CM];
-  // global reads of a row are issued one row ahead (their latency would otherwise sit on every row)
+  // global reads of a row are issued one row ahead
   uint8_t ocur[CM], onext[CM];
 #pragma unroll
   for (int k = 0; k < CM; ++k) ocur[k] = j0 + k < j1 ? occ[j0 + k] : 0;
@@ -288,33 +310,29 @@ __global__ __launch_bounds__(64) void costmap_chamfer_kernel(const uint8_t* __re
     for (int k = 0; k < CM; ++k) onext[k] = j0 + k < j1 ? onrow[j0 + k] : 0;
     uint64_t run = 0xFFFFFFFFull;  // the chain inside the chunk, no left input yet
 #pragma unroll
-    for (int g = 0; g < CM; g += 8) {  // 8 columns at a time: the group's loads before its chain
-      const int jb = j0 + g;
-      uint32_t w1[12], w2[10];
-#pragma unroll
-      for (int k = 0; k < 12; ++k) w1[k] = up1[min(jb - 2 + k, W + 1)];  // up1[jb-2 .. jb+9]
-#pragma unroll
-      for (int k = 0; k < 10; ++k) w2[k] = up2[min(jb - 1 + k, W + 1)];  // up2[jb-1 .. jb+8]
-      const uint8_t* o = ocur + g;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        uint32_t t = min(w2[k] + CV_LONG, w2[k + 2] + CV_LONG);
-        t = min(t, w1[k] + CV_LONG);
-        t = min(t, w1[k + 1] + CV_DIAG);
-        t = min(t, w1[k + 2] + CV_HV);
-        t = min(t, w1[k + 3] + CV_DIAG);
-        t = min(t, w1[k + 4] + CV_LONG);
-        const uint64_t nr = o[k] ? 0ull : min((uint64_t)t, run + CV_HV);
-        run = jb + k < j1 ? nr : run;
-        loc[g + k] = (uint32_t)nr;
-      }
+    for (int k = 0; k < CM; ++k) {
+      const int j = j0 + k;
+      const int jc = min(j, W - 1);  // (columns past the chunk end are computed, not kept)
+      uint32_t t = min(up2[jc - 1] + CV_LONG, up2[jc + 1] + CV_LONG);
+      t = min(t, up1[jc - 2] + CV_LONG);
+      t = min(t, up1[jc - 1] + CV_DIAG);
+      t = min(t, up1[jc] + CV_HV);
+      t = min(t, up1[jc + 1] + CV_DIAG);
+      t = min(t, up1[jc + 2] + CV_LONG);
+      const uint64_t nr = ocur[k] ? 0ull : min((uint64_t)t, run + CV_HV);
+      run = j < j1 ? nr : run;
+      loc[k] = (uint32_t)nr;
     }
     // value at column j0 - 1: a source at column js holding v contributes v + (j - js) HV, the
     // border (INIT at column -1) INIT + (j + 1) HV; carried as v + (W - js) HV, which stays below
     // 2^32 (v < 3.3e9, W HV < 5.4e8 at W <= 8192), and the minimum exceeds (W - j) HV
     const uint32_t mine = j0 < j1 ? (uint32_t)run + (uint32_t)(W - (j1 - 1)) * CV_HV : 0xFFFFFFFFu;
-    const uint32_t carry = min(wave_excl_min_scan_up(mine), CV_INIT + (uint32_t)(W + 1) * CV_HV);
-    __syncthreads();  // every lane has read the previous rows' slots it needs (cur is written below)
+    const uint32_t incl = wave_incl_min_scan(mine);
+    const uint32_t excl = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)incl, 0x138, 0xF, 0xF, false);
+    uint32_t* tt = tot + (i & 1) * CH_W;
+    if (lane == 63) tt[wv] = incl;
+    __syncthreads();  // wave totals visible; every thread has read the rows it needs (cur written below)
+    const uint32_t carry = min(min(excl, waves_prefix_min<true>(tt, wv, lane)), CV_INIT + (uint32_t)(W + 1) * CV_HV);
 #pragma unroll
     for (int k = 0; k < CM; ++k) {
       const int j = j0 + k;
@@ -326,11 +344,11 @@ __global__ __launch_bounds__(64) void costmap_chamfer_kernel(const uint8_t* __re
     }
 #pragma unroll
     for (int k = 0; k < CM; ++k) ocur[k] = onext[k];
-    __syncthreads();
+    __syncthreads();  // row i visible
   }
-  __threadfence_block();  // the forward rows in tmp are re-read below by the same lanes only
+  __threadfence_block();  // the forward rows in tmp are re-read below by the same threads only
   // ---- backward pass: rows bottom to top, columns right to left
-  for (int k = lane; k < 3 * S; k += 64) srows[k] = CV_INIT;
+  for (int k = tid; k < 3 * S; k += CH_T) srows[k] = CV_INIT;
   __syncthreads();
   float dmin = INFINITY, dmax = -INFINITY;
   uint32_t fcur[CM], fnext[CM];
@@ -346,34 +364,31 @@ __global__ __launch_bounds__(64) void costmap_chamfer_kernel(const uint8_t* __re
     for (int k = 0; k < CM; ++k) fnext[k] = j0 + k < j1 ? tnrow[j0 + k] : 0u;
     uint64_t run = 0xFFFFFFFFull;
 #pragma unroll
-    for (int g = CM - 8; g >= 0; g -= 8) {  // right to left, 8 columns at a time
-      const int jl = j0 + g;  // columns jl .. jl + 7 (those < j1)
-      uint32_t w1[12], w2[10];
-#pragma unroll
-      for (int k = 0; k < 12; ++k) w1[k] = dn1[min(jl - 2 + k, W + 1)];  // dn1[jl-2 .. jl+9]
-#pragma unroll
-      for (int k = 0; k < 10; ++k) w2[k] = dn2[min(jl - 1 + k, W + 1)];  // dn2[jl-1 .. jl+8]
-      const uint32_t* f = fcur + g;
-#pragma unroll
-      for (int k = 7; k >= 0; --k) {
-        uint32_t t = f[k];
-        t = min(t, w2[k + 2] + CV_LONG);  // dn2[j + 1]
-        t = min(t, w2[k] + CV_LONG);      // dn2[j - 1]
-        t = min(t, w1[k + 4] + CV_LONG);  // dn1[j + 2]
-        t = min(t, w1[k + 3] + CV_DIAG);  // dn1[j + 1]
-        t = min(t, w1[k + 2] + CV_HV);    // dn1[j]
-        t = min(t, w1[k + 1] + CV_DIAG);  // dn1[j - 1]
-        t = min(t, w1[k] + CV_LONG);      // dn1[j - 2]
-        const uint64_t nr = min((uint64_t)t, run + CV_HV);
-        run = jl + k < j1 ? nr : run;
-        loc[g + k] = (uint32_t)nr;
-      }
+    for (int k = CM - 1; k >= 0; --k) {  // right to left
+      const int j = j0 + k;
+      const int jc = min(j, W - 1);
+      uint32_t t = fcur[k];
+      t = min(t, dn2[jc + 1] + CV_LONG);
+      t = min(t, dn2[jc - 1] + CV_LONG);
+      t = min(t, dn1[jc + 2] + CV_LONG);
+      t = min(t, dn1[jc + 1] + CV_DIAG);
+      t = min(t, dn1[jc] + CV_HV);
+      t = min(t, dn1[jc - 1] + CV_DIAG);
+      t = min(t, dn1[jc - 2] + CV_LONG);
+      const uint64_t nr = min((uint64_t)t, run + CV_HV);
+      run = j < j1 ? nr : run;
+      loc[k] = (uint32_t)nr;
     }
     // value at column j1: a source at column js holding v contributes v + (js - j) HV, the border
     // (INIT at column W) INIT + (W - j) HV; carried as v + js HV (< 2^32 as above)
     const uint32_t mine = j0 < j1 ? (uint32_t)run + (uint32_t)j0 * CV_HV : 0xFFFFFFFFu;
-    const uint32_t carry = min(wave_excl_min_scan_down(mine, lane), CV_INIT + (uint32_t)W * CV_HV);
+    const uint32_t down = wave_excl_min_scan_down(mine, lane);
+    // this wave's total: the inclusive scan from the top lane down, read at lane 0
+    const uint32_t wtot = min(down, mine);
+    uint32_t* tt = tot + (i & 1) * CH_W;
+    if (lane == 0) tt[wv] = wtot;
     __syncthreads();
+    const uint32_t carry = min(min(down, waves_prefix_min<false>(tt, wv, lane)), CV_INIT + (uint32_t)W * CV_HV);
 #pragma unroll
     for (int k = 0; k < CM; ++k) {
       const int j = j0 + k;
@@ -395,25 +410,38 @@ __global__ __launch_bounds__(64) void costmap_chamfer_kernel(const uint8_t* __re
     dmin = fminf(dmin, __shfl_xor(dmin, o, 64));
     dmax = fmaxf(dmax, __shfl_xor(dmax, o, 64));
   }
+  float* red = reinterpret_cast<float*>(srows);  // the rows are dead now
   if (lane == 0) {
+    red[wv] = dmin;
+    red[CH_W + wv] = dmax;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int k = 1; k < CH_W; ++k) {
+      dmin = fminf(dmin, red[k]);
+      dmax = fmaxf(dmax, red[CH_W + k]);
+    }
     range[0] = __builtin_bit_cast(int32_t, dmin);
     range[1] = __builtin_bit_cast(int32_t, dmax);
   }
 }
 
-// cv2.normalize(NORM_MINMAX, 0, 1) (:375) in float64 from the float32 map, then (1 - d)**power
-// (:376): 1 - d in float32, the power correctly rounded to float32.
+// cv2.normalize(NORM_MINMAX, 0, 1) (:375) as OpenCV 4.x's cv::normalize / convertTo write it for a
+// CV_32F destination: scale = 1 / (smax - smin) (0 if smax - smin <= DBL_EPSILON) rounded to
+// float, shift = -(float)(smin * scale), dst = fma(src, scale, shift) in float32 (cvt_32f's v_fma);
+// then (1 - d)**power (:376): 1 - d in float32, the power correctly rounded to float32.
 __global__ __launch_bounds__(CM_THREADS) void costmap_cv_scale_kernel(const float* __restrict__ dist, int64_t n,
                                                                       const int32_t* __restrict__ range, int power,
                                                                       float* __restrict__ out) {
-  const double lo = (double)__builtin_bit_cast(float, range[0]);
-  const double hi = (double)__builtin_bit_cast(float, range[1]);
-  const double scale = (hi - lo > 2.220446049250313e-16) ? 1.0 / (hi - lo) : 0.0;
-  const double shift = 0.0 - lo * scale;
+  const double smin = (double)__builtin_bit_cast(float, range[0]);
+  const double smax = (double)__builtin_bit_cast(float, range[1]);
+  const double scale = 1.0 * ((smax - smin > 2.220446049250313e-16) ? 1.0 / (smax - smin) : 0.0);
+  const float a = (float)scale;
+  const float b = 0.0f - (float)(smin * (double)a);
   for (int64_t i = (int64_t)blockIdx.x * CM_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * CM_THREADS) {
-    const float dn = (float)((double)dist[i] * scale + shift);
-    const float b = 1.0f - dn;
-    out[i] = (float)pow_int_dd((double)b, power);
+    const float dn = __builtin_fmaf(dist[i], a, b);
+    const float bb = 1.0f - dn;
+    out[i] = (float)pow_int_dd((double)bb, power);
   }
 }
 
@@ -428,19 +456,17 @@ hipError_t launch_costmap_build(const CostmapScratch& sc, int n_obs, int size, i
                      sc.xs, size, sc.occ, sc.range);
   if (metric == COSTMAP_CHAMFER5) {
     float* dist = reinterpret_cast<float*>(sc.d2);
-    const size_t lds = (size_t)3 * (size + 2 * CH_B) * sizeof(uint32_t);
+    const size_t lds = ((size_t)3 * (size + 2 * CH_B) + 2 * CH_W) * sizeof(uint32_t);
     uint32_t* t32 = reinterpret_cast<uint32_t*>(sc.g2);
-    const int per = (size + 63) / 64;  // columns per lane
-    if (per <= 8)
-      hipLaunchKernelGGL(costmap_chamfer_kernel<8>, dim3(1), dim3(64), lds, st, sc.occ, size, size, t32, dist, sc.range);
-    else if (per <= 16)
-      hipLaunchKernelGGL(costmap_chamfer_kernel<16>, dim3(1), dim3(64), lds, st, sc.occ, size, size, t32, dist, sc.range);
-    else if (per <= 32)
-      hipLaunchKernelGGL(costmap_chamfer_kernel<32>, dim3(1), dim3(64), lds, st, sc.occ, size, size, t32, dist, sc.range);
-    else if (per <= 64)
-      hipLaunchKernelGGL(costmap_chamfer_kernel<64>, dim3(1), dim3(64), lds, st, sc.occ, size, size, t32, dist, sc.range);
+    const int per = (size + CH_T - 1) / CH_T;  // columns per thread
+    if (per <= 1)
+      hipLaunchKernelGGL(costmap_chamfer_kernel<1>, dim3(1), dim3(CH_T), lds, st, sc.occ, size, size, t32, dist, sc.range);
+    else if (per <= 2)
+      hipLaunchKernelGGL(costmap_chamfer_kernel<2>, dim3(1), dim3(CH_T), lds, st, sc.occ, size, size, t32, dist, sc.range);
+    else if (per <= 4)
+      hipLaunchKernelGGL(costmap_chamfer_kernel<4>, dim3(1), dim3(CH_T), lds, st, sc.occ, size, size, t32, dist, sc.range);
     else
-      hipLaunchKernelGGL(costmap_chamfer_kernel<128>, dim3(1), dim3(64), lds, st, sc.occ, size, size, t32, dist, sc.range);
+      hipLaunchKernelGGL(costmap_chamfer_kernel<8>, dim3(1), dim3(CH_T), lds, st, sc.occ, size, size, t32, dist, sc.range);
     const unsigned blocks = (unsigned)std::min<size_t>((cells + CM_THREADS - 1) / CM_THREADS, 256 * 8);
     hipLaunchKernelGGL(costmap_cv_scale_kernel, dim3(blocks), dim3(CM_THREADS), 0, st, dist, (int64_t)cells,
                        sc.range, power, out);

@@ -353,6 +353,7 @@ struct Lean {
   int emin;      // min frexp exponent of the numerators
   int nlo, nhi;  // min / max bit pattern of the squared norms
   int n1lo = 0x3F800000, n1hi = 0x3F800000;  // ... of the squared norms of unit vectors (sqrt_near1)
+  int emin40 = 0;  // min frexp exponent of the numerators guarded at 2^-40 (orient_step, see there)
 };
 constexpr int kLeanEmin = -79;          // |a| >= 2^-80 <=> frexp exponent >= -79
 constexpr int kLeanNlo = 0x17800000;    // 2^-80
@@ -363,9 +364,10 @@ __device__ __forceinline__ void lean_init(Lean& l) {
   l.nhi = kLeanNlo;
 }
 constexpr int kNear1 = 4095;  // sqrt_near1: squared norms within 4095 ulps of 1
+constexpr int kLeanEmin40 = -39;  // |a| >= 2^-40 <=> frexp exponent >= -39
 __device__ __forceinline__ bool lean_bad(const Lean& l) {
   return (l.emin < kLeanEmin) | (l.nlo < kLeanNlo) | (l.nhi > kLeanNhi) | (l.n1lo < 0x3F800000 - kNear1) |
-         (l.n1hi > 0x3F800000 + kNear1);
+         (l.n1hi > 0x3F800000 + kNear1) | (l.emin40 < kLeanEmin40);
 }
 // correctly rounded sqrt of a normal positive n (neighbour residual test)
 __device__ __forceinline__ float sqrt_cr(float n) {
@@ -522,6 +524,15 @@ __device__ __forceinline__ Recip lean_norm_near1(float n, Lean& l) {
   r.y = __builtin_fmaf(__builtin_fmaf(-r.b, y0, 1.0f), y0, y0);
   return r;
 }
+// lean_norm_near1 for a squared norm PROVEN within 4095 ulps of 1 (no guard; see orient_step)
+__device__ __forceinline__ Recip norm_near1_trusted(float n) {
+  const int nb = __builtin_bit_cast(int, n);
+  Recip r;
+  r.b = __builtin_bit_cast(float, (int)((unsigned)(nb + 0x3F800000) >> 1));
+  const float y0 = __builtin_amdgcn_rcpf(r.b);
+  r.y = __builtin_fmaf(__builtin_fmaf(-r.b, y0, 1.0f), y0, y0);
+  return r;
+}
 __device__ __forceinline__ Recip lean_norm2(float n, Lean& l) {
   const int nb = __builtin_bit_cast(int, n);
   l.nlo = min(l.nlo, nb);
@@ -544,9 +555,10 @@ __device__ __forceinline__ float lean_div_s(float a, const Recip& r, Lean& l) {
   const float e1 = __builtin_fmaf(r.b, q1, -a);
   return __builtin_fmaf(-e1, r.y, q1);
 }
-// (a.x, a.y) / r.b, each lane lean_div_s
+// (a.x, a.y) / r.b, each lane lean_div_s (G = 0: numerators proven in range, no guard)
+template <int G = 1>
 __device__ __forceinline__ f2 lean_div2(f2 a, const Recip& r, Lean& l) {
-  l.emin = min(l.emin, min(__builtin_amdgcn_frexp_expf(a.x), __builtin_amdgcn_frexp_expf(a.y)));
+  if constexpr (G == 1) l.emin = min(l.emin, min(__builtin_amdgcn_frexp_expf(a.x), __builtin_amdgcn_frexp_expf(a.y)));
   const f2 b = bc2(r.b), y = bc2(r.y);
   const f2 q0 = a * y;
   const f2 e0 = pk_fma(b, q0, -a);
@@ -556,10 +568,16 @@ __device__ __forceinline__ f2 lean_div2(f2 a, const Recip& r, Lean& l) {
 }
 // (a.x, a.y, az) / r.b: lean_div2 and lean_div_s with their dependent steps interleaved, so the
 // scalar chain's instructions fill the wait states between the packed chain's dependent steps
-// (same operations, same results)
+// (same operations, same results).  G: 0 = numerators proven in range (no guard), 1 = guarded at
+// 2^-80 (emin), 2 = guarded at 2^-40 (emin40).
+template <int G = 1>
 __device__ __forceinline__ void lean_div3(f2 a, float az, const Recip& r, Lean& l, f2& qxy, float& qz) {
-  l.emin = min(l.emin, min(min(__builtin_amdgcn_frexp_expf(a.x), __builtin_amdgcn_frexp_expf(a.y)),
-                           __builtin_amdgcn_frexp_expf(az)));
+  if constexpr (G == 1)
+    l.emin = min(l.emin, min(min(__builtin_amdgcn_frexp_expf(a.x), __builtin_amdgcn_frexp_expf(a.y)),
+                             __builtin_amdgcn_frexp_expf(az)));
+  if constexpr (G == 2)
+    l.emin40 = min(l.emin40, min(min(__builtin_amdgcn_frexp_expf(a.x), __builtin_amdgcn_frexp_expf(a.y)),
+                                 __builtin_amdgcn_frexp_expf(az)));
   const f2 b = bc2(r.b), y = bc2(r.y);
   const f2 q0 = a * y;
   const float q0z = az * r.y;
@@ -586,6 +604,15 @@ struct Head {  // heading vector (x, y packed)
 
 // _get_heading_tangent_vector + _update_orientation (projection_warp.py:168-248): the new heading
 // from the previous one, the surface normal n and sin / cos / (1 - cos) of w dt.
+// Guards of the fast path (F): only the two vectors that can come out arbitrary are checked,
+//   p = h - (h.n) n: every component 0 or |.| >= 2^-40, |p|^2 in [2^-80, 2^80];
+//   r (the Rodrigues rotation): every component 0 or |.| >= 2^-40, |r|^2 within 4095 ulps of 1.
+// The rest follows.  t = p / |p| has components 0 or >= 2^-40 / 2^40 = 2^-80 (the quotient guard),
+// and with p's quotients exact |t|^2 = 1 + e, |e| <= ~14 ulps (3-term sum of squares of correctly
+// rounded quotients by a correctly rounded square root of a 3-term sum: ~5u + 2u + 3u + 2u), so
+// the second normalisation needs no guard.  Likewise the new heading h' = r / |r| has components
+// 0 or >= 2^-41 and |h'|^2 within ~14 ulps of 1: the next position update (advance_step<true,
+// false>) needs no guard either.  Out of range -> the caller redoes the step with IEEE operators.
 template <bool F>
 __device__ __forceinline__ Head orient_step(f2 nxy, float nz, const Head& h, float sn, float cs, float omc,
                                            Lean& l) {
@@ -598,10 +625,10 @@ __device__ __forceinline__ Head orient_step(f2 nxy, float nz, const Head& h, flo
   if constexpr (F) {
     const f2 p2 = pxy * pxy;
     const Recip r = lean_norm2((p2.x + p2.y) + pz * pz, l);
-    lean_div3(pxy, pz, r, l, txy, tz);
+    lean_div3<2>(pxy, pz, r, l, txy, tz);
     const f2 t2 = txy * txy;
-    const Recip ro = lean_norm_near1((t2.x + t2.y) + tz * tz, l);
-    lean_div3(txy, tz, ro, l, oxy, oz);
+    const Recip ro = norm_near1_trusted((t2.x + t2.y) + tz * tz);
+    lean_div3<0>(txy, tz, ro, l, oxy, oz);
   } else {
     const float pn = sqrtf((pxy.x * pxy.x + pxy.y * pxy.y) + pz * pz);
     txy = f2{pxy.x / pn, pxy.y / pn};
@@ -621,7 +648,7 @@ __device__ __forceinline__ Head orient_step(f2 nxy, float nz, const Head& h, flo
   if constexpr (F) {
     const f2 r2 = rxy * rxy;
     const Recip r = lean_norm_near1((r2.x + r2.y) + rz * rz, l);
-    lean_div3(rxy, rz, r, l, o.xy, o.z);
+    lean_div3<2>(rxy, rz, r, l, o.xy, o.z);
   } else {
     const float rn = sqrtf((rxy.x * rxy.x + rxy.y * rxy.y) + rz * rz);
     o.xy = f2{rxy.x / rn, rxy.y / rn};
@@ -630,13 +657,20 @@ __device__ __forceinline__ Head orient_step(f2 nxy, float nz, const Head& h, flo
   return o;
 }
 // _update_position (projection_warp.py:207-223): pos + normalize(h).xy * v * dt
-template <bool F>
+// GUARD = false: h is the heading a fast-path orient_step just produced (its guards cover this
+// normalisation, see orient_step).
+template <bool F, bool GUARD = true>
 __device__ __forceinline__ f2 advance_step(const Head& h, float v, float dt, f2 pos, Lean& l) {
   f2 u;
   if constexpr (F) {
     const f2 h2 = h.xy * h.xy;
-    const Recip r = lean_norm_near1((h2.x + h2.y) + h.z * h.z, l);
-    u = lean_div2(h.xy, r, l);
+    if constexpr (GUARD) {
+      const Recip r = lean_norm_near1((h2.x + h2.y) + h.z * h.z, l);
+      u = lean_div2(h.xy, r, l);
+    } else {
+      const Recip r = norm_near1_trusted((h2.x + h2.y) + h.z * h.z);
+      u = lean_div2<0>(h.xy, r, l);
+    }
   } else {
     const float hn = sqrtf((h.xy.x * h.xy.x + h.xy.y * h.xy.y) + h.z * h.z);
     u = f2{h.xy.x / hn, h.xy.y / hn};
@@ -1051,8 +1085,12 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
       float snA = 0.f, csA = 0.f, omA = 0.f, snB = 0.f, csB = 0.f, omB = 0.f;
       const f2 cell_off = f2{-a.x_min, a.y_min};
       const float fi_hi = (float)(a.grid - 1), fj_lo = (float)(1 - a.rows);
-      const float4* ntab0 = dem.N + (a.grid + 2);  // entry (jj, ii) = (1 - tjj, ti + 1): offset ti - tjj * (grid + 1)
+      // entry (jj, ii) = (1 - tjj, ti + 1) of the table: element (ti + grid + 2) - tjj * (grid + 1) >= 0 from
+      // dem.N, addressed as the uniform base plus a 32-bit byte offset (table < 4 GiB, check_grid):
+      // one v_mad_i32_i24 (|tjj|, grid + 1 < 2^23) instead of a quarter-rate 32-bit multiply and 64-bit adds
+      const char* nbase = reinterpret_cast<const char*>(dem.N);
       const int nrow = a.grid + 1;
+      const int ncol0 = a.grid + 2;
       // normal-table entry of the cell holding pos (Dem::cell + Dem::normal_cell)
       auto gather = [&](f2 pos, float4& nv) __attribute__((always_inline)) {
         f2 f;
@@ -1066,12 +1104,13 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
         }
         const int ti = (int)__builtin_amdgcn_fmed3f(f.x, -1.0f, fi_hi);  // min(i, grid - 1)
         const int tjj = (int)__builtin_amdgcn_fmed3f(f.y, fj_lo, 1.0f);  // -min(j, rows - 1)
+        const int idx = __mul24(tjj, -nrow) + (ti + ncol0);
 #if defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 1  // diagnostic builds only: one cell (L1 hits)
-        nv = ntab0[(ti - tjj * nrow) & 0];
+        nv = *reinterpret_cast<const float4*>(nbase + ((uint32_t)(idx << 4) & 0u));
 #elif defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 2  // diagnostic: no load
-        nv = make_float4(__builtin_bit_cast(float, ti) * 1e-30f, __builtin_bit_cast(float, tjj) * 1e-30f, 1.0f, 0.f);
+        nv = make_float4(__builtin_bit_cast(float, idx) * 1e-30f, 0.f, 1.0f, 0.f);
 #else
-        nv = ntab0[ti - tjj * nrow];
+        nv = *reinterpret_cast<const float4*>(nbase + (uint32_t)(idx << 4));
 #endif
       };
       auto read_in = [&](int t, float& v, float& sn, float& cs, float& om, int need) __attribute__((always_inline)) {
@@ -1109,7 +1148,7 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
         lean_init(l);
         Head ho = orient_step<true>(nxy, nz, hd, snX, csX, omX, l);
         f2 p1 = pX;
-        if constexpr (more) p1 = advance_step<true>(ho, v1, a.dt, pX, l);
+        if constexpr (more) p1 = advance_step<true, false>(ho, v1, a.dt, pX, l);
         if (__builtin_expect(lean_bad(l), 0)) {  // operand outside the fast range: IEEE redo
           ho = orient_step<false>(nxy, nz, hd, snX, csX, omX, l);
           if constexpr (more) p1 = advance_step<false>(ho, v1, a.dt, pX, l);

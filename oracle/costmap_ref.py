@@ -26,9 +26,10 @@ pass over the upper half-mask and a backward pass over the lower one, d = float(
 Pinned only against the literal per-pixel loop below (`chamfer_l2_5x5_loops`), not against cv2
 itself (parity unpinned: x86 wheels of opencv may route this call through IPP's float
 implementation instead, which can differ in the last bits).
-:375 cv2.normalize(NORM_MINMAX, 0, 1): scale = 1 / (max - min), shift = -min * scale in float64,
-dst = float32(src * scale + shift) (OpenCV's convertTo with alpha, beta); a constant map gives
-scale 0 -> all zeros.
+:375 cv2.normalize(NORM_MINMAX, 0, 1) as OpenCV 4.x writes it for a CV_32F destination (norm.cpp,
+convert_scale.simd.hpp): scale = 1 / (max - min) rounded to float32, shift = -(float)(min * scale),
+dst = fmaf(src, scale, shift) in float32 (one rounding); a constant map gives scale 0 -> all zeros.
+Parity unpinned (no cv2 here).
 :376 (1 - d)**20 on the float32 map: 1 - d rounded to float32, the power correctly rounded to
 float32 (computed in float64: what numpy's float32 power / libm powf return barring last-bit ties).
 
@@ -169,12 +170,45 @@ def chamfer_l2_5x5_loops(occ):
     return out
 
 
+DBL_EPSILON = float(np.finfo(np.float64).eps)
+
+
+def fmaf32(x, a, b):
+    """float32 fused multiply-add, round(x * a + b) with ONE rounding, on float32 arrays / scalars.
+
+    x * a is exact in float64 (24 + 24 significand bits); s = x * a + b rounded to float64 plus
+    its exact error e (TwoSum) represent the exact sum.  Rounding s to float32 equals rounding the
+    exact sum except when s lies exactly halfway between two float32 neighbours and e != 0: then
+    the exact sum lies on e's side of that midpoint."""
+    x64 = np.asarray(x, np.float32).astype(np.float64)
+    p = x64 * np.float64(np.float32(a))
+    b64 = np.float64(np.float32(b))
+    s = p + b64
+    bb = s - p
+    e = (p - (s - bb)) + (b64 - bb)
+    r = s.astype(np.float32)
+    r64 = r.astype(np.float64)
+    d = s - r64                                     # exact (Sterbenz)
+    other = np.where(d > 0, np.nextafter(r, np.float32(np.inf)), np.nextafter(r, np.float32(-np.inf)))
+    mid = (d != 0) & ((r64 + other.astype(np.float64)) * 0.5 == s)
+    toward = mid & (e != 0) & (np.sign(e) == np.sign(d))
+    return np.where(toward, other, r).astype(np.float32)
+
+
 def cv_normalize_minmax(d):
-    """cv2.normalize(d, None, 0, 1.0, NORM_MINMAX) on a float32 map."""
-    lo, hi = float(d.min()), float(d.max())
-    scale = 1.0 / (hi - lo) if hi - lo > np.finfo(np.float64).eps else 0.0
-    shift = 0.0 - lo * scale
-    return (d.astype(np.float64) * scale + shift).astype(np.float32)
+    """cv2.normalize(d, None, 0, 1.0, NORM_MINMAX) on a float32 map, as OpenCV 4.x's
+    modules/core/src/norm.cpp (cv::normalize) and convert_scale.simd.hpp write it for a CV_32F
+    destination (rtype = the source's CV_32F, dst=None): smin, smax by minMaxIdx (float64);
+    scale = (dmax - dmin) * (1 / (smax - smin)) if smax - smin > DBL_EPSILON else 0, then
+    scale = (float)scale and shift = (float)dmin - (float)(smin * scale) (the CV_32F branch);
+    convertTo(dst, CV_32F, scale, shift) -> cvt_32f with a = (float)scale, b = (float)shift,
+    dst = v_fma(src, a, b): one float32 fused multiply-add per element (FMA hardware, the AVX2
+    dispatch of the x86 wheels).  Parity unpinned: cv2 is not installable here."""
+    smin, smax = float(d.min()), float(d.max())
+    scale = 1.0 * (1.0 / (smax - smin) if smax - smin > DBL_EPSILON else 0.0)
+    scale = float(np.float32(scale))
+    shift = float(np.float32(0.0) - np.float32(smin * scale))
+    return fmaf32(d, np.float32(scale), np.float32(shift))
 
 
 def cv_power(dn, power):

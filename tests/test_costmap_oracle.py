@@ -70,3 +70,39 @@ def test_chamfer_costmap_edges():
     assert np.array_equal(full, np.ones((size, size), np.float32))   # min == max: scale 0
     cm = CR.create_obstacles_costmap_cv(_rocks(5, 4.0, 3), (0, 0), size, 5.0, 0.3)
     assert cm.dtype == np.float32 and cm.max() == 1.0 and cm.min() == 0.0
+
+
+def test_fmaf32_single_rounding():
+    """The oracle's float32 fma (cv::normalize's convertTo, v_fma) rounds once: against exact
+    rational arithmetic on random operands and on constructed halfway cases."""
+    from fractions import Fraction
+    rng = np.random.default_rng(3)
+    x = rng.random(4000).astype(np.float32)
+    a = np.float32(rng.random() * 3 + 0.1)
+    b = np.float32(-rng.random())
+    # operands whose float64 sum lands exactly on a float32 midpoint with a non-zero error term
+    x = np.concatenate([x, np.float32([1.0 + 2.0 ** -23, 1.5, 3.0])])
+    got = CR.fmaf32(x, a, b)
+    for xi, gi in zip(x, got):
+        exact = Fraction(float(xi)) * Fraction(float(a)) + Fraction(float(b))
+        lo = np.float32(float(exact))
+        cands = [lo, np.nextafter(lo, np.float32(np.inf)), np.nextafter(lo, np.float32(-np.inf))]
+        best = min(cands, key=lambda c: (abs(Fraction(float(c)) - exact), int(np.float32(c).view(np.uint32)) & 1))
+        assert gi == best, (xi, gi, best)
+    # midpoint construction: x * a + b = m + tiny where m is a float32 midpoint
+    m = Fraction(1) + Fraction(1, 2 ** 24)          # halfway between 1 and 1 + 2^-23
+    got = CR.fmaf32(np.float32([1.0]), np.float32(1.0), np.float32(2.0 ** -24))
+    assert got[0] == np.float32(1.0)                # tie -> even (e == 0)
+    assert m > 1
+
+
+def test_cv_normalize_float32_path():
+    """cv::normalize(NORM_MINMAX) for CV_32F: float scale / shift and a float32 fma."""
+    d = np.float32([[0.5, 2.0], [7.25, 3.0]])
+    out = CR.cv_normalize_minmax(d)
+    scale = np.float32(1.0 / (7.25 - 0.5))
+    shift = np.float32(0.0) - np.float32(0.5 * float(scale))
+    exp = CR.fmaf32(d, scale, shift)
+    np.testing.assert_array_equal(out, exp)
+    assert out.dtype == np.float32 and out.min() == 0.0
+    np.testing.assert_array_equal(CR.cv_normalize_minmax(np.full((3, 3), 2.0, np.float32)), np.zeros((3, 3), np.float32))
