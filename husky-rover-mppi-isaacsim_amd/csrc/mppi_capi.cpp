@@ -289,7 +289,8 @@ Plan make_plan(const mppi_ctx* c) {
     // 15H floats), which runs beside a rollout workgroup on one CU
     const size_t base = (pl.lds_bytes + 15) / 16 * 16;
     const size_t row2 = (size_t)2 * (TB + 4) * sizeof(float);  // UCACHE_ROW: one float4 of bank skew
-    const size_t budget = kLdsBytes - ((size_t)15 * H * sizeof(float) + 2047) / 1024 * 1024;
+    // (1 KiB more: the fused step launch's static ticket words and LDS allocation granularity)
+    const size_t budget = kLdsBytes - ((size_t)15 * H * sizeof(float) + 2047) / 1024 * 1024 - 1024;
     pl.ucache_steps = base < budget ? (int)std::min<size_t>((size_t)H, (budget - base) / row2) : 0;
     if (pl.ucache_steps > 0) pl.lds_bytes = base + (size_t)pl.ucache_steps * row2;
   }
