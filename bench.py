@@ -61,6 +61,7 @@ CONFIGS = {
 KERNEL_SOURCES = ("mppi_kernels.hip", "mppi_kernels.h", "mppi_detmath.h", "mppi_capi.cpp", "Makefile")
 
 
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -411,6 +412,17 @@ def timed_run(torch, dist, run, proj, warmup, steps, step0, async_tail, kernel_t
     return el
 
 
+def chain_static(path=os.path.join(ROOT, "profiles", "isa", "chain_count.json")):
+    """The chain step's static instruction count (profiles/isa/chain_count.py) if it was taken
+    from the current kernel sources, else None."""
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return rec.get("instructions_per_step") if rec.get("src_sha256") == source_hash() else None
+
+
 def pmc_traffic(path, kernel, K_local, H):
     """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary, only if it was
     measured on the current kernel sources (src_sha256) at the same K and H; else None."""
@@ -476,6 +488,7 @@ def main():
     _, fin_ms, n_fin = run.eng.timing()
     tail_ms, n_tail = run.eng.tail_timing()
     info = run.eng.launch_info()
+    clock = run.eng.chain_clock()   # the last rollout's chain wave: shader MHz and cycles per step
     record_bytes = run.eng.record_len() * 8
     k_local = run.k_local
     run.close()
@@ -536,8 +549,10 @@ def main():
         k_avg_ms = roll_ms / max(n_roll, 1)
         alg_bytes = BYTES_PER_ROLLOUT_STEP * k_local * H
         achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9
-        # the rollout kernel the plan chose: role split (1024-thread workgroups) or pair (512)
-        kernel = "mppi_rollout_roles_kernel" if info.get("block") == 1024 else "mppi_rollout_pair_kernel"
+        # the rollout kernel the plan chose: role split (1024-thread workgroups) or pair (512), or
+        # the fused step launch (rollout + finish in one kernel)
+        kernel = ("mppi_step_fused_kernel" if info.get("fused") else
+                  "mppi_rollout_roles_kernel" if info.get("block") == 1024 else "mppi_rollout_pair_kernel")
         traffic, traffic_src = pmc_traffic(args.pmc_json, kernel, k_local, H)
         rec = {
             "metric": "MPPI steps/sec at K=65536 H=100 on 750x750 costmap; 1/2/4/8-GPU scaling",
@@ -567,6 +582,10 @@ def main():
                 "sync_steps_per_s": round(args.steps / el_sync, 3),
                 "sync_ms_per_step": round(el_sync / args.steps * 1e3, 4),
                 "finish_kernel_avg_ms": round(fin_ms / max(n_fin, 1), 5),
+                "chain": {"instructions_per_step": chain_static(),
+                          "cycles_per_step": round(clock["cycles_per_step"], 1),
+                          "shader_clock_mhz": round(clock["shader_mhz"], 1),
+                          "source": "s_memtime / s_memrealtime of the chain wave of trajectories 0-63, last step"},
                 "tail_kernel_avg_ms": round(tail_ms / n_tail, 5) if n_tail else None,
                 "src_sha256": source_hash(),
             },

@@ -154,6 +154,7 @@ struct mppi_ctx {
   double* level1 = nullptr;       // finish kernel first-level records
   size_t level1_cap = 0;
   unsigned* level1_cnt = nullptr;
+  uint64_t* clk = nullptr;  // [4] chain clock stamps of the last sampled rollout (RolloutArgs::clk)
   // tiled bilinear binning scratch
   int* bin_tile_of = nullptr;
   size_t bin_n_cap = 0;
@@ -396,6 +397,7 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   a.pen = p.collision_penalty;
   a.T = p.temperature;
   a.cost_out = c->cost;
+  a.clk = c->clk;
   a.nodes = c->nodes;
   a.ustore = c->ustore;
   a.inj_u1 = c->inj1;
@@ -1145,6 +1147,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipHostMalloc(&c->done, 64, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->cdiv_bad, sizeof(unsigned)) != hipSuccess ||
       hipMalloc(&c->level1_cnt, 128) != hipSuccess ||  // [0]: finish handoff, [16]: fused record count
+      hipMalloc(&c->clk, 4 * sizeof(uint64_t)) != hipSuccess ||
       hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->tail_in[1], 3 * H * sizeof(float)) != hipSuccess ||
@@ -1227,6 +1230,7 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->bin_tile_of) hipFree(c->bin_tile_of);
   if (c->level1) hipFree(c->level1);
   if (c->level1_cnt) hipFree(c->level1_cnt);
+  if (c->clk) hipFree(c->clk);
   if (c->bin_counts) hipFree(c->bin_counts);
   if (c->bin_cursor) hipFree(c->bin_cursor);
   if (c->noise_stream) hipStreamDestroy(c->noise_stream);
@@ -1544,6 +1548,20 @@ int mppi_get_timing(mppi_ctx* c, double* roll, double* fin, int64_t* n) {
   if (roll) *roll = c->t_roll;
   if (fin) *fin = c->t_fin;
   if (n) *n = c->launches;
+  return MPPI_OK;
+}
+
+int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
+  if (!c || !out) return fail(MPPI_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  uint64_t v[4] = {0, 0, 0, 0};
+  HIP_TRY(hipMemcpy(v, c->clk, sizeof(v), hipMemcpyDeviceToHost));
+  const double cyc = (double)(v[2] - v[0]), ticks = (double)(v[3] - v[1]);  // s_memrealtime: 100 MHz
+  const int H = H_of(c);
+  const double vals[4] = {ticks > 0 ? cyc / (ticks * 10.0) : 0.0,  // shader clock, MHz
+                          H > 0 ? cyc / H : 0.0, ticks / 100.0, cyc};
+  for (int i = 0; i < n && i < 4; ++i) out[i] = vals[i];
   return MPPI_OK;
 }
 

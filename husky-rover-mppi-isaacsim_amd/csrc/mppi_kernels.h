@@ -87,6 +87,9 @@ struct RolloutArgs {
   int wave_prio;        // pair kernel: raise the waves' issue priority (s_setprio 2)
   int ucache_steps;     // pair kernel, MODE 0: steps [0, n) keep their sampled controls in LDS
                         // ([2][n][TB] floats after the scratch) for leaf_records
+  // optional [4]: the chain wave of group 0 in workgroup 0 stores s_memtime / s_memrealtime at
+  // the start and the end of its H steps (shader clock cycles per step and the clock rate)
+  uint64_t* clk;
 };
 
 

@@ -1071,6 +1071,12 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
   using F_ = std::false_type;
   const int H = a.H;
   bool nobad = false;
+  const bool clk = a.clk != nullptr && blockIdx.x == 0 && tj < 64;  // wave-uniform
+  uint64_t clk_t0 = 0, clk_r0 = 0;
+  if (clk) {
+    clk_t0 = __builtin_amdgcn_s_memtime();
+    clk_r0 = __builtin_amdgcn_s_memrealtime();
+  }
   // dem.cdiv (uniform) as a compile-time tag: one copy of the loop per cell-division path, so
   // no branch inside a step separates the gather from the work around it
   auto body = [&](auto cd_tag) __attribute__((always_inline)) {
@@ -1197,6 +1203,15 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
     body(T_{});
   else
     body(F_{});
+  if (clk) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (tj == 0) {
+      a.clk[0] = clk_t0;
+      a.clk[1] = clk_r0;
+      a.clk[2] = t1;
+      a.clk[3] = r1;
+    }
+  }
 }
 
 template <int TB, int PROJ, int MODE, bool DUMP>

@@ -92,6 +92,7 @@ _PROTOS = {
                                   C.POINTER(C.c_int64)]),
     "mppi_get_tail_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "mppi_get_launch_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]),
+    "mppi_get_chain_clock": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int32]),
     "mppi_bilinear_query": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
     "mppi_selftest": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.POINTER(C.c_int64)]),
     "mppi_bilinear_tiles": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
@@ -466,6 +467,12 @@ class Engine:
         keys = ("reserved", "block", "blocks", "window_cols", "window_rows", "lds_bytes", "finish_kind",
                 "finish_records", "finish_ncol", "finish_groups", "ucache_steps", "fused")
         return dict(zip(keys, [int(v) for v in info]))
+
+    def chain_clock(self):
+        """mppi_get_chain_clock: shader MHz, cycles per chain step, chain us and cycles of the last rollout."""
+        v = (C.c_double * 4)()
+        self._c(self.lib.mppi_get_chain_clock(self.ctx, v, 4), "mppi_get_chain_clock")
+        return dict(zip(("shader_mhz", "cycles_per_step", "chain_us", "chain_cycles"), [float(x) for x in v]))
 
     def selftest(self, what, n=1 << 24, seed=1):
         bad = C.c_int64()

@@ -287,6 +287,12 @@ int mppi_get_tail_timing(mppi_ctx* ctx, double* tail_ms, int64_t* launches);
  * fused launch (mppi_step_fused_kernel), else 0. */
 int mppi_get_launch_info(mppi_ctx* ctx, int64_t* info, int32_t n);
 
+/* Shader clock of the last sampled 3D rollout, from the chain wave of trajectories 0..63
+ * (s_memtime / s_memrealtime at the start and the end of its H steps), up to 4 values:
+ * out[0] = shader clock in MHz, [1] = shader cycles per chain step, [2] = the chain's
+ * microseconds, [3] = its shader cycles.  Waits for the context stream. */
+int mppi_get_chain_clock(mppi_ctx* ctx, double* out, int32_t n);
+
 /* Standalone DEM bilinear kernel: for n query points
  * (x[i], y[i]) in device memory, heights[i] = corner lookup + bilinear exactly
  * as projection_warp.py:8-100, on the context's DEM. */
