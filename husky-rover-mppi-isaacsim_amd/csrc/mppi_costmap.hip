@@ -283,6 +283,10 @@ __device__ inline uint32_t waves_prefix_min(const uint32_t* tot, int w, int lane
   return (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
 }
 
+// Global reads of later rows (occupancy forward, the forward result backward) are issued CH_PF
+// rows ahead into a register ring: a row takes well under the HBM latency.
+constexpr int CH_PF = 4;
+
 template <int CM>
 __global__ __launch_bounds__(CH_T) void costmap_chamfer_kernel(const uint8_t* __restrict__ occ, int H, int W,
                                                                uint32_t* __restrict__ tmp, float* __restrict__ dist,
@@ -296,18 +300,22 @@ __global__ __launch_bounds__(CH_T) void costmap_chamfer_kernel(const uint8_t* __
   for (int k = tid; k < 3 * S; k += CH_T) srows[k] = CV_INIT;
   __syncthreads();
   uint32_t loc[CM];
-  // global reads of a row are issued one row ahead
-  uint8_t ocur[CM], onext[CM];
+  uint32_t pre[CH_PF][CM];  // rows i .. i + CH_PF - 1 of the pass's global input, slot r % CH_PF
+  auto load_occ = [&](int r, uint32_t (&dst)[CM]) __attribute__((always_inline)) {
+    const uint8_t* row = occ + (size_t)min(r, H - 1) * W;
 #pragma unroll
-  for (int k = 0; k < CM; ++k) ocur[k] = j0 + k < j1 ? occ[j0 + k] : 0;
+    for (int k = 0; k < CM; ++k) dst[k] = j0 + k < j1 ? row[j0 + k] : 0u;
+  };
+  auto load_tmp = [&](int r, uint32_t (&dst)[CM]) __attribute__((always_inline)) {
+    const uint32_t* row = tmp + (size_t)max(r, 0) * W;
+#pragma unroll
+    for (int k = 0; k < CM; ++k) dst[k] = j0 + k < j1 ? row[j0 + k] : 0u;
+  };
   // ---- forward pass: rows top to bottom, columns left to right
-  for (int i = 0; i < H; ++i) {
+  auto frow = [&](int i, uint32_t (&oc)[CM]) __attribute__((always_inline)) {
     const uint32_t* up2 = srows + ((i + 1) % 3) * S + CH_B;  // row i - 2 (INIT above the map)
     const uint32_t* up1 = srows + ((i + 2) % 3) * S + CH_B;  // row i - 1
     uint32_t* cur = srows + (i % 3) * S + CH_B;
-    const uint8_t* onrow = occ + (size_t)min(i + 1, H - 1) * W;
-#pragma unroll
-    for (int k = 0; k < CM; ++k) onext[k] = j0 + k < j1 ? onrow[j0 + k] : 0;
     uint64_t run = 0xFFFFFFFFull;  // the chain inside the chunk, no left input yet
 #pragma unroll
     for (int k = 0; k < CM; ++k) {
@@ -319,10 +327,11 @@ __global__ __launch_bounds__(CH_T) void costmap_chamfer_kernel(const uint8_t* __
       t = min(t, up1[jc] + CV_HV);
       t = min(t, up1[jc + 1] + CV_DIAG);
       t = min(t, up1[jc + 2] + CV_LONG);
-      const uint64_t nr = ocur[k] ? 0ull : min((uint64_t)t, run + CV_HV);
+      const uint64_t nr = oc[k] ? 0ull : min((uint64_t)t, run + CV_HV);
       run = j < j1 ? nr : run;
       loc[k] = (uint32_t)nr;
     }
+    load_occ(i + CH_PF, oc);  // this slot's next row
     // value at column j0 - 1: a source at column js holding v contributes v + (j - js) HV, the
     // border (INIT at column -1) INIT + (j + 1) HV; carried as v + (W - js) HV, which stays below
     // 2^32 (v < 3.3e9, W HV < 5.4e8 at W <= 8192), and the minimum exceeds (W - j) HV
@@ -342,32 +351,34 @@ __global__ __launch_bounds__(CH_T) void costmap_chamfer_kernel(const uint8_t* __
         tmp[(size_t)i * W + j] = v;
       }
     }
-#pragma unroll
-    for (int k = 0; k < CM; ++k) ocur[k] = onext[k];
     __syncthreads();  // row i visible
+  };
+#pragma unroll
+  for (int q = 0; q < CH_PF; ++q) load_occ(q, pre[q]);
+  int i = 0;
+  for (; i + CH_PF <= H; i += CH_PF) {
+#pragma unroll
+    for (int q = 0; q < CH_PF; ++q) frow(i + q, pre[q]);
   }
+#pragma unroll
+  for (int q = 0; q < CH_PF; ++q)
+    if (i + q < H) frow(i + q, pre[q]);
   __threadfence_block();  // the forward rows in tmp are re-read below by the same threads only
   // ---- backward pass: rows bottom to top, columns right to left
   for (int k = tid; k < 3 * S; k += CH_T) srows[k] = CV_INIT;
   __syncthreads();
   float dmin = INFINITY, dmax = -INFINITY;
-  uint32_t fcur[CM], fnext[CM];
-#pragma unroll
-  for (int k = 0; k < CM; ++k) fcur[k] = j0 + k < j1 ? tmp[(size_t)(H - 1) * W + j0 + k] : 0u;
-  for (int i = H - 1; i >= 0; --i) {
+  auto brow = [&](int i, uint32_t (&fc)[CM]) __attribute__((always_inline)) {
     const int r = H - 1 - i;                                  // rows done so far
     const uint32_t* dn2 = srows + ((r + 1) % 3) * S + CH_B;  // row i + 2 (INIT below the map)
     const uint32_t* dn1 = srows + ((r + 2) % 3) * S + CH_B;  // row i + 1
     uint32_t* cur = srows + (r % 3) * S + CH_B;
-    const uint32_t* tnrow = tmp + (size_t)max(i - 1, 0) * W;
-#pragma unroll
-    for (int k = 0; k < CM; ++k) fnext[k] = j0 + k < j1 ? tnrow[j0 + k] : 0u;
     uint64_t run = 0xFFFFFFFFull;
 #pragma unroll
     for (int k = CM - 1; k >= 0; --k) {  // right to left
       const int j = j0 + k;
       const int jc = min(j, W - 1);
-      uint32_t t = fcur[k];
+      uint32_t t = fc[k];
       t = min(t, dn2[jc + 1] + CV_LONG);
       t = min(t, dn2[jc - 1] + CV_LONG);
       t = min(t, dn1[jc + 2] + CV_LONG);
@@ -379,6 +390,7 @@ __global__ __launch_bounds__(CH_T) void costmap_chamfer_kernel(const uint8_t* __
       run = j < j1 ? nr : run;
       loc[k] = (uint32_t)nr;
     }
+    load_tmp(i - CH_PF, fc);
     // value at column j1: a source at column js holding v contributes v + (js - j) HV, the border
     // (INIT at column W) INIT + (W - j) HV; carried as v + js HV (< 2^32 as above)
     const uint32_t mine = j0 < j1 ? (uint32_t)run + (uint32_t)j0 * CV_HV : 0xFFFFFFFFu;
@@ -401,10 +413,18 @@ __global__ __launch_bounds__(CH_T) void costmap_chamfer_kernel(const uint8_t* __
         dmax = fmaxf(dmax, d);
       }
     }
-#pragma unroll
-    for (int k = 0; k < CM; ++k) fcur[k] = fnext[k];
     __syncthreads();
+  };
+#pragma unroll
+  for (int q = 0; q < CH_PF; ++q) load_tmp(H - 1 - q, pre[q]);
+  i = H - 1;
+  for (; i - CH_PF + 1 >= 0; i -= CH_PF) {
+#pragma unroll
+    for (int q = 0; q < CH_PF; ++q) brow(i - q, pre[q]);
   }
+#pragma unroll
+  for (int q = 0; q < CH_PF; ++q)
+    if (i - q >= 0) brow(i - q, pre[q]);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     dmin = fminf(dmin, __shfl_xor(dmin, o, 64));
