@@ -80,6 +80,9 @@ def parse():
     ap.add_argument("--no-costmap", action="store_true", help="skip the obstacle-costmap builder leg")
     ap.add_argument("--sync", action="store_true",
                     help="report the synchronous mode (no deferred optimal rollout) as the headline")
+    ap.add_argument("--prewarm-ms", type=float, default=150.0,
+                    help="untimed steps run first for this long, so that the timed passes start at the GPU's "
+                         "steady clock (a short --steps/--warmup run otherwise starts below it)")
     ap.add_argument("--group-devices", default=None,
                     help="comma-separated device of each group member (default with --gpus N>1 and no "
                          "torch.distributed launcher: 0,1,...,N-1)")
@@ -468,6 +471,16 @@ def main():
     run = Runner(args.config, local_rank, world, devices=devices)
     group_info = run.group.info() if run.group is not None else None
     K, H = run.K, run.H
+    # untimed: bring the GPU to its steady clock before the measured passes
+    prewarm_steps = 0
+    t_pw = time.perf_counter()
+    run.set_async_tail(True)
+    # (ranks of torch.distributed take the same fixed number of steps: every step has a collective)
+    fixed = int(args.prewarm_ms) if world > 1 else None
+    while (prewarm_steps < fixed) if fixed is not None else ((time.perf_counter() - t_pw) * 1e3 < args.prewarm_ms):
+        run.step(args.proj, 1_000_000 + prewarm_steps)
+        prewarm_steps += 1
+    run.outputs()
     # synchronous MPPI_step semantics first (every output in host memory when step() returns)
     el_sync = timed_run(torch, dist, run, args.proj, args.warmup, args.steps, 0, False)
     # headline: the optimal rollout of step i (it only feeds trajectories_sim) overlaps step i+1;
@@ -579,12 +592,17 @@ def main():
                 "speedup_vs_1": round(speedup, 3) if speedup is not None else None,
                 "rollout_kernel": info,
                 "pipelined_tail": not args.sync,
+                "prewarm": {"ms": args.prewarm_ms, "steps": prewarm_steps},
                 "sync_steps_per_s": round(args.steps / el_sync, 3),
                 "sync_ms_per_step": round(el_sync / args.steps * 1e3, 4),
                 "finish_kernel_avg_ms": round(fin_ms / max(n_fin, 1), 5),
                 "chain": {"instructions_per_step": chain_static(),
                           "cycles_per_step": round(clock["cycles_per_step"], 1),
                           "shader_clock_mhz": round(clock["shader_mhz"], 1),
+                          "chain_us": round(clock["chain_us"], 2),
+                          "wg0_start_to_chain_us": round(clock["start_to_chain_us"], 2),
+                          "wg0_chain_to_roles_done_us": round(clock["chain_to_roles_done_us"], 2),
+                          "wg0_leaf_us": round(clock["leaf_us"], 2),
                           "source": "s_memtime / s_memrealtime of the chain wave of trajectories 0-63, last step"},
                 "tail_kernel_avg_ms": round(tail_ms / n_tail, 5) if n_tail else None,
                 "src_sha256": source_hash(),

@@ -1147,7 +1147,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipHostMalloc(&c->done, 64, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->cdiv_bad, sizeof(unsigned)) != hipSuccess ||
       hipMalloc(&c->level1_cnt, 128) != hipSuccess ||  // [0]: finish handoff, [16]: fused record count
-      hipMalloc(&c->clk, 4 * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&c->clk, 8 * sizeof(uint64_t)) != hipSuccess ||
       hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->tail_in[1], 3 * H * sizeof(float)) != hipSuccess ||
@@ -1555,13 +1555,17 @@ int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
   if (!c || !out) return fail(MPPI_EINVAL, "null argument");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  uint64_t v[4] = {0, 0, 0, 0};
+  uint64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   HIP_TRY(hipMemcpy(v, c->clk, sizeof(v), hipMemcpyDeviceToHost));
   const double cyc = (double)(v[2] - v[0]), ticks = (double)(v[3] - v[1]);  // s_memrealtime: 100 MHz
   const int H = H_of(c);
-  const double vals[4] = {ticks > 0 ? cyc / (ticks * 10.0) : 0.0,  // shader clock, MHz
-                          H > 0 ? cyc / H : 0.0, ticks / 100.0, cyc};
-  for (int i = 0; i < n && i < 4; ++i) out[i] = vals[i];
+  auto us = [&](int a, int b) { return v[a] && v[b] && v[b] >= v[a] ? (double)(v[b] - v[a]) / 100.0 : 0.0; };
+  const double vals[7] = {ticks > 0 ? cyc * 100.0 / ticks : 0.0,  // shader clock, MHz (ticks: 100 MHz)
+                          H > 0 ? cyc / H : 0.0, ticks / 100.0, cyc,
+                          us(4, 1),   // workgroup start -> chain start
+                          us(3, 5),   // chain end -> every role done
+                          us(5, 6)};  // -> leaf record written
+  for (int i = 0; i < n && i < 7; ++i) out[i] = vals[i];
   return MPPI_OK;
 }
 

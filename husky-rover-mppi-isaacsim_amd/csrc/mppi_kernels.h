@@ -87,8 +87,10 @@ struct RolloutArgs {
   int wave_prio;        // pair kernel: raise the waves' issue priority (s_setprio 2)
   int ucache_steps;     // pair kernel, MODE 0: steps [0, n) keep their sampled controls in LDS
                         // ([2][n][TB] floats after the scratch) for leaf_records
-  // optional [4]: the chain wave of group 0 in workgroup 0 stores s_memtime / s_memrealtime at
-  // the start and the end of its H steps (shader clock cycles per step and the clock rate)
+  // optional [8]: the chain wave of group 0 in workgroup 0 stores s_memtime / s_memrealtime at
+  // the start and the end of its H steps ([0..3]: shader clock cycles per step and the clock
+  // rate); role-split kernel, workgroup 0: s_memrealtime at its start, when every role is done,
+  // and when its leaf record is written ([4..6])
   uint64_t* clk;
 };
 

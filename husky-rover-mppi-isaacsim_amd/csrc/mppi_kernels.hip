@@ -1668,6 +1668,8 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
   const float res_half_neg = (-a.res) / 2.0f;
   const float res_sq = a.res * a.res;
   bool nobad = false;
+  const bool clk_wg = a.clk != nullptr && blockIdx.x == 0 && tid == 0;
+  if (clk_wg) a.clk[4] = __builtin_amdgcn_s_memrealtime();  // workgroup 0 starts
   if (tid < 4 * NG) flags[tid] = 0;
   if constexpr (MODE == 0)
     for (int i = tid; i < 2 * H; i += NT) unom_lds[i] = i < H ? a.u_nom1[i] : a.u_nom2[i - H];
@@ -1952,6 +1954,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
   }
 #endif
   __syncthreads();  // WHEEL's slope sums are in sw_lds
+  if (clk_wg) a.clk[5] = __builtin_amdgcn_s_memrealtime();  // every role of workgroup 0 done
   if (role == ROLE_COST) {  // critics_warp.py:325-329, this f32 add order
     float cost = a.w_path * c_pf;
     cost = cost + a.w_slope * sw_lds[tj];
@@ -1966,6 +1969,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
                                       a.ucache_steps);
   else
     leaf_records<TB, NT, false, FUSED>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
+  if (clk_wg) a.clk[6] = __builtin_amdgcn_s_memrealtime();  // workgroup 0's leaf record written
   if constexpr (FUSED) {  // the record is written through: count it (D8: complete, then a relaxed count)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
