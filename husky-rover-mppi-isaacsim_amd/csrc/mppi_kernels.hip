@@ -905,50 +905,68 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
 #ifdef MPPI_STAMPS
   LEAF_STAMP(1);
 #endif
-  // rows (leaf, j), j in [1, E): two threads per row, each the pairwise tree over one half
-  // (128 trajectories) of the leaf in index order, the row = (left half) + (right half).
-  // A thread streams its half-row as whole 128-byte lines (8 float4 loads back to back).
+  // rows (leaf, j), j in [1, E): the pairwise tree over the leaf's 256 trajectories in index
+  // order = (half 0) + (half 1), half = ((line 0 + line 1) + (line 2 + line 3)), line = 32
+  // trajectories (8 float4 groups, a pairwise tree of its own).  One LINE per thread (eight
+  // units of a row in eight adjacent lanes, combined by lane shuffles in the same order), the
+  // loads of all of a thread's lines issued before any is used: the re-read normals rows come
+  // from HBM / MALL, and one line after another per thread left that latency exposed 4 times.
   const int NR = NL * (E - 1);
-  for (int it = tid; it < 2 * NR; it += NT) {
-    const int r = it >> 1, half = it & 1;
-    const int leaf = r / (E - 1), j = 1 + r - leaf * (E - 1);
-    const float4* w4 = reinterpret_cast<const float4*>(wbuf + 256 * leaf + 128 * half);
-    const float4* u4 = reinterpret_cast<const float4*>(ub_block + (size_t)(j >= 2 ? j - 2 : 0) * TB +
-                                                       256 * leaf + 128 * half);
-    float nom = 0.f, sg = 0.f, lo = 0.f, hi = 0.f;
-    bool cached = false;  // the sampled controls of this row are in LDS (no normals re-read)
-    if constexpr (EPS) {  // rows hold the normals: u = clamp(u_nom[t+1] + sigma*eps) as sampled
-      const int c = (j - 2) >= H ? 1 : 0;
-      const int t = max(j - 2, 0) - c * H;
-      const int ti = min(t + 1, H - 1);
-      nom = c ? a.u_nom2[ti] : a.u_nom1[ti];
-      sg = c ? a.s2 : a.s1;
-      lo = c ? a.min_u2 : a.min_u1;
-      hi = c ? a.max_u2 : a.max_u1;
-      if (j >= 2 && t < uc_steps) {
-        cached = true;
-        u4 = reinterpret_cast<const float4*>(ucache + (size_t)(c * uc_steps + t) * UCACHE_ROW + 256 * leaf +
-                                             128 * half);
-      }
-    }
-    // the half-row's pairwise tree = ((line0 + line1) + (line2 + line3)), each line (8 float4
-    // groups, 32 trajectories) a pairwise tree of its own; one line in registers at a time
-    double s01 = 0.0, s23 = 0.0;
-#pragma unroll 1
-    for (int line = 0; line < 4; ++line) {
-      float4 uq[8];
+  const int NU = 8 * NR;                     // units (row, half, line)
+  constexpr int LR = 1;                      // lines in flight per thread
+  for (int u0 = 0; u0 < NU; u0 += LR * NT) {
+    float4 uq[LR][8];
+    int jr[LR];
+    bool cached_r[LR];
+    float nom_r[LR], sg_r[LR], lo_r[LR], hi_r[LR];
+    const float4* w4r[LR];
 #pragma unroll
-      for (int g = 0; g < 8; ++g) uq[g] = (j >= 2) ? u4[8 * line + g] : make_float4(1.f, 1.f, 1.f, 1.f);
+    for (int q = 0; q < LR; ++q) {
+      const int it = u0 + q * NT + tid;      // 8 consecutive units of a row share 8 adjacent lanes
+      const int itc = min(it, NU - 1);
+      const int r = itc >> 3, half = (itc >> 2) & 1, line = itc & 3;
+      const int leaf = r / (E - 1), j = 1 + r - leaf * (E - 1);
+      jr[q] = j;
+      const int tr0 = 256 * leaf + 128 * half + 32 * line;  // first trajectory of the line
+      w4r[q] = reinterpret_cast<const float4*>(wbuf + tr0);
+      const float4* u4 = reinterpret_cast<const float4*>(ub_block + (size_t)(j >= 2 ? j - 2 : 0) * TB + tr0);
+      bool cached = false;  // the sampled controls of this row are in LDS (no normals re-read)
+      float nom = 0.f, sg = 0.f, lo = 0.f, hi = 0.f;
+      if constexpr (EPS) {  // rows hold the normals: u = clamp(u_nom[t+1] + sigma*eps) as sampled
+        const int c = (j - 2) >= H ? 1 : 0;
+        const int t = max(j - 2, 0) - c * H;
+        const int ti = min(t + 1, H - 1);
+        nom = c ? a.u_nom2[ti] : a.u_nom1[ti];
+        sg = c ? a.s2 : a.s1;
+        lo = c ? a.min_u2 : a.min_u1;
+        hi = c ? a.max_u2 : a.max_u1;
+        if (j >= 2 && t < uc_steps) {
+          cached = true;
+          u4 = reinterpret_cast<const float4*>(ucache + (size_t)(c * uc_steps + t) * UCACHE_ROW + tr0);
+        }
+      }
+      cached_r[q] = cached;
+      nom_r[q] = nom;
+      sg_r[q] = sg;
+      lo_r[q] = lo;
+      hi_r[q] = hi;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) uq[q][g] = (j >= 2) ? u4[g] : make_float4(1.f, 1.f, 1.f, 1.f);
+    }
+#pragma unroll
+    for (int q = 0; q < LR; ++q) {
+      const int it = u0 + q * NT + tid;
+      const int j = jr[q];
       double gs[8];
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
-        const float4 w = w4[8 * line + g];
-        float4 u = uq[g];
-        if (EPS && !cached) {
-          u.x = clampf(nom + sg * u.x, lo, hi);
-          u.y = clampf(nom + sg * u.y, lo, hi);
-          u.z = clampf(nom + sg * u.z, lo, hi);
-          u.w = clampf(nom + sg * u.w, lo, hi);
+        const float4 w = w4r[q][g];
+        float4 u = uq[q][g];
+        if (EPS && !cached_r[q]) {
+          u.x = clampf(nom_r[q] + sg_r[q] * u.x, lo_r[q], hi_r[q]);
+          u.y = clampf(nom_r[q] + sg_r[q] * u.y, lo_r[q], hi_r[q]);
+          u.z = clampf(nom_r[q] + sg_r[q] * u.z, lo_r[q], hi_r[q]);
+          u.w = clampf(nom_r[q] + sg_r[q] * u.w, lo_r[q], hi_r[q]);
         }
         double x0 = (double)w.x, x1 = (double)w.y, x2 = (double)w.z, x3 = (double)w.w;  // j == 1: S
         if (j >= 2) {
@@ -960,14 +978,16 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
         gs[g] = (x0 + x1) + (x2 + x3);
       }
       const double ls = ((gs[0] + gs[1]) + (gs[2] + gs[3])) + ((gs[4] + gs[5]) + (gs[6] + gs[7]));
-      if (line == 0) s01 = ls;
-      else if (line == 1) s01 = s01 + ls;
-      else if (line == 2) s23 = ls;
-      else s23 = s23 + ls;
+      // (line 0 + line 1), (line 2 + line 3): left + right; then the half; then the row
+      const double s2 = ls + __shfl_xor(ls, 1, 64);
+      const double hs = s2 + __shfl_xor(s2, 2, 64);
+      const double rs = hs + __shfl_xor(hs, 4, 64);
+      if (it < NU && (it & 7) == 0) {
+        const int r = it >> 3;
+        const int leaf = r / (E - 1);
+        red[leaf * E + jr[q]] = rs;
+      }
     }
-    const double hsum = s01 + s23;
-    const double other = __shfl_xor(hsum, 1, 64);  // the partner half (adjacent lane)
-    if (half == 0) red[leaf * E + j] = hsum + other;
   }
 #ifdef MPPI_STAMPS
   LEAF_STAMP(4);
