@@ -603,6 +603,9 @@ def main():
                           "wg0_start_to_chain_us": round(clock["start_to_chain_us"], 2),
                           "wg0_chain_to_roles_done_us": round(clock["chain_to_roles_done_us"], 2),
                           "wg0_leaf_us": round(clock["leaf_us"], 2),
+                          "wg_start_spread_us": round(clock["wg_start_spread_us"], 2),
+                          "wg_end_spread_us": round(clock["wg_end_spread_us"], 2),
+                          "wg_span_us": round(clock["wg_span_us"], 2),
                           "source": "s_memtime / s_memrealtime of the chain wave of trajectories 0-63, last step"},
                 "tail_kernel_avg_ms": round(tail_ms / n_tail, 5) if n_tail else None,
                 "src_sha256": source_hash(),

@@ -1147,7 +1147,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipHostMalloc(&c->done, 64, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->cdiv_bad, sizeof(unsigned)) != hipSuccess ||
       hipMalloc(&c->level1_cnt, 128) != hipSuccess ||  // [0]: finish handoff, [16]: fused record count
-      hipMalloc(&c->clk, 8 * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&c->clk, (kClkBase + 2 * kClkBlocks) * sizeof(uint64_t)) != hipSuccess ||
       hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->tail_in[1], 3 * H * sizeof(float)) != hipSuccess ||
@@ -1555,17 +1555,32 @@ int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
   if (!c || !out) return fail(MPPI_EINVAL, "null argument");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  uint64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  HIP_TRY(hipMemcpy(v, c->clk, sizeof(v), hipMemcpyDeviceToHost));
+  std::vector<uint64_t> all((size_t)kClkBase + 2 * kClkBlocks, 0);
+  HIP_TRY(hipMemcpy(all.data(), c->clk, all.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  const uint64_t* v = all.data();
+  // per-workgroup start / end of the last role-split rollout (its plan's blocks)
+  const int nb = std::min(c->last_plan.roles ? c->last_plan.blocks : 0, kClkBlocks);
+  uint64_t s_lo = UINT64_MAX, s_hi = 0, e_lo = UINT64_MAX, e_hi = 0;
+  for (int b = 0; b < nb; ++b) {
+    const uint64_t s0 = v[kClkBase + 2 * b], e0 = v[kClkBase + 2 * b + 1];
+    s_lo = std::min(s_lo, s0);
+    s_hi = std::max(s_hi, s0);
+    e_lo = std::min(e_lo, e0);
+    e_hi = std::max(e_hi, e0);
+  }
+  const bool wg_ok = nb > 0 && e_hi >= s_lo && e_lo >= s_lo;
   const double cyc = (double)(v[2] - v[0]), ticks = (double)(v[3] - v[1]);  // s_memrealtime: 100 MHz
   const int H = H_of(c);
   auto us = [&](int a, int b) { return v[a] && v[b] && v[b] >= v[a] ? (double)(v[b] - v[a]) / 100.0 : 0.0; };
-  const double vals[7] = {ticks > 0 ? cyc * 100.0 / ticks : 0.0,  // shader clock, MHz (ticks: 100 MHz)
-                          H > 0 ? cyc / H : 0.0, ticks / 100.0, cyc,
-                          us(4, 1),   // workgroup start -> chain start
-                          us(3, 5),   // chain end -> every role done
-                          us(5, 6)};  // -> leaf record written
-  for (int i = 0; i < n && i < 7; ++i) out[i] = vals[i];
+  const double vals[10] = {ticks > 0 ? cyc * 100.0 / ticks : 0.0,  // shader clock, MHz (ticks: 100 MHz)
+                           H > 0 ? cyc / H : 0.0, ticks / 100.0, cyc,
+                           us(4, 1),   // workgroup start -> chain start
+                           us(3, 5),   // chain end -> every role done
+                           us(5, 6),   // -> leaf record written
+                           wg_ok ? (double)(s_hi - s_lo) / 100.0 : 0.0,   // first -> last workgroup start
+                           wg_ok ? (double)(e_hi - e_lo) / 100.0 : 0.0,   // first -> last record written
+                           wg_ok ? (double)(e_hi - s_lo) / 100.0 : 0.0};  // first start -> last record
+  for (int i = 0; i < n && i < 10; ++i) out[i] = vals[i];
   return MPPI_OK;
 }
 

@@ -93,6 +93,9 @@ struct RolloutArgs {
   // and when its leaf record is written ([4..6])
   uint64_t* clk;
 };
+// clk layout: [0..8) the stamps above, then (role-split kernel) [kClkBase + 2 b], [.. + 1] =
+// s_memrealtime when workgroup b (< kClkBlocks) starts and when its record is written
+constexpr int kClkBase = 8, kClkBlocks = 4096;
 
 
 // The rollout kernel (mppi_rollout_pair_kernel): 256 trajectories per 512-thread workgroup, a

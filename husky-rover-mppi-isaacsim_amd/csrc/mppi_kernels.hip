@@ -1690,6 +1690,8 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
   bool nobad = false;
   const bool clk_wg = a.clk != nullptr && blockIdx.x == 0 && tid == 0;
   if (clk_wg) a.clk[4] = __builtin_amdgcn_s_memrealtime();  // workgroup 0 starts
+  const bool clk_any = a.clk != nullptr && tid == 0 && blockIdx.x < kClkBlocks;
+  if (clk_any) a.clk[kClkBase + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();  // every workgroup
   if (tid < 4 * NG) flags[tid] = 0;
   if constexpr (MODE == 0)
     for (int i = tid; i < 2 * H; i += NT) unom_lds[i] = i < H ? a.u_nom1[i] : a.u_nom2[i - H];
@@ -1990,6 +1992,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
   else
     leaf_records<TB, NT, false, FUSED>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
   if (clk_wg) a.clk[6] = __builtin_amdgcn_s_memrealtime();  // workgroup 0's leaf record written
+  if (clk_any) a.clk[kClkBase + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
   if constexpr (FUSED) {  // the record is written through: count it (D8: complete, then a relaxed count)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -470,10 +470,11 @@ class Engine:
 
     def chain_clock(self):
         """mppi_get_chain_clock: shader MHz, cycles per chain step, chain us and cycles of the last rollout."""
-        v = (C.c_double * 7)()
-        self._c(self.lib.mppi_get_chain_clock(self.ctx, v, 7), "mppi_get_chain_clock")
+        v = (C.c_double * 10)()
+        self._c(self.lib.mppi_get_chain_clock(self.ctx, v, 10), "mppi_get_chain_clock")
         return dict(zip(("shader_mhz", "cycles_per_step", "chain_us", "chain_cycles", "start_to_chain_us",
-                         "chain_to_roles_done_us", "leaf_us"), [float(x) for x in v]))
+                         "chain_to_roles_done_us", "leaf_us", "wg_start_spread_us", "wg_end_spread_us",
+                         "wg_span_us"), [float(x) for x in v]))
 
     def selftest(self, what, n=1 << 24, seed=1):
         bad = C.c_int64()

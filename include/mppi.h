@@ -288,11 +288,13 @@ int mppi_get_tail_timing(mppi_ctx* ctx, double* tail_ms, int64_t* launches);
 int mppi_get_launch_info(mppi_ctx* ctx, int64_t* info, int32_t n);
 
 /* Shader clock of the last sampled 3D rollout, from the chain wave of trajectories 0..63
- * (s_memtime / s_memrealtime at the start and the end of its H steps), up to 7 values:
+ * (s_memtime / s_memrealtime at the start and the end of its H steps), up to 10 values:
  * out[0] = shader clock in MHz, [1] = shader cycles per chain step, [2] = the chain's
  * microseconds, [3] = its shader cycles; role-split kernel, workgroup 0, microseconds:
  * [4] = workgroup start -> chain start, [5] = chain end -> every role done, [6] -> leaf
- * record written (0 where not measured).  Waits for the context stream. */
+ * record written; over all workgroups (the first 4096): [7] = first -> last workgroup start,
+ * [8] = first -> last record written, [9] = first start -> last record (0 where not measured).
+ * Waits for the context stream. */
 int mppi_get_chain_clock(mppi_ctx* ctx, double* out, int32_t n);
 
 /* Standalone DEM bilinear kernel: for n query points
