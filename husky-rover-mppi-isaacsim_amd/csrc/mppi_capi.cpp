@@ -1581,6 +1581,9 @@ int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
                            wg_ok ? (double)(e_hi - e_lo) / 100.0 : 0.0,   // first -> last record written
                            wg_ok ? (double)(e_hi - s_lo) / 100.0 : 0.0};  // first start -> last record
   for (int i = 0; i < n && i < 10; ++i) out[i] = vals[i];
+  // then, per workgroup b, the time from the first workgroup start to b's record (microseconds)
+  for (int b = 0; b < nb && 10 + b < n; ++b)
+    out[10 + b] = wg_ok ? (double)(v[kClkBase + 2 * b + 1] - s_lo) / 100.0 : 0.0;
   return MPPI_OK;
 }
 

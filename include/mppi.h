@@ -293,8 +293,8 @@ int mppi_get_launch_info(mppi_ctx* ctx, int64_t* info, int32_t n);
  * microseconds, [3] = its shader cycles; role-split kernel, workgroup 0, microseconds:
  * [4] = workgroup start -> chain start, [5] = chain end -> every role done, [6] -> leaf
  * record written; over all workgroups (the first 4096): [7] = first -> last workgroup start,
- * [8] = first -> last record written, [9] = first start -> last record (0 where not measured).
- * Waits for the context stream. */
+ * [8] = first -> last record written, [9] = first start -> last record (0 where not measured);
+ * out[10 + b] = first start -> workgroup b's record.  Waits for the context stream. */
 int mppi_get_chain_clock(mppi_ctx* ctx, double* out, int32_t n);
 
 /* Standalone DEM bilinear kernel: for n query points
