@@ -146,6 +146,11 @@ struct mppi_ctx {
                                // 2 also with the deferred optimal rollout (MPPI_FUSED)
   int fused_noise_groups = -1; // noise of step + 2 in the launch: -1 one workgroup per CU the finish leaves,
                                // n > 0 n workgroups, 0 before the launch on the context stream (MPPI_FUSED_NOISE_GROUPS)
+  // fused launch with the deferred tail: the noise of step + 2 on the noise stream behind a stream
+  // memory wait on this signal word, which the launch writes when its rollout part is done
+  // (MPPI_FUSED_NOISE_GROUPS=-2); nullptr where signal memory is unavailable
+  unsigned* sig = nullptr;
+  unsigned sig_seq = 0;
   uint64_t fused_wait_ticks = 200000000ull;  // fused finish's record wait bound (2 s at 100 MHz; mppi_set_option)
   int noise_gpc = 0;  // noise kernel workgroups per CU: 0 auto = 4 (measured: profiles/r02_notes.md) (MPPI_NOISE_GPC)
   hipEvent_t ev_roll_done = nullptr;
@@ -486,10 +491,19 @@ int sync_tail(mppi_ctx* c) {
   return MPPI_OK;
 }
 
+// The signal word at the latest sequence number the noise stream may wait for: a launch that did
+// not write it (failed step, context teardown) must not leave the noise stream waiting.
+void release_signal(mppi_ctx* c) {
+  if (!c->sig) return;
+  const unsigned v = c->sig_seq;
+  if (hipMemcpy(c->sig, &v, sizeof(v), hipMemcpyHostToDevice) != hipSuccess) (void)hipGetLastError();
+}
+
 // Zero the finish handoff counters (level1_cnt[0]) and the fused launch's record counter
 // ([16]) after a step that did not complete them; the context stream must be idle.
 void rearm_counters(mppi_ctx* c) {
   if (hipMemsetAsync(c->level1_cnt, 0, 128, c->stream) == hipSuccess) hipStreamSynchronize(c->stream);
+  release_signal(c);
 }
 
 // Spin until the finish kernel has published c->seq (all outputs in pinned host
@@ -893,6 +907,9 @@ int enqueue_fused(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, i
   // before the launch on the context stream).  Any other missing step (first steps, a jump of the
   // step counter) is generated before the launch on the context stream.
   const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
+  const bool gated = c->sig != nullptr;  // MPPI_FUSED_NOISE_GROUPS=-2
+  int gated_slot = -1;
+  uint64_t gated_target = 0;
   for (int d = 1; d <= c->noise_ahead; ++d) {
     const uint64_t target = step + (uint64_t)d;
     bool have = false;
@@ -905,7 +922,10 @@ int enqueue_fused(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, i
       HIP_TRY(hipStreamWaitEvent(c->stream, c->eps_ev[v], 0));
       c->eps_pending[v] = false;
     }
-    if (last && c->fused_noise_groups != 0) {
+    if (last && gated) {  // after the launch, on the noise stream, gated on its rollout part
+      gated_slot = v;
+      gated_target = target;
+    } else if (last && c->fused_noise_groups > 0 || (last && c->fused_noise_groups == -1)) {
       z.noise_eps = c->eps[v];
       z.noise_n_base = target * nb;
       z.noise_groups = c->fused_noise_groups > 0 ? c->fused_noise_groups : std::max(c->num_cus - groups, 1);
@@ -935,6 +955,10 @@ int enqueue_fused(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, i
   z.fin_groups = groups;
   z.rec_cnt = c->level1_cnt + 16;
   z.wait_ticks = c->fused_wait_ticks;
+  if (gated_slot >= 0) {
+    z.roll_done = c->sig;
+    z.roll_seq = ++c->sig_seq;
+  }
   c->fin_kind = 1;
   c->fin_P = P;
   c->fin_ncol = ncol;
@@ -944,6 +968,13 @@ int enqueue_fused(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, i
   if (c->timing) {
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     c->ev_roll_pending = true;
+  }
+  if (gated_slot >= 0) {
+    HIP_TRY(hipStreamWaitValue32(c->noise_stream, c->sig, z.roll_seq, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    HIP_TRY(launch_noise(c->p.seed, gated_target * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[gated_slot],
+                         c->noise_stream, noise_groups(c, pl)));
+    HIP_TRY(hipEventRecord(c->eps_ev[gated_slot], c->noise_stream));
+    c->eps_pending[gated_slot] = true;
   }
   if (z.f.mode == 2) return enqueue_tail(c, z.f, par);
   return MPPI_OK;
@@ -1125,7 +1156,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   if (const char* e = std::getenv("MPPI_ROLES")) c->roles = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_NOISE_GPC")) c->noise_gpc = std::max(std::atoi(e), 0);
   if (const char* e = std::getenv("MPPI_FUSED")) c->fused = std::min(std::max(std::atoi(e), 0), 2);
-  if (const char* e = std::getenv("MPPI_FUSED_NOISE_GROUPS")) c->fused_noise_groups = std::max(std::atoi(e), -1);
+  if (const char* e = std::getenv("MPPI_FUSED_NOISE_GROUPS")) c->fused_noise_groups = std::max(std::atoi(e), -2);
   const char* ep = std::getenv("MPPI_STREAM_PRIO");
   const bool use_prio = !(ep && std::atoi(ep) == 0);
   const int H = p.num_iterations;
@@ -1179,6 +1210,13 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   *c->done = 0;
   if (hipMemset(c->level1_cnt, 0, 128) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
+  if (c->fused_noise_groups == -2) {
+    int wv = 0;
+    if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) != hipSuccess || !wv ||
+        hipExtMallocWithFlags(reinterpret_cast<void**>(&c->sig), 64, hipMallocSignalMemory) != hipSuccess ||
+        hipMemset(c->sig, 0, 64) != hipSuccess)
+      return cleanup(fail(MPPI_EHIP, "MPPI_FUSED_NOISE_GROUPS=-2: no stream wait-value / signal memory"));
+  }
 
   if (hipDeviceSynchronize() != hipSuccess) return cleanup(fail(MPPI_EHIP, "device sync failed"));
   *out = c;
@@ -1198,6 +1236,7 @@ void mppi_destroy(mppi_ctx* c) {
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->tail_stream) hipStreamSynchronize(c->tail_stream);
+  release_signal(c);
   if (c->noise_stream) hipStreamSynchronize(c->noise_stream);
   if (c->Z_owned && c->Z) hipFree(c->Z);
   if (c->ntab) hipFree(c->ntab);
@@ -1214,6 +1253,7 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->stage) hipHostFree(c->stage);
   if (c->done) hipHostFree(c->done);
   if (c->cdiv_bad) hipFree(c->cdiv_bad);
+  if (c->sig) hipFree(c->sig);
   delete[] c->out_host;
   for (int i = 0; i < kTailSlots; ++i) {
     if (c->tail_in[i]) hipFree(c->tail_in[i]);

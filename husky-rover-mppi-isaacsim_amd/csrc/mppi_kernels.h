@@ -134,6 +134,11 @@ struct FusedArgs {
   uint64_t noise_n_base;
   int noise_groups;
   uint64_t wait_ticks;
+  // optional: the workgroup taking the last ticket (every record counted, the rollout part done)
+  // stores roll_seq to *roll_done (system scope); a stream memory wait gates the noise of a later
+  // step on it (noise beside the finish, as the three-launch schedule places it)
+  unsigned* roll_done;
+  unsigned roll_seq;
 };
 hipError_t launch_step_fused(const RolloutArgs& a, const FusedArgs& z, size_t lds, hipStream_t st, int proj);
 // record tree finish (mppi_finish_kernel): the fallback where the column-split shape does not fit

@@ -3266,6 +3266,8 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_fused_kernel(const Roll
     const int ticket = roles_body<TB, PROJ, 0, false, true>(a, z.rec_cnt, sh);
     const int blk = ticket - (z.nroll - z.fin_groups);
     if (blk < 0) return;
+    if (ticket == z.nroll - 1 && z.roll_done && threadIdx.x == 0)  // every rollout workgroup has counted
+      __hip_atomic_store(z.roll_done, z.roll_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_s_setprio(0);  // the rollout waves' priorities do not carry into the finish
     if (threadIdx.x == 0) {  // bounded (z.wait_ticks of the 100 MHz clock): a lost count cannot hang the device
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
