@@ -146,9 +146,9 @@ struct mppi_ctx {
                                // 2 also with the deferred optimal rollout (MPPI_FUSED)
   int fused_noise_groups = -1; // noise of step + 2 in the launch: -1 one workgroup per CU the finish leaves,
                                // n > 0 n workgroups, 0 before the launch on the context stream (MPPI_FUSED_NOISE_GROUPS)
-  // fused launch with the deferred tail: the noise of step + 2 on the noise stream behind a stream
-  // memory wait on this signal word, which the launch writes when its rollout part is done
-  // (MPPI_FUSED_NOISE_GROUPS=-2); nullptr where signal memory is unavailable
+  // fused launch: the noise of step + 2 on the noise stream behind a one-wave gate kernel that
+  // waits for this word, which the launch writes when its rollout part is done
+  // (MPPI_FUSED_NOISE_GROUPS=-2); nullptr otherwise
   unsigned* sig = nullptr;
   unsigned sig_seq = 0;
   uint64_t fused_wait_ticks = 200000000ull;  // fused finish's record wait bound (2 s at 100 MHz; mppi_set_option)
@@ -970,7 +970,7 @@ int enqueue_fused(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, i
     c->ev_roll_pending = true;
   }
   if (gated_slot >= 0) {
-    HIP_TRY(hipStreamWaitValue32(c->noise_stream, c->sig, z.roll_seq, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    HIP_TRY(launch_gate(c->sig, z.roll_seq, c->fused_wait_ticks, c->noise_stream));
     HIP_TRY(launch_noise(c->p.seed, gated_target * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[gated_slot],
                          c->noise_stream, noise_groups(c, pl)));
     HIP_TRY(hipEventRecord(c->eps_ev[gated_slot], c->noise_stream));
@@ -1210,13 +1210,9 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   *c->done = 0;
   if (hipMemset(c->level1_cnt, 0, 128) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
-  if (c->fused_noise_groups == -2) {
-    int wv = 0;
-    if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device) != hipSuccess || !wv ||
-        hipExtMallocWithFlags(reinterpret_cast<void**>(&c->sig), 64, hipMallocSignalMemory) != hipSuccess ||
-        hipMemset(c->sig, 0, 64) != hipSuccess)
-      return cleanup(fail(MPPI_EHIP, "MPPI_FUSED_NOISE_GROUPS=-2: no stream wait-value / signal memory"));
-  }
+  if (c->fused_noise_groups == -2 &&
+      (hipMalloc(reinterpret_cast<void**>(&c->sig), 64) != hipSuccess || hipMemset(c->sig, 0, 64) != hipSuccess))
+    return cleanup(fail(MPPI_EHIP, "signal word allocation failed"));
 
   if (hipDeviceSynchronize() != hipSuccess) return cleanup(fail(MPPI_EHIP, "device sync failed"));
   *out = c;

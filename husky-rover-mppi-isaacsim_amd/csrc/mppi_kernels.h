@@ -141,6 +141,9 @@ struct FusedArgs {
   unsigned roll_seq;
 };
 hipError_t launch_step_fused(const RolloutArgs& a, const FusedArgs& z, size_t lds, hipStream_t st, int proj);
+// one wave on `st` that returns once *sig >= seq (unsigned compare) or after `ticks` of the 100 MHz
+// clock: whatever `st` holds next runs after the fused launch's rollout part
+hipError_t launch_gate(const unsigned* sig, unsigned seq, uint64_t ticks, hipStream_t st);
 // record tree finish (mppi_finish_kernel): the fallback where the column-split shape does not fit
 hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, int groups = 1);
 // column-split finish: every workgroup builds the pair-scale table and reduces ncol columns

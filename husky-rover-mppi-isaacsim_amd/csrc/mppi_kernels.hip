@@ -3307,6 +3307,19 @@ hipError_t launch_step_fused(const RolloutArgs& a, const FusedArgs& z, size_t ld
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(64) void mppi_gate_kernel(const unsigned* sig, unsigned seq, uint64_t ticks) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int)(__hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0 &&
+         __builtin_amdgcn_s_memrealtime() - t0 < ticks)
+    __builtin_amdgcn_s_sleep(8);
+}
+
+hipError_t launch_gate(const unsigned* sig, unsigned seq, uint64_t ticks, hipStream_t st) {
+  hipLaunchKernelGGL(mppi_gate_kernel, dim3(1), dim3(64), 0, st, sig, seq, ticks);
+  return hipGetLastError();
+}
+
 hipError_t launch_noise(uint64_t seed, uint64_t n_base, int64_t k_offset, int blocks, int H, float* eps,
                         hipStream_t st, int max_groups) {
   // Grid capped (max_groups, a few workgroups per CU): the noise of step i+2 is generated
