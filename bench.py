@@ -215,7 +215,7 @@ def bilinear_bench(torch, device, reps=20):
 
     NOT on the MPPI step path (the rollout gathers the DEM through L1/L2): a standalone kernel
     for the north-star '>=60 % of HBM roofline on the bilinear kernel' figure.  `frac` is the
-    lookup kernel alone with the queries already binned by 64x64-cell tile; `frac_incl_binning`
+    lookup kernel alone with the queries already binned by 128x128-cell tile; `frac_incl_binning`
     times the binning (count, scan, scatter) and the lookup together on the same stream.
     Algorithmic bytes = the DEM once + 12 B per query (x, y in, h out).
     """
@@ -233,7 +233,7 @@ def bilinear_bench(torch, device, reps=20):
     y = (torch.rand(N, device=device, generator=g) * 2 - 1) * hw
     nt = eng.bilinear_tiles()
     xb, yb = torch.empty_like(x), torch.empty_like(y)
-    perm = torch.empty(N, dtype=torch.int64, device=device)
+    perm = torch.empty(N, dtype=torch.int32, device=device)
     off = torch.empty(nt + 1, dtype=torch.int32, device=device)
     h = torch.empty_like(x)
 
@@ -277,7 +277,7 @@ def bilinear_bench(torch, device, reps=20):
             "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel_avg_ms": round(ms, 4),
             "incl_binning_ms": round(ms_all, 4), "frac_incl_binning": round(achieved_all / HBM_PEAK_GBS, 4),
             "algorithmic_bytes_per_launch": alg,
-            "workload": f"C5 tile {G}^2 DEM (synthetic), N={N} uniform queries binned by 64x64 tile",
+            "workload": f"C5 tile {G}^2 DEM (synthetic), N={N} uniform queries binned by 128x128 tile",
             "scattered_query_ms": round(scat_ms, 3),
             "scattered_frac": round(alg / (scat_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 

@@ -161,7 +161,7 @@ struct mppi_ctx {
   unsigned* level1_cnt = nullptr;
   uint64_t* clk = nullptr;  // [4] chain clock stamps of the last sampled rollout (RolloutArgs::clk)
   // tiled bilinear binning scratch
-  int* bin_tile_of = nullptr;
+  int* bin_tile_of = nullptr;  // per-chunk tile histograms [chunks][tiles]
   size_t bin_n_cap = 0;
   int* bin_counts = nullptr;
   int* bin_cursor = nullptr;
@@ -925,7 +925,7 @@ int enqueue_fused(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, i
     if (last && gated) {  // after the launch, on the noise stream, gated on its rollout part
       gated_slot = v;
       gated_target = target;
-    } else if (last && c->fused_noise_groups > 0 || (last && c->fused_noise_groups == -1)) {
+    } else if (last && (c->fused_noise_groups > 0 || c->fused_noise_groups == -1)) {
       z.noise_eps = c->eps[v];
       z.noise_n_base = target * nb;
       z.noise_groups = c->fused_noise_groups > 0 ? c->fused_noise_groups : std::max(c->num_cus - groups, 1);
@@ -1651,18 +1651,19 @@ int mppi_bilinear_tiles(mppi_ctx* c, int32_t* ntiles) {
 }
 
 int mppi_bin_queries(mppi_ctx* c, const float* x, const float* y, int64_t n, float* xs_out, float* ys_out,
-                     int64_t* perm, int32_t* tile_off) {
+                     int32_t* perm, int32_t* tile_off) {
   if (!c || !x || !y || !xs_out || !ys_out || !perm || !tile_off) return fail(MPPI_EINVAL, "null argument");
   if (!c->Z) return fail(MPPI_ESTATE, "no DEM");
   if (n < 0 || n > INT32_MAX) return fail(MPPI_EINVAL, "n out of range [0, 2^31)");
   HIP_TRY(hipSetDevice(c->device));
   int32_t nt = 0;
   mppi_bilinear_tiles(c, &nt);
-  if ((size_t)std::max<int64_t>(n, 1) > c->bin_n_cap) {
+  const size_t hist = (size_t)bin_chunks(n, nt) * nt;  // [chunks][tiles] per-chunk histograms
+  if (std::max<size_t>(hist, 1) > c->bin_n_cap) {
     if (c->bin_tile_of) HIP_TRY(hipFree(c->bin_tile_of));
     c->bin_tile_of = nullptr;
-    HIP_TRY(hipMalloc(&c->bin_tile_of, (size_t)std::max<int64_t>(n, 1) * sizeof(int)));
-    c->bin_n_cap = (size_t)std::max<int64_t>(n, 1);
+    HIP_TRY(hipMalloc(&c->bin_tile_of, std::max<size_t>(hist, 1) * sizeof(int)));
+    c->bin_n_cap = std::max<size_t>(hist, 1);
   }
   if ((size_t)nt > c->bin_t_cap) {
     if (c->bin_counts) HIP_TRY(hipFree(c->bin_counts));

@@ -166,11 +166,15 @@ hipError_t launch_noise(uint64_t seed, uint64_t n_base, int64_t k_offset, int bl
                         hipStream_t st, int max_groups);
 hipError_t launch_bilinear(const float* Z, int rows, int grid, float x_min, float y_min, float res,
                            const float* xs, const float* ys, float* hs, int64_t n, hipStream_t st);
-// LDS-tiled lookup over queries binned by 64x64-cell DEM tile (tile count = ceil(rows/64)*ceil(cols/64))
-constexpr int BIL_TILE = 64;
+// LDS-tiled lookup over queries binned by BIL_TILE x BIL_TILE-cell DEM tile (tile count =
+// ceil(rows/BIL_TILE) * ceil(cols/BIL_TILE) <= 16384 for rows * cols < 2^28).  Binning: G chunks of
+// the queries, each one workgroup with an LDS histogram (hist[G][ntiles] scratch), the tile
+// counts' exclusive scan, then each chunk scattered from the tile cursors; perm int32 (n < 2^31).
+constexpr int BIL_TILE = 128;
+int bin_chunks(int64_t n, int ntiles);  // G for n queries
 hipError_t launch_bin_queries(const float* xs, const float* ys, int64_t n, float x_min, float y_min, float res,
-                              float rinv, int cdiv, int rows, int grid, int* tile_of, int* counts, int* cursor,
-                              int* off, float* xs_out, float* ys_out, int64_t* perm, hipStream_t st);
+                              float rinv, int cdiv, int rows, int grid, int* hist, int* counts, int* cursor,
+                              int* off, float* xs_out, float* ys_out, int32_t* perm, hipStream_t st);
 hipError_t launch_bilinear_tiled(const float* Z, int rows, int grid, float x_min, float y_min, float res,
                                  float rinv, int cdiv, const float* xs, const float* ys, float* hs,
                                  const int* tile_off, hipStream_t st);

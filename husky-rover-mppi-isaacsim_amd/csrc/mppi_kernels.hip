@@ -2870,8 +2870,9 @@ __global__ __launch_bounds__(256) void mppi_bilinear_kernel(const float* __restr
 // DEM byte is read once and each query moves 12 bytes, the kernel's algorithmic
 // traffic.  Cell index and corners follow projection_warp.py:8-48 exactly as
 // Dem::corners (the same clamping), the height projection_warp.py:70-100.
-constexpr int BIL_TS = 64;
+constexpr int BIL_TS = BIL_TILE;
 constexpr int BIL_W = BIL_TS + 1;
+constexpr int BIL_T = 1024;  // threads of the lookup and binning workgroups
 
 // corner rows (r0, r1) and columns (c0, c1) of a query, clamped as Dem::corners
 __device__ __forceinline__ void query_cell(float x, float y, float x_min, float y_min, float res,
@@ -2903,44 +2904,44 @@ __device__ __forceinline__ float frac_div(float x, float res, float rinv, int cd
   return x / res;
 }
 
-__global__ __launch_bounds__(256) void mppi_bilinear_tiled_kernel(
+__global__ __launch_bounds__(BIL_T) void mppi_bilinear_tiled_kernel(
     const float* __restrict__ Z, int rows, int grid, float x_min, float y_min, float res, float rinv,
     int cdiv, const float* __restrict__ xs, const float* __restrict__ ys, float* __restrict__ hs,
     const int* __restrict__ tile_off, int ntx) {
-  __shared__ float win[BIL_W * BIL_W];
+  extern __shared__ float win[];  // [BIL_W * BIL_W]
   const int tile = blockIdx.x;
   const int q0 = tile_off[tile], q1 = tile_off[tile + 1];
   if (q0 == q1) return;
   const int r0 = (tile / ntx) * BIL_TS, c0 = (tile % ntx) * BIL_TS;
-  {  // stage the window: every load issued before the first LDS store
-    constexpr int NLD = (BIL_W * BIL_W + 255) / 256;
+  {  // stage the window: every load of a round issued before its LDS stores
+    constexpr int NLD = (BIL_W * BIL_W + BIL_T - 1) / BIL_T;
     float tmp[NLD];
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
-      const int idx = threadIdx.x + 256 * k;
+      const int idx = threadIdx.x + BIL_T * k;
       const int wr = idx / BIL_W, wc = idx - wr * BIL_W;
       tmp[k] = (idx < BIL_W * BIL_W) ? Z[(size_t)min(r0 + wr, rows - 1) * grid + min(c0 + wc, grid - 1)] : 0.0f;
     }
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
-      const int idx = threadIdx.x + 256 * k;
+      const int idx = threadIdx.x + BIL_T * k;
       if (idx < BIL_W * BIL_W) win[idx] = tmp[k];
     }
   }
   __syncthreads();
   // BIL_UNROLL queries per thread per pass, loads issued before any is used
   constexpr int BIL_UNROLL = 4;
-  for (int qb = q0 + threadIdx.x; qb < q1; qb += 256 * BIL_UNROLL) {
+  for (int qb = q0 + threadIdx.x; qb < q1; qb += BIL_T * BIL_UNROLL) {
     float xv[BIL_UNROLL], yv[BIL_UNROLL];
 #pragma unroll
     for (int u = 0; u < BIL_UNROLL; ++u) {
-      const int q = qb + 256 * u;
+      const int q = qb + BIL_T * u;
       xv[u] = (q < q1) ? xs[q] : 0.0f;
       yv[u] = (q < q1) ? ys[q] : 0.0f;
     }
 #pragma unroll
     for (int u = 0; u < BIL_UNROLL; ++u) {
-      const int q = qb + 256 * u;
+      const int q = qb + BIL_T * u;
       if (q < q1) {
         const float x = xv[u], y = yv[u];
         int ra, ca, rb, cb;
@@ -2960,19 +2961,42 @@ __global__ __launch_bounds__(256) void mppi_bilinear_tiled_kernel(
   }
 }
 
-// Binning: tile of each query (the tile holding its first corner cell), counts,
-// exclusive scan, stable-free scatter (order inside a tile is arbitrary; perm maps
-// sorted position -> input index).
-__global__ __launch_bounds__(256) void mppi_bin_count_kernel(const float* xs, const float* ys, int64_t n,
-                                                             float x_min, float y_min, float res, float rinv,
-                                                             int cdiv, int rows, int grid, int ntx,
-                                                             int* __restrict__ tile_of, int* counts) {
-  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n; q += (int64_t)gridDim.x * 256) {
-    int ra, ca, rb, cb;
-    query_cell(xs[q], ys[q], x_min, y_min, res, rinv, cdiv, rows, grid, ra, ca, rb, cb);
-    const int t = (ra / BIL_TS) * ntx + ca / BIL_TS;
-    tile_of[q] = t;
-    atomicAdd(&counts[t], 1);
+// Binning: the tile of each query (the tile holding its first corner cell).  G chunks of the
+// queries (bin_chunks), one workgroup each: an LDS histogram over the tiles, written to
+// hist[g][ntiles] and added to the tile counts (one global atomic per non-empty bin per chunk
+// instead of one per query); then the exclusive scan of the counts; then each chunk claims its
+// run of every tile from the tile cursors (one atomic per non-empty bin) and scatters its queries
+// with LDS ranks.  Order inside a tile is arbitrary; perm maps sorted position -> input index.
+__device__ __forceinline__ int query_tile(float x, float y, float x_min, float y_min, float res, float rinv, int cdiv,
+                                          int rows, int grid, int ntx) {
+  int ra, ca, rb, cb;
+  query_cell(x, y, x_min, y_min, res, rinv, cdiv, rows, grid, ra, ca, rb, cb);
+  return (ra / BIL_TS) * ntx + ca / BIL_TS;
+}
+
+int bin_chunks(int64_t n, int ntiles) {
+  // ~16 queries per tile and chunk (runs of 64 B in the scatter), 64 .. 2048 chunks
+  const int64_t g = n / (16 * (int64_t)std::max(ntiles, 1));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(g, std::min<int64_t>(64, (n + 1023) / 1024)), 2048));
+}
+
+__global__ __launch_bounds__(BIL_T) void mppi_bin_hist_kernel(const float* __restrict__ xs, const float* __restrict__ ys,
+                                                              int64_t n, int64_t chunk, float x_min, float y_min,
+                                                              float res, float rinv, int cdiv, int rows, int grid,
+                                                              int ntx, int ntiles, int* __restrict__ hist,
+                                                              int* __restrict__ counts) {
+  extern __shared__ int lh[];  // [ntiles]
+  for (int t = threadIdx.x; t < ntiles; t += BIL_T) lh[t] = 0;
+  __syncthreads();
+  const int64_t b = (int64_t)blockIdx.x * chunk, e = min(n, b + chunk);
+  for (int64_t q = b + threadIdx.x; q < e; q += BIL_T)
+    atomicAdd(&lh[query_tile(xs[q], ys[q], x_min, y_min, res, rinv, cdiv, rows, grid, ntx)], 1);
+  __syncthreads();
+  int* gh = hist + (size_t)blockIdx.x * ntiles;
+  for (int t = threadIdx.x; t < ntiles; t += BIL_T) {
+    const int h = lh[t];
+    gh[t] = h;
+    if (h) atomicAdd(&counts[t], h);
   }
 }
 
@@ -3001,32 +3025,47 @@ __global__ __launch_bounds__(1024) void mppi_bin_scan_kernel(const int* counts, 
   if (threadIdx.x == 1023) off[ntiles] = part[1023];
 }
 
-__global__ __launch_bounds__(256) void mppi_bin_scatter_kernel(const float* xs, const float* ys, int64_t n,
-                                                               const int* tile_of, int* cursor, float* xs_out,
-                                                               float* ys_out, int64_t* perm) {
-  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n; q += (int64_t)gridDim.x * 256) {
-    const int pos = atomicAdd(&cursor[tile_of[q]], 1);
-    xs_out[pos] = xs[q];
-    ys_out[pos] = ys[q];
-    perm[pos] = q;
+__global__ __launch_bounds__(BIL_T) void mppi_bin_scatter_kernel(const float* __restrict__ xs,
+                                                                 const float* __restrict__ ys, int64_t n,
+                                                                 int64_t chunk, float x_min, float y_min, float res,
+                                                                 float rinv, int cdiv, int rows, int grid, int ntx,
+                                                                 int ntiles, const int* __restrict__ hist,
+                                                                 int* __restrict__ cursor, float* __restrict__ xs_out,
+                                                                 float* __restrict__ ys_out, int32_t* __restrict__ perm) {
+  extern __shared__ int lb[];  // [ntiles] this chunk's next position in each tile
+  const int* gh = hist + (size_t)blockIdx.x * ntiles;
+  for (int t = threadIdx.x; t < ntiles; t += BIL_T) {
+    const int h = gh[t];
+    lb[t] = h ? atomicAdd(&cursor[t], h) : 0;
+  }
+  __syncthreads();
+  const int64_t b = (int64_t)blockIdx.x * chunk, e = min(n, b + chunk);
+  for (int64_t q = b + threadIdx.x; q < e; q += BIL_T) {
+    const float x = xs[q], y = ys[q];
+    const int pos = atomicAdd(&lb[query_tile(x, y, x_min, y_min, res, rinv, cdiv, rows, grid, ntx)], 1);
+    xs_out[pos] = x;
+    ys_out[pos] = y;
+    perm[pos] = (int32_t)q;
   }
 }
 
 hipError_t launch_bin_queries(const float* xs, const float* ys, int64_t n, float x_min, float y_min, float res,
-                              float rinv, int cdiv, int rows, int grid, int* tile_of, int* counts, int* cursor,
-                              int* off, float* xs_out, float* ys_out, int64_t* perm, hipStream_t st) {
+                              float rinv, int cdiv, int rows, int grid, int* hist, int* counts, int* cursor,
+                              int* off, float* xs_out, float* ys_out, int32_t* perm, hipStream_t st) {
   const int ntx = (grid + BIL_TS - 1) / BIL_TS, nty = (rows + BIL_TS - 1) / BIL_TS;
   const int ntiles = ntx * nty;
   hipError_t e = hipMemsetAsync(counts, 0, (size_t)ntiles * sizeof(int), st);
   if (e != hipSuccess) return e;
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
+  const int G = bin_chunks(n, ntiles);
+  const int64_t chunk = (n + G - 1) / G;
+  const size_t lds = (size_t)ntiles * sizeof(int);
   if (n > 0)
-    hipLaunchKernelGGL(mppi_bin_count_kernel, dim3(blocks), dim3(256), 0, st, xs, ys, n, x_min, y_min, res, rinv,
-                       cdiv, rows, grid, ntx, tile_of, counts);
+    hipLaunchKernelGGL(mppi_bin_hist_kernel, dim3(G), dim3(BIL_T), lds, st, xs, ys, n, chunk, x_min, y_min, res, rinv,
+                       cdiv, rows, grid, ntx, ntiles, hist, counts);
   hipLaunchKernelGGL(mppi_bin_scan_kernel, dim3(1), dim3(1024), 0, st, counts, ntiles, off, cursor);
   if (n > 0)
-    hipLaunchKernelGGL(mppi_bin_scatter_kernel, dim3(blocks), dim3(256), 0, st, xs, ys, n, tile_of, cursor, xs_out,
-                       ys_out, perm);
+    hipLaunchKernelGGL(mppi_bin_scatter_kernel, dim3(G), dim3(BIL_T), lds, st, xs, ys, n, chunk, x_min, y_min, res,
+                       rinv, cdiv, rows, grid, ntx, ntiles, hist, cursor, xs_out, ys_out, perm);
   return hipGetLastError();
 }
 
@@ -3034,8 +3073,8 @@ hipError_t launch_bilinear_tiled(const float* Z, int rows, int grid, float x_min
                                  float rinv, int cdiv, const float* xs, const float* ys, float* hs,
                                  const int* tile_off, hipStream_t st) {
   const int ntx = (grid + BIL_TS - 1) / BIL_TS, nty = (rows + BIL_TS - 1) / BIL_TS;
-  hipLaunchKernelGGL(mppi_bilinear_tiled_kernel, dim3(ntx * nty), dim3(256), 0, st, Z, rows, grid, x_min, y_min,
-                     res, rinv, cdiv, xs, ys, hs, tile_off, ntx);
+  hipLaunchKernelGGL(mppi_bilinear_tiled_kernel, dim3(ntx * nty), dim3(BIL_T), (size_t)BIL_W * BIL_W * sizeof(float),
+                     st, Z, rows, grid, x_min, y_min, res, rinv, cdiv, xs, ys, hs, tile_off, ntx);
   return hipGetLastError();
 }
 

@@ -304,15 +304,16 @@ int mppi_bilinear_query(mppi_ctx* ctx, const float* x_dev, const float* y_dev, f
                         int64_t n);
 
 /* LDS-tiled DEM lookup (projection_warp.py:8-100 per query).
- * mppi_bin_queries reorders n device-resident query points by 64x64-cell DEM
- * tile: xs_out/ys_out [n] tile by tile, perm[pos] = input index of the point now
- * at pos, tile_off [ntiles+1] (ntiles from mppi_bilinear_tiles); synchronous.
- * mppi_bilinear_tiled then computes h[pos] for the binned points, each tile's
- * window staged once in LDS; it is ASYNCHRONOUS on the context stream
- * (mppi_sync waits).  Results are bitwise identical to mppi_bilinear_query. */
+ * mppi_bin_queries reorders n < 2^31 device-resident query points by 128x128-cell
+ * DEM tile: xs_out/ys_out [n] tile by tile, perm[pos] = input index (int32) of the
+ * point now at pos, tile_off [ntiles+1] (ntiles from mppi_bilinear_tiles);
+ * synchronous (order inside a tile is unspecified).  mppi_bilinear_tiled then
+ * computes h[pos] for the binned points, each tile's window staged once in LDS; it
+ * is ASYNCHRONOUS on the context stream (mppi_sync waits).  Results are bitwise
+ * identical to mppi_bilinear_query. */
 int mppi_bilinear_tiles(mppi_ctx* ctx, int32_t* ntiles);
 int mppi_bin_queries(mppi_ctx* ctx, const float* x_dev, const float* y_dev, int64_t n, float* xs_out_dev,
-                     float* ys_out_dev, int64_t* perm_dev, int32_t* tile_off_dev);
+                     float* ys_out_dev, int32_t* perm_dev, int32_t* tile_off_dev);
 int mppi_bilinear_tiled(mppi_ctx* ctx, const float* xs_dev, const float* ys_dev,
                         const int32_t* tile_off_dev, float* h_dev);
 /* Wait for all work enqueued on the context stream. */

@@ -41,7 +41,7 @@ def test_bilinear_query_and_tiled_match_oracle(which):
     import torch
     if which == "c3":
         Z, hw, _ = hp.c3_scene()
-    else:   # ragged map: rows/cols not multiples of the 64-cell tile
+    else:   # ragged map: rows/cols not multiples of the 128-cell tile
         rng = np.random.default_rng(3)
         Z = rng.normal(size=(203, 203)).astype(np.float32)
         hw = 10.15
@@ -60,7 +60,7 @@ def test_bilinear_query_and_tiled_match_oracle(which):
     nt = eng.bilinear_tiles()
     xs = torch.empty_like(xd)
     ys = torch.empty_like(xd)
-    perm = torch.empty(n, dtype=torch.int64, device="cuda")
+    perm = torch.empty(n, dtype=torch.int32, device="cuda")
     off = torch.empty(nt + 1, dtype=torch.int32, device="cuda")
     eng.bin_queries(xd.data_ptr(), yd.data_ptr(), n, xs.data_ptr(), ys.data_ptr(), perm.data_ptr(), off.data_ptr())
     o = off.cpu().numpy()
@@ -85,7 +85,7 @@ def test_bin_queries_empty():
     assert nt == 1
     e = torch.empty(1, device="cuda")   # valid pointers; n = 0
     off = torch.full((nt + 1,), -1, dtype=torch.int32, device="cuda")
-    perm = torch.empty(1, dtype=torch.int64, device="cuda")
+    perm = torch.empty(1, dtype=torch.int32, device="cuda")
     eng.bin_queries(e.data_ptr(), e.data_ptr(), 0, e.data_ptr(), e.data_ptr(), perm.data_ptr(), off.data_ptr())
     assert off.cpu().tolist() == [0, 0]
     eng.close()
