@@ -1644,6 +1644,9 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 // ~98 and ~120 us (profiles/r02_notes.md); 0: ~9900 against ~9200 steps/s
 #define MPPI_SIDE_PRIO 0
 #endif
+#ifndef MPPI_PROD_PRIO
+#define MPPI_PROD_PRIO MPPI_SIDE_PRIO  // the producer's (the chain waits on it each step)
+#endif
 constexpr int ROLE_CHAIN = 0, ROLE_PROD = 1, ROLE_WHEEL = 2, ROLE_COST = 3, NROLES = 4;
 
 // FUSED: returns the workgroup's ticket (its rank among the workgroups that have completed their
@@ -1673,6 +1676,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
   const int tj = grp * 64 + (tid & 63);  // trajectory within the workgroup
   if (a.wave_prio) {  // above the deferred optimal rollout (priority 0); the chain above all
     if (role == ROLE_CHAIN) __builtin_amdgcn_s_setprio(3);
+    else if (role == ROLE_PROD) __builtin_amdgcn_s_setprio(MPPI_PROD_PRIO);
     else __builtin_amdgcn_s_setprio(MPPI_SIDE_PRIO);
   }
   int* f_prod = flags + grp;
