@@ -78,6 +78,8 @@ def parse():
                     help="record the rollout kernel's HIP events inside the timed region (not a separate pass)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 full-step leg (N=1)")
     ap.add_argument("--no-costmap", action="store_true", help="skip the obstacle-costmap builder leg")
+    ap.add_argument("--no-sync-pass", action="store_true",
+                    help="skip the synchronous-mode pass (profiling runs: only the headline schedule's launches)")
     ap.add_argument("--sync", action="store_true",
                     help="report the synchronous mode (no deferred optimal rollout) as the headline")
     ap.add_argument("--prewarm-ms", type=float, default=150.0,
@@ -482,7 +484,7 @@ def main():
         prewarm_steps += 1
     run.outputs()
     # synchronous MPPI_step semantics first (every output in host memory when step() returns)
-    el_sync = timed_run(torch, dist, run, args.proj, args.warmup, args.steps, 0, False)
+    el_sync = None if args.no_sync_pass else timed_run(torch, dist, run, args.proj, args.warmup, args.steps, 0, False)
     # headline: the optimal rollout of step i (it only feeds trajectories_sim) overlaps step i+1;
     # every step's outputs still reach pinned host memory inside the timed region
     s0 = args.warmup + args.steps
@@ -593,9 +595,10 @@ def main():
                 "rollout_kernel": info,
                 "pipelined_tail": not args.sync,
                 "prewarm": {"ms": args.prewarm_ms, "steps": prewarm_steps},
-                "sync_steps_per_s": round(args.steps / el_sync, 3),
-                "sync_ms_per_step": round(el_sync / args.steps * 1e3, 4),
-                "finish_kernel_avg_ms": round(fin_ms / max(n_fin, 1), 5),
+                "sync_steps_per_s": round(args.steps / el_sync, 3) if el_sync else None,
+                "sync_ms_per_step": round(el_sync / args.steps * 1e3, 4) if el_sync else None,
+                # (a fused step launch has no separate finish kernel: it is inside the kernel timed above)
+                "finish_kernel_avg_ms": round(fin_ms / max(n_fin, 1), 5) if not info.get("fused") else None,
                 "chain": {"instructions_per_step": chain_static(),
                           "cycles_per_step": round(clock["cycles_per_step"], 1),
                           "shader_clock_mhz": round(clock["shader_mhz"], 1),

@@ -279,6 +279,8 @@ class Engine:
         H = self.H
         self._buf = {n: np.zeros(3 * H if n.endswith("_sim") else H, np.float32) for n in self.OUT_NAMES}
         self._out = MppiOutputs(*[_fp(self._buf[n]) for n in self.OUT_NAMES])
+        self._outref = C.byref(self._out)
+        self._step_fn = self.lib.mppi_step   # the per-step call, bound once (it sits on the step's host path)
         self._keep = []
         self.async_tail = False
 
@@ -388,7 +390,9 @@ class Engine:
                     right_wheel_sim=b["right_wheel_sim"].reshape(H, 3).copy())
 
     def step(self, proj="3d", step=0, copy=True):
-        self._c(self.lib.mppi_step(self.ctx, PROJ[proj], int(step), C.byref(self._out)), "mppi_step")
+        rc = self._step_fn(self.ctx, PROJ[proj], int(step), self._outref)
+        if rc != MPPI_OK:
+            self._c(rc, "mppi_step")
         return self._outputs() if copy else None
 
     def step_injected(self, u1, u2, proj="3d"):

@@ -20,8 +20,9 @@ from collections import defaultdict
 
 def short(name):
     name = name.strip('"')
-    for key in ("mppi_rollout_roles_kernel", "mppi_rollout_pair_kernel", "mppi_noise_kernel", "mppi_tail_kernel",
-                "mppi_colfin_kernel", "mppi_finish_kernel", "mppi_bilinear_kernel"):
+    for key in ("mppi_rollout_roles_kernel", "mppi_rollout_pair_kernel", "mppi_step_fused_kernel", "mppi_noise_kernel",
+                "mppi_tail_kernel", "mppi_gate_kernel", "mppi_colfin_kernel", "mppi_finish_kernel",
+                "mppi_bilinear_kernel"):
         if key in name:
             return key
     return name.split("(")[0][:60]

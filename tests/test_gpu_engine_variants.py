@@ -9,7 +9,10 @@ Each toggle below changes only WHERE or WHEN work runs, never the arithmetic:
   MPPI_ROLES=0/1    the pair rollout kernel / the role-split one at any K
   MPPI_NOISE_GPC=1  noise grid of one workgroup per CU
   MPPI_FUSED=0      rollout, finish and noise as three launches instead of the fused step launch
-  MPPI_FUSED_NOISE_GROUPS=0/7  the fused launch without its noise workgroups / with only 7
+  MPPI_FUSED=1      the fused launch for synchronous steps only (three launches with the deferred tail)
+  MPPI_FUSED_NOISE_GROUPS=0/7/-1  the fused launch's noise before it on the context stream / inside it
+                    on 7 workgroups / inside it on one workgroup per CU (default: after it on the
+                    noise stream behind a gate kernel)
   MPPI_WAVE_PRIO=0  rollout waves at the default issue priority (no s_setprio)
 The toggles are read when a context is created, so each variant gets its own engine.
 Sizes: n = 256 leaf records (C3 K) and n = 1024 (C5 K) at a short horizon.
@@ -58,11 +61,13 @@ def _run(env, K, H, steps=3, info=None, step_ids=None):
 @pytest.mark.parametrize("env", [{"MPPI_COLFIN": "0"}, {"MPPI_UCACHE": "0"}, {"MPPI_NOISE_AT": "1"},
                                  {"MPPI_NOISE_AT": "2"}, {"MPPI_NOISE_AHEAD": "1"}, {"MPPI_ROLES": "0"},
                                  {"MPPI_ROLES": "1"}, {"MPPI_NOISE_GPC": "1"}, {"MPPI_FUSED": "0"},
-                                 {"MPPI_FUSED_NOISE_GROUPS": "0"}, {"MPPI_FUSED_NOISE_GROUPS": "7"},
+                                 {"MPPI_FUSED": "1"}, {"MPPI_FUSED_NOISE_GROUPS": "0"},
+                                 {"MPPI_FUSED_NOISE_GROUPS": "7"}, {"MPPI_FUSED_NOISE_GROUPS": "-1"},
                                  {"MPPI_WAVE_PRIO": "0"}],
                          ids=["record-tree", "no-ucache", "noise-after-finish", "noise-beside-rollout",
                               "noise-one-ahead", "pair-kernel", "role-split-kernel", "noise-1-per-cu",
-                              "unfused", "fused-noise-separate", "fused-7-noise-groups", "no-wave-priority"])
+                              "unfused", "fused-sync-only", "fused-noise-separate", "fused-7-noise-groups",
+                              "fused-noise-inside", "no-wave-priority"])
 def test_variant_bitwise_equal(K, H, env):
     ref, ref_costs = _run({}, K, H)
     got, got_costs = _run(env, K, H)
@@ -127,7 +132,8 @@ def test_timing_modes():
         for i in range(4, 8):
             eng.step("3d", i, copy=False)
         roll, fin, n = eng.timing()
-        assert n == 4 and roll > 0.0 and fin > 0.0
+        fused = eng.launch_info()["fused"] == 1   # a fused launch times rollout + finish as one kernel
+        assert n == 4 and roll > 0.0 and (fin == 0.0 if fused else fin > 0.0)
         assert eng.tail_timing()[1] >= 3
         with pytest.raises(Exception):
             eng.set_timing(3)
