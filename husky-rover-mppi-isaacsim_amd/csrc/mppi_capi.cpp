@@ -142,12 +142,13 @@ struct mppi_ctx {
   long tr_n = 0;
   int wave_prio = 1;  // rollout waves raise their issue priority (env MPPI_WAVE_PRIO=0: off)
   int roles = -1;     // rollout kernel: -1 auto (role split at <= 1 workgroup per CU), 0 pair, 1 roles (MPPI_ROLES)
-  int fused = 2;               // one launch per step (mppi_step_fused_kernel): 0 never, 1 synchronous steps only,
-                               // 2 also with the deferred optimal rollout (MPPI_FUSED)
-  int fused_noise_groups = -2; // noise of step + 2: -2 after the launch on the noise stream behind a gate kernel
-                               // that waits for the launch's rollout part (default), -1 inside the launch on one
-                               // workgroup per CU the finish leaves, n > 0 on n workgroups, 0 before the launch on
-                               // the context stream (MPPI_FUSED_NOISE_GROUPS)
+  int fused = 1;               // one launch per step (mppi_step_fused_kernel): 0 never, 1 synchronous steps only,
+                               // 2 also with the deferred optimal rollout (MPPI_FUSED; 2 is faster on average but
+                               // unstable run to run: profiles/r03_notes.md)
+  int fused_noise_groups = -1; // noise of step + 2: -1 inside the launch on one workgroup per CU the finish leaves
+                               // (default), n > 0 on n workgroups, 0 before the launch on the context stream, -2
+                               // after the launch on the noise stream behind a gate kernel that waits for the
+                               // launch's rollout part (MPPI_FUSED_NOISE_GROUPS)
   // fused launch: the noise of step + 2 on the noise stream behind a one-wave gate kernel that
   // waits for this word, which the launch writes when its rollout part is done
   // (MPPI_FUSED_NOISE_GROUPS=-2); nullptr otherwise

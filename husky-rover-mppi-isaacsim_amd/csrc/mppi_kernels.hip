@@ -2329,32 +2329,35 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
   f2* lr = reinterpret_cast<f2*>(chain);  // [H] (L, R) pairs; chain is free until the optimal rollout
   if (wave == 0) {
     if (lane == 0) {
+      // blocks of FB steps: the next block's input pairs are read (LDS) before this block's
+      // recurrence and its results written after it, so the recurrence never waits for an LDS
+      // write to complete (LDS reads and writes share one in-order counter)
+      constexpr int FB = 8;
       const f2* in2 = reinterpret_cast<const f2*>(uo);
       const f2 a2 = bc2(f.oa);
       f2 LR = f2{f.wl, f.wr};
-      int t = 0;
-      if (H >= 4) {
-        f2 i0 = in2[0], i1 = in2[1], i2 = in2[2], i3 = in2[3];
-        for (; t + 4 <= H; t += 4) {
-          const int tn = min(t + 4, H - 4);  // the next four pairs (clamped: re-read at the end)
-          const f2 n0 = in2[tn], n1 = in2[tn + 1], n2 = in2[tn + 2], n3 = in2[tn + 3];
-          LR = LR * a2 + i0;
-          lr[t] = LR;
-          LR = LR * a2 + i1;
-          lr[t + 1] = LR;
-          LR = LR * a2 + i2;
-          lr[t + 2] = LR;
-          LR = LR * a2 + i3;
-          lr[t + 3] = LR;
-          i0 = n0;
-          i1 = n1;
-          i2 = n2;
-          i3 = n3;
+      f2 cur[FB];
+#pragma unroll
+      for (int k = 0; k < FB; ++k) cur[k] = in2[min(k, H - 1)];
+      for (int t = 0; t < H; t += FB) {
+        f2 nxt[FB], o[FB];
+#pragma unroll
+        for (int k = 0; k < FB; ++k) nxt[k] = in2[min(t + FB + k, H - 1)];
+#pragma unroll
+        for (int k = 0; k < FB; ++k) {
+          LR = LR * a2 + cur[k];  // steps past H are computed and dropped
+          o[k] = LR;
         }
-      }
-      for (; t < H; ++t) {
-        LR = LR * a2 + in2[t];
-        lr[t] = LR;
+        if (t + FB <= H) {
+#pragma unroll
+          for (int k = 0; k < FB; ++k) lr[t + k] = o[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < FB; ++k)
+            if (t + k < H) lr[t + k] = o[k];
+        }
+#pragma unroll
+        for (int k = 0; k < FB; ++k) cur[k] = nxt[k];
       }
     }
 #ifdef MPPI_STAMPS

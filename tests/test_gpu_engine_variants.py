@@ -9,10 +9,10 @@ Each toggle below changes only WHERE or WHEN work runs, never the arithmetic:
   MPPI_ROLES=0/1    the pair rollout kernel / the role-split one at any K
   MPPI_NOISE_GPC=1  noise grid of one workgroup per CU
   MPPI_FUSED=0      rollout, finish and noise as three launches instead of the fused step launch
-  MPPI_FUSED=1      the fused launch for synchronous steps only (three launches with the deferred tail)
-  MPPI_FUSED_NOISE_GROUPS=0/7/-1  the fused launch's noise before it on the context stream / inside it
-                    on 7 workgroups / inside it on one workgroup per CU (default: after it on the
-                    noise stream behind a gate kernel)
+  MPPI_FUSED=2      the fused launch also with the deferred tail (default: synchronous steps only)
+  MPPI_FUSED_NOISE_GROUPS=0/7/-2  the fused launch's noise before it on the context stream / inside it
+                    on 7 workgroups / after it on the noise stream behind a gate kernel (default:
+                    inside it on one workgroup per CU the finish leaves)
   MPPI_WAVE_PRIO=0  rollout waves at the default issue priority (no s_setprio)
 The toggles are read when a context is created, so each variant gets its own engine.
 Sizes: n = 256 leaf records (C3 K) and n = 1024 (C5 K) at a short horizon.
@@ -61,13 +61,13 @@ def _run(env, K, H, steps=3, info=None, step_ids=None):
 @pytest.mark.parametrize("env", [{"MPPI_COLFIN": "0"}, {"MPPI_UCACHE": "0"}, {"MPPI_NOISE_AT": "1"},
                                  {"MPPI_NOISE_AT": "2"}, {"MPPI_NOISE_AHEAD": "1"}, {"MPPI_ROLES": "0"},
                                  {"MPPI_ROLES": "1"}, {"MPPI_NOISE_GPC": "1"}, {"MPPI_FUSED": "0"},
-                                 {"MPPI_FUSED": "1"}, {"MPPI_FUSED_NOISE_GROUPS": "0"},
-                                 {"MPPI_FUSED_NOISE_GROUPS": "7"}, {"MPPI_FUSED_NOISE_GROUPS": "-1"},
+                                 {"MPPI_FUSED": "2"}, {"MPPI_FUSED_NOISE_GROUPS": "0"},
+                                 {"MPPI_FUSED_NOISE_GROUPS": "7"}, {"MPPI_FUSED_NOISE_GROUPS": "-2"},
                                  {"MPPI_WAVE_PRIO": "0"}],
                          ids=["record-tree", "no-ucache", "noise-after-finish", "noise-beside-rollout",
                               "noise-one-ahead", "pair-kernel", "role-split-kernel", "noise-1-per-cu",
-                              "unfused", "fused-sync-only", "fused-noise-separate", "fused-7-noise-groups",
-                              "fused-noise-inside", "no-wave-priority"])
+                              "unfused", "fused-pipelined-too", "fused-noise-separate", "fused-7-noise-groups",
+                              "fused-noise-gated", "no-wave-priority"])
 def test_variant_bitwise_equal(K, H, env):
     ref, ref_costs = _run({}, K, H)
     got, got_costs = _run(env, K, H)
