@@ -304,9 +304,9 @@ Plan make_plan(const mppi_ctx* c) {
     if (pl.ucache_steps > 0) pl.lds_bytes = base + (size_t)pl.ucache_steps * row2;
   }
   // finish kernel: tree phase [16][2H+2] doubles + 64 x (15 PairScale + 16 m); phase 2
-  // uo[2H] v[H] w[H] sin[H] cos[H] chain[12H] out[16H] floats
+  // uo[2][PS] v[H] w[H] sin[H] cos[H] chain[12H] out[16H] lr[2][PS] floats (fin_phase2_floats)
   pl.fin_tree_bytes = (size_t)16 * (2 * H + 2) * sizeof(double) + (size_t)64 * (15 * 16 + 16 * 4);
-  pl.fin_win_offset = (int)(((size_t)34 * H * sizeof(float) + 15) / 16 * 16);
+  pl.fin_win_offset = (int)(((size_t)fin_phase2_floats(H) * sizeof(float) + 15) / 16 * 16);
   pl.fin_lds_bytes = std::max(pl.fin_tree_bytes, (size_t)pl.fin_win_offset);
   return pl;
 }

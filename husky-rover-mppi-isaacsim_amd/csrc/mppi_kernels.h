@@ -96,6 +96,11 @@ struct RolloutArgs {
 // clk layout: [0..8) the stamps above, then (role-split kernel) [kClkBase + 2 b], [.. + 1] =
 // s_memrealtime when workgroup b (< kClkBlocks) starts and when its record is written
 constexpr int kClkBase = 8, kClkBlocks = 4096;
+// The finish's phase-2 LDS (finish_phase2): uo[2][PS] v w sin cos[H] chain[12H] out[16H]
+// lr[2][PS] floats, PS = the filter rows' stride (a multiple of 4 floats, >= H + 32 for the
+// filter's read-ahead); the DEM window (LDS finish) starts at fin_phase2_floats(H) floats.
+__host__ __device__ inline int fin_plane_stride(int H) { return ((H + 3) & ~3) + 32; }
+__host__ __device__ inline int fin_phase2_floats(int H) { return 4 * fin_plane_stride(H) + 32 * H; }
 
 
 // The rollout kernel (mppi_rollout_pair_kernel): 256 trajectories per 512-thread workgroup, a

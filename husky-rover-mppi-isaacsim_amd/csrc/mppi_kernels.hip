@@ -483,6 +483,7 @@ __device__ __forceinline__ void chain3d_lean(const Dem<false>& dem, float res_ha
 // reference computes the same operation on x and y.  Range guards and the IEEE redo as
 // chain3d_lean.
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 bc2(float s) { return f2{s, s}; }
 // [x > 0] for an int x in one v_med3_i32 (written out: the compiler rewrites min(max(x, 0), 1)
@@ -764,11 +765,13 @@ __device__ __forceinline__ int costmap_index(int size, float hw, const Recip& rr
 
 #ifdef MPPI_STAMPS
 // Diagnostic build only (profiles/ubench/stamps.sh): per-wave cycle stamps.
-__device__ uint64_t g_dbg_stamps[64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8 + 16];
+__device__ uint64_t g_dbg_stamps[64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8 + 32];
 #define FIN_STAMP(k)                                                                    \
   do {                                                                                  \
-    if (threadIdx.x == 0)                                                               \
+    if (threadIdx.x == 0) {                                                             \
       g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+      g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+    }                                                                                   \
   } while (0)
 #define LEAF_STAMP(k)                                                                   \
   do {                                                                                  \
@@ -793,7 +796,7 @@ __device__ __forceinline__ float wave_min(float v) {
 }
 
 // Record combine a (+) b for element j (oracle/mppi_ref.py combine).
-struct PairScale {
+struct __attribute__((aligned(16))) PairScale {  // one 16-byte LDS read
   float m;
   float ea, eb;
   int mode;  // 0 normal, 1 take a, 2 take b
@@ -820,6 +823,21 @@ __device__ __forceinline__ double pair_apply(const PairScale& p, double a, doubl
   if (p.mode == 2) return b;
   if (j == 0) return (double)p.m;
   return (double)p.ea * a + (double)p.eb * b;
+}
+// The same value without branches (selects after the arithmetic; what a discarded product of an
+// empty side holds does not matter): a wave's pair applies then issue their LDS reads together
+// instead of a dependent read of `mode`, a branch, then a read of the scales, per pair.
+// (The empty asm statement pins the products ahead of the selects: without it the compiler turns
+// the selects back into branches around the loads.)
+__device__ __forceinline__ PairScale ld_scale(const PairScale* ps) { return *ps; }
+__device__ __forceinline__ double pair_apply_raw(const PairScale p, double a, double b, int j) {
+  double r = (double)p.ea * a + (double)p.eb * b;
+  asm volatile("" : "+v"(r));
+  const double n = j == 0 ? (double)p.m : r;
+  return p.mode == 1 ? a : (p.mode == 2 ? b : n);
+}
+__device__ __forceinline__ double pair_apply_sel(const PairScale& ps, double a, double b, int j) {
+  return pair_apply_raw(ps, a, b, j);
 }
 
 // Subtree over an aligned group of G records (log2 G levels of the binary tree):
@@ -2281,15 +2299,17 @@ __device__ __forceinline__ void signal_done(const FinishArgs& f) {
 // (V/S of the root record); the optimal-sequence filter, the outputs, and the
 // optimal rollout (whole, or step 0 with the rest deferred, f.mode 2), then the
 // completion word.  Called by all `nthreads` threads of one workgroup; smem holds
-// uo[2H] v[H] w[H] sn[H] cs[H] chain[12H] out[16H] floats (+ the DEM window for LDS).
+// uo[2][PS] v[H] w[H] sn[H] cs[H] chain[12H] out[16H] lr[2][PS] floats (fin_phase2_floats, then
+// the DEM window for LDS).
 template <bool LDS>
 // qpre: the DEM corners of the robot's cell, loaded at the start of the finish by waves 0 and
 // nthreads / 64 - 1 (the waves that use them here), or nullptr.
 __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, unsigned char* smem, int tid,
                                               int nthreads, const float* qpre = nullptr) {
   const int H = f.H;
-  float* uo = reinterpret_cast<float*>(smem);
-  float* vb = uo + 2 * H;
+  const int PS = fin_plane_stride(H);
+  float* uo = reinterpret_cast<float*>(smem);  // [2][PS]: the L inputs, then the R inputs
+  float* vb = uo + 2 * PS;
   float* wb = vb + H;
   float* snb = wb + H;
   float* csb = snb + H;
@@ -2297,14 +2317,15 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
   // outputs are staged here and stored to f.out (pinned host memory) in one burst at the
   // end: a workgroup barrier after host stores would wait for their PCIe round trip
   float* ostage = chain + 12 * H;  // [16H]
+  float* lrp = ostage + 16 * H;    // [2][PS]: the filtered L, then R (16-byte aligned)
   const int nout = f.mode == 2 ? 4 * H + 12 : 16 * H;
   const float one_m_a = 1.0f - f.oa;
   if (tid < 2 * H) {
     f.u_nom_next[tid] = ures;
     ostage[tid] = ures;
     // optimal-sequence wheel filter (sampling_warp.py:120-138, k=3.0, a=0.92): the
-    // inputs (u*k)*(1-a) in parallel, only the recurrence L = L*a + in on lane 0
-    uo[tid < H ? 2 * tid : 2 * (tid - H) + 1] = (ures * f.ok) * one_m_a;  // (L, R) input pairs
+    // inputs (u*k)*(1-a) in parallel, only the recurrences L = L*a + in on two lanes
+    uo[tid < H ? tid : PS + (tid - H)] = (ures * f.ok) * one_m_a;
   }
   float* win = reinterpret_cast<float*>(smem + f.win_offset);
   if constexpr (LDS) {
@@ -2323,41 +2344,67 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
   dem.init(f.Z, win, f.rows, f.grid, f.wx0, f.wy0, f.W, f.Wr, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
   dem.N = f.ntab;
   const int lane = tid & 63, wave = tid >> 6;
-  // the recurrence L = L a + in_L, R = R a + in_R on lane 0 of wave 0 with (L, R) packed: one
-  // v_pk_mul and one v_pk_add per step (IEEE per component: the reference's two roundings), the
-  // input pairs read four steps ahead, each step's (L, R) stored to LDS (no per-step select)
-  f2* lr = reinterpret_cast<f2*>(chain);  // [H] (L, R) pairs; chain is free until the optimal rollout
   if (wave == 0) {
-    if (lane == 0) {
-      // blocks of FB steps: the next block's input pairs are read (LDS) before this block's
-      // recurrence and its results written after it, so the recurrence never waits for an LDS
-      // write to complete (LDS reads and writes share one in-order counter)
-      constexpr int FB = 8;
-      const f2* in2 = reinterpret_cast<const f2*>(uo);
-      const f2 a2 = bc2(f.oa);
-      f2 LR = f2{f.wl, f.wr};
-      f2 cur[FB];
+    if (lane < 2) {
+      // The two recurrences L = L a + in_L (lane 0) and R = R a + in_R (lane 1), one v_mul and one
+      // v_add per step (the reference's two IEEE roundings), each lane over its own planar row.
+      // A lone wave's LDS instructions cost far more issue time than its VALU ones (one lane
+      // packing (L, R) with a read and a write per two steps: ~44 cycles per step against ~23
+      // here, profiles/ubench/filt.hip), so every LDS access moves 4 steps (ds_read/write_b128):
+      // two blocks of 16 steps per iteration, each block's inputs read one block before it runs
+      // (the read-ahead stays inside the row's PS >= H + 32 floats), results written after it
+      const f4* p = reinterpret_cast<const f4*>(uo + lane * PS);
+      f4* q = reinterpret_cast<f4*>(lrp + lane * PS);
+      const float a = f.oa;
+      float x = lane ? f.wr : f.wl;
+      f4 A[4], B[4];
 #pragma unroll
-      for (int k = 0; k < FB; ++k) cur[k] = in2[min(k, H - 1)];
-      for (int t = 0; t < H; t += FB) {
-        f2 nxt[FB], o[FB];
+      for (int k = 0; k < 4; ++k) A[k] = p[k];
+      int t = 0;
+      for (; t + 32 <= H; t += 32, p += 8, q += 8) {
 #pragma unroll
-        for (int k = 0; k < FB; ++k) nxt[k] = in2[min(t + FB + k, H - 1)];
+        for (int k = 0; k < 4; ++k) B[k] = p[4 + k];
 #pragma unroll
-        for (int k = 0; k < FB; ++k) {
-          LR = LR * a2 + cur[k];  // steps past H are computed and dropped
-          o[k] = LR;
+        for (int k = 0; k < 4; ++k) {
+          x = x * a + A[k].x;
+          A[k].x = x;
+          x = x * a + A[k].y;
+          A[k].y = x;
+          x = x * a + A[k].z;
+          A[k].z = x;
+          x = x * a + A[k].w;
+          A[k].w = x;
         }
-        if (t + FB <= H) {
 #pragma unroll
-          for (int k = 0; k < FB; ++k) lr[t + k] = o[k];
-        } else {
+        for (int k = 0; k < 4; ++k) q[k] = A[k];
 #pragma unroll
-          for (int k = 0; k < FB; ++k)
-            if (t + k < H) lr[t + k] = o[k];
+        for (int k = 0; k < 4; ++k) A[k] = p[8 + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          x = x * a + B[k].x;
+          B[k].x = x;
+          x = x * a + B[k].y;
+          B[k].y = x;
+          x = x * a + B[k].z;
+          B[k].z = x;
+          x = x * a + B[k].w;
+          B[k].w = x;
         }
 #pragma unroll
-        for (int k = 0; k < FB; ++k) cur[k] = nxt[k];
+        for (int k = 0; k < 4; ++k) q[4 + k] = B[k];
+#ifdef MPPI_STAMPS
+        if (t == 0) FIN_STAMP(7);
+        if (t == 32) FIN_STAMP(8);
+#endif
+      }
+#ifdef MPPI_STAMPS
+      FIN_STAMP(14);
+#endif
+      const float* pf = reinterpret_cast<const float*>(p);
+      float* qf = reinterpret_cast<float*>(q);
+      for (int k = 0; t < H; ++t, ++k) {
+        x = x * a + pf[k];
+        qf[k] = x;
       }
     }
 #ifdef MPPI_STAMPS
@@ -2365,7 +2412,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
 #endif
   } else if (wave == nthreads / 64 - 1 && f.mode == 2) {
     if (lane == 0) {  // step 0 of the optimal rollout needs only the first filter step
-      const float L0 = f.wl * f.oa + uo[0], R0 = f.wr * f.oa + uo[1];
+      const float L0 = f.wl * f.oa + uo[0], R0 = f.wr * f.oa + uo[PS];
       const float v0 = clampf((L0 + R0) / 2.0f, f.vmin, f.vmax);
       const float w0 = clampf(((-L0) + R0) / f.rwheel, f.wmin, f.wmax);
       float sn0, cs0;
@@ -2375,8 +2422,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
   }
   __syncthreads();
   for (int t = tid; t < H; t += nthreads) {
-    const f2 LRt = lr[t];
-    const float L = LRt.x, R = LRt.y;
+    const float L = lrp[t], R = lrp[PS + t];
     const float v = clampf((L + R) / 2.0f, f.vmin, f.vmax);
     const float w = clampf(((-L) + R) / f.rwheel, f.wmin, f.wmax);
     float sn, cs;
@@ -2716,32 +2762,55 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
     const int l = log2P - (r <= 1 ? 0 : 32 - __clz(r - 1));
     const int i = g - colfin_level_base(P, l);
     const float* s = mlev + (2 * P - ((2 * P) >> l));
-    lps[g] = pair_scale(s[2 * i], s[2 * i + 1], f.T);
+    // the register levels (l < 4, w = 8 >> l nodes per group) transposed: node k of group gi at
+    // k * NG + gi, so the lanes of one column (consecutive groups) read consecutive entries
+    // (group-major, their 16-byte reads hit the same banks: an up to 32-way conflict)
+    const int lc = min(l, 3);  // (no division by 8 >> l = 0 above level 3)
+    const int dst = l < 4 ? colfin_level_base(P, l) + (i & ((8 >> lc) - 1)) * NG + (i >> (3 - lc)) : g;
+    lps[dst] = pair_scale(s[2 * i], s[2 * i + 1], f.T);
   }
   __syncthreads();
 #ifdef MPPI_STAMPS
   if (blk == 0) FIN_STAMP(9);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (blk == 0) FIN_STAMP(11);
 #endif
-  // (3) the 4 lowest levels of every item in registers
+  // (3) the 4 lowest levels of every item in registers, each level's pair scales read together
+  //     ahead of its arithmetic (one LDS round trip per level, not two per pair), then the
+  //     scales of the shuffle levels, all at once.  (Deeper prefetch raised the fused step
+  //     launch, which shares this code, from 89 to 117 VGPRs.)
   double v0 = 0.0;
+  const int NGW = min(NG, 64);
+  PairScale sh[6];  // the shuffle levels' scales (k = 1, 2, 4, .. < NGW)
   if (has_item) {
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
       const int w = 8 >> l;
-      const PairScale* ps = lps + colfin_level_base(P, l) + it_g * w;
+      PairScale cur[8];
 #pragma unroll
-      for (int i = 0; i < w; ++i) v[i] = pair_apply(ps[i], v[2 * i], v[2 * i + 1], col);
+      for (int i = 0; i < w; ++i) cur[i] = ld_scale(lps + colfin_level_base(P, l) + it_g + i * NG);
+#pragma unroll
+      for (int i = 0; i < w; ++i) v[i] = pair_apply_raw(cur[i], v[2 * i], v[2 * i + 1], col);
     }
     v0 = v[0];
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+      if ((1 << q) < NGW) sh[q] = ld_scale(lps + colfin_level_base(P, 4 + q) + (it_g >> (q + 1)));
   }
+#ifdef MPPI_STAMPS
+  if (blk == 0) FIN_STAMP(15);
+#endif
   // (4a) the next levels inside a wave: a column's NG (<= 64 at a time) consecutive lanes
   //      combine by lane shuffles, left child = the lane with the bit clear (no barrier)
-  const int NGW = min(NG, 64);
   int lvl = 4;
-  for (int k = 1; k < NGW; k *= 2, ++lvl) {
-    const double o = __shfl_xor(v0, k, 64);  // every lane: item groups are NG-aligned
-    if (has_item && (it_g & (2 * k - 1)) == 0)
-      v0 = pair_apply(lps[colfin_level_base(P, lvl) + it_g / (2 * k)], v0, o, col);
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const int k = 1 << q;
+    if (k < NGW) {
+      const double o = __shfl_xor(v0, k, 64);  // every lane: item groups are NG-aligned
+      if (has_item && (it_g & (2 * k - 1)) == 0) v0 = pair_apply_raw(sh[q], v0, o, col);
+      ++lvl;
+    }
   }
   if (has_item && (it_g & (NGW - 1)) == 0) part[it_c * NG + it_g] = v0;
   __syncthreads();
@@ -2753,7 +2822,7 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
       const int c = it % ncols, i = it / ncols;
       const int cc = (c < nc) ? c0 + c : 1;
       double* pc = part + c * NG;
-      pc[2 * stride * i] = pair_apply(ps[i], pc[2 * stride * i], pc[2 * stride * i + stride], cc);
+      pc[2 * stride * i] = pair_apply_sel(ps[i], pc[2 * stride * i], pc[2 * stride * i + stride], cc);
     }
     __syncthreads();
   }

@@ -29,7 +29,7 @@ def main():
     eng.set_dem(Z, hw)
     eng.set_costmap(cm, hw)
     eng.set_state(_lib.make_state(-60.0, -5.0, goal_x=65.0, goal_y=10.0))
-    n = 64 * 16 * 6 + 1024 * 2 + 64 * 8 + 16
+    n = 64 * 16 * 6 + 1024 * 2 + 64 * 8 + 32
     rows = []
     for i in range(12):
         eng.step("3d", i)
@@ -37,7 +37,7 @@ def main():
             eng.outputs()
             buf = (C.c_uint64 * n)()
             assert lib.mppi_debug_stamps(buf, n) == 0
-            rows.append(np.array(buf, dtype=np.float64)[-16:])
+            rows.append(np.array(buf, dtype=np.float64)[-32:])
     fs = np.median(np.array(rows), axis=0)
     us = lambda a, b: (fs[b] - fs[a]) / 100.0  # noqa: E731
     print(f"K={K} H={H} async={asyn}: finish phases (us, median of {len(rows)} steps, workgroup 0 / last)")
@@ -45,6 +45,15 @@ def main():
     print(f"  u_opt read {us(13, 1):.2f}  phase2 setup {us(1, 2):.2f}  filter {us(2, 12):.2f}  "
           f"v/w/sincos {us(12, 3):.2f}  outputs {us(3, 4):.2f}  signal {us(4, 5):.2f}")
     print(f"  total start -> signal {us(0, 5):.2f}")
+    cyc = lambda a, b: fs[16 + b] - fs[16 + a]  # noqa: E731
+    print(f"  shader clock over start -> signal {cyc(0, 5) / us(0, 5):.0f} MHz; filter {cyc(2, 12):.0f} cycles "
+          f"({cyc(2, 12) / us(2, 12):.0f} MHz), register levels {cyc(11, 15):.0f} cycles")
+    if fs[11] > 0:
+        print(f"  columns: leaf loads done {us(9, 11):.2f}  register levels {us(11, 15):.2f}  "
+              f"shuffle/LDS levels {us(15, 10):.2f}")
+    if fs[7] > 0:
+        print(f"  filter: first 16 steps {us(2, 7):.2f}  next 48 {us(7, 8):.2f}  to loop end {us(8, 14):.2f}  "
+              f"tail steps {us(14, 12):.2f}")
 
 
 if __name__ == "__main__":
