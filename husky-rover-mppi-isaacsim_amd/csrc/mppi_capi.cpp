@@ -94,6 +94,7 @@ struct mppi_ctx {
   // step buffers
   float* cost = nullptr;
   double* nodes = nullptr;
+  float* rec_m = nullptr;  // [nodes_cap / E] the records' m, contiguous
   size_t nodes_cap = 0;
   double* scratch0 = nullptr;
   double* scratch1 = nullptr;
@@ -162,6 +163,7 @@ struct mppi_ctx {
   double* level1 = nullptr;       // finish kernel first-level records
   size_t level1_cap = 0;
   unsigned* level1_cnt = nullptr;
+  unsigned long long* uopt = nullptr;  // [2H] the column-split finish's tagged u_opt words
   uint64_t* clk = nullptr;  // [4] chain clock stamps of the last sampled rollout (RolloutArgs::clk)
   // tiled bilinear binning scratch
   int* bin_tile_of = nullptr;  // per-chunk tile histograms [chunks][tiles]
@@ -324,10 +326,13 @@ int ensure_nodes(mppi_ctx* c, int blocks) {
   const size_t need = (size_t)std::max(blocks, 1) * E_of(c);
   if (need <= c->nodes_cap) return MPPI_OK;
   if (c->nodes) hipFree(c->nodes);
+  if (c->rec_m) hipFree(c->rec_m);
   if (c->scratch0) hipFree(c->scratch0);
   if (c->scratch1) hipFree(c->scratch1);
   c->nodes = c->scratch0 = c->scratch1 = nullptr;
+  c->rec_m = nullptr;
   HIP_TRY(hipMalloc(&c->nodes, need * sizeof(double)));
+  HIP_TRY(hipMalloc(&c->rec_m, (size_t)std::max(blocks, 1) * sizeof(float)));
   const size_t half = ((size_t)std::max(blocks, 1) + 1) / 2 * E_of(c);
   HIP_TRY(hipMalloc(&c->scratch0, half * sizeof(double)));
   HIP_TRY(hipMalloc(&c->scratch1, half * sizeof(double)));
@@ -407,6 +412,7 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   a.cost_out = c->cost;
   a.clk = c->clk;
   a.nodes = c->nodes;
+  a.rec_m = c->rec_m;
   a.ustore = c->ustore;
   a.inj_u1 = c->inj1;
   a.inj_u2 = c->inj2;
@@ -419,6 +425,7 @@ void fill_finish(const mppi_ctx* c, const Plan& pl, const mppi_state& st, Finish
   f.T = p.temperature;
   f.scratch0 = c->scratch0;
   f.scratch1 = c->scratch1;
+  f.uopt = c->uopt;
   f.u_nom_next = c->u_nom[c->cur ^ 1];
   f.out = c->stage;
   f.Z = c->Z;
@@ -760,6 +767,7 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
   if (rc) return rc;
   f.recs = recs;
   f.n_recs = n;
+  f.rec_m = recs == c->nodes ? c->rec_m : nullptr;  // this context's rollout records
   if (n > 1) {
     rc = ensure_nodes(c, n);
     if (rc) return rc;
@@ -942,6 +950,7 @@ int enqueue_fused(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, i
   rc = prepare_finish(c, pl, c->st, 1, nullptr, z.f, par);
   if (rc) return rc;
   z.f.recs = c->nodes;
+  z.f.rec_m = c->rec_m;
   z.f.n_recs = pl.blocks;
   if (c->level1_cap < 1 || c->level1_cap * (size_t)E_of(c) < (size_t)E_of(c)) {
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1181,6 +1190,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipHostMalloc(&c->done, 64, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->cdiv_bad, sizeof(unsigned)) != hipSuccess ||
       hipMalloc(&c->level1_cnt, 128) != hipSuccess ||  // [0]: finish handoff, [16]: fused record count
+      hipMalloc(&c->uopt, (size_t)2 * H * sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&c->clk, (kClkBase + 2 * kClkBlocks) * sizeof(uint64_t)) != hipSuccess ||
       hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
@@ -1211,7 +1221,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   c->out_host = new float[16 * H]();
   std::memset(c->stage, 0, 16 * H * sizeof(float));
   *c->done = 0;
-  if (hipMemset(c->level1_cnt, 0, 128) != hipSuccess)
+  if (hipMemset(c->level1_cnt, 0, 128) != hipSuccess || hipMemset(c->uopt, 0, (size_t)2 * H * sizeof(unsigned long long)) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
   if (c->fused_noise_groups == -2 &&
       (hipMalloc(reinterpret_cast<void**>(&c->sig), 64) != hipSuccess || hipMemset(c->sig, 0, 64) != hipSuccess))
@@ -1244,6 +1254,7 @@ void mppi_destroy(mppi_ctx* c) {
   for (float* u : c->u_nom)
     if (u) hipFree(u);
   if (c->cost) hipFree(c->cost);
+  if (c->rec_m) hipFree(c->rec_m);
   if (c->nodes) hipFree(c->nodes);
   if (c->scratch0) hipFree(c->scratch0);
   if (c->scratch1) hipFree(c->scratch1);
@@ -1269,6 +1280,7 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->bin_tile_of) hipFree(c->bin_tile_of);
   if (c->level1) hipFree(c->level1);
   if (c->level1_cnt) hipFree(c->level1_cnt);
+  if (c->uopt) hipFree(c->uopt);
   if (c->clk) hipFree(c->clk);
   if (c->bin_counts) hipFree(c->bin_counts);
   if (c->bin_cursor) hipFree(c->bin_cursor);

@@ -13,6 +13,8 @@ struct FinishArgs {
              // 2: finish with the optimal rollout deferred to mppi_tail_kernel (step 0 only here)
   const double* recs;
   int n_recs;
+  const float* rec_m;  // [n_recs] the records' m contiguous, or null (read from recs)
+  unsigned long long* uopt;  // [2H] colfin: the u_opt handoff words {u bits, seq << 32} (zeroed once)
   double* scratch0;
   double* scratch1;
   double* record_out;  // mode 0
@@ -78,6 +80,7 @@ struct RolloutArgs {
   // outputs
   float* cost_out;   // [K]
   double* nodes;     // [blocks][2H+2]
+  float* rec_m;      // [blocks] or null: each record's m again, contiguous (the finish's scale table)
   float* ustore;     // [blocks][2][H][block] sampled controls kept for the weighted sum
   // injected controls (MODE 1), trajectory-major [K*H]
   const float* inj_u1;

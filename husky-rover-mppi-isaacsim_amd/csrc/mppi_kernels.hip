@@ -765,13 +765,19 @@ __device__ __forceinline__ int costmap_index(int size, float hw, const Recip& rr
 
 #ifdef MPPI_STAMPS
 // Diagnostic build only (profiles/ubench/stamps.sh): per-wave cycle stamps.
-__device__ uint64_t g_dbg_stamps[64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8 + 32];
+__device__ uint64_t g_dbg_stamps[64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8 + 64 + 128 * 4];
 #define FIN_STAMP(k)                                                                    \
   do {                                                                                  \
     if (threadIdx.x == 0) {                                                             \
       g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-      g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+      g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + 32 + (k)] = __builtin_amdgcn_s_memtime(); \
     }                                                                                   \
+  } while (0)
+// per finish workgroup b < 128: [.. + 64 + 4 b + k]
+#define FINWG_STAMP(b, k)                                                                \
+  do {                                                                                  \
+    if (threadIdx.x == 0 && (b) < 128)                                                  \
+      g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + 64 + 4 * (b) + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #define LEAF_STAMP(k)                                                                   \
   do {                                                                                  \
@@ -1032,6 +1038,12 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
       __hip_atomic_store(a.nodes + (size_t)blockIdx.x * E + j, val[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else
       a.nodes[(size_t)blockIdx.x * E + j] = val[0];
+    if (j == 0 && a.rec_m) {  // m again in the contiguous array (one line per 32 records to read)
+      if constexpr (WT)
+        __hip_atomic_store(a.rec_m + blockIdx.x, lm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        a.rec_m[blockIdx.x] = lm[0];
+    }
   }
 }
 
@@ -2679,14 +2691,15 @@ root_ready:
 // One round trip through global memory instead of two (level 1, then the last group) or
 // more (n > 256), and every level but the 4 in registers is an LDS pass.
 // LDS: PairScale[P - 1] | node minima m[2P] (all levels) | partial[ncol + 1][P / 16] doubles.
-constexpr int COLFIN_PMAX = 4096;  // leaf records (K <= 1,048,576 per context)
+constexpr int COLFIN_PMAX = 4096;
+constexpr uint64_t kColfinPollTicks = 200000000ull;  // the last workgroup's u_opt wait bound (2 s)  // leaf records (K <= 1,048,576 per context)
 __device__ __forceinline__ int colfin_level_base(int P, int l) { return P - (P >> l); }
 
 // Records written by this launch's own rollout blocks (fused launch, RECS_WT) are read with
 // agent-scope atomic loads: they bypass a stale line of the previous step's records in this XCD's
 // L2 (the rollout blocks store them write-through).
-template <bool RECS_WT>
-__device__ __forceinline__ double rec_load(const double* p) {
+template <bool RECS_WT, typename V>
+__device__ __forceinline__ V rec_load(const V* p) {
   if constexpr (RECS_WT) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else return *p;
 }
@@ -2730,11 +2743,54 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
   const bool extra_s = c0 > 1;
   const int ncols = nc + (extra_s ? 1 : 0);
   const int NG = P >> 4;  // register groups of 16 leaves per column
-  // (1) leaf values of (column, group) items in registers; loads issued before the scale
-  //     table is built so their latency overlaps it
+  // (1) the records' minima (the scale table waits on them; thread t < T owns the L consecutive
+  //     records [t L, t L + L)), then the leaf values of the (column, group) items on other waves,
+  //     whose latency overlaps the table
+  const int L = P > FIN_THREADS ? P / FIN_THREADS : 1;  // 1, 2 or 4 (P <= COLFIN_PMAX)
+  const int T = P / L;
+  float lm[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+#ifdef MPPI_STAMPS
+  if (blk == 0) FIN_STAMP(18);
+#endif
+  // (2) pair scales: first the node minima (the m pair_scale forms; level l of the minima at
+  //     mlev + 2P - (2P >> l), level 0 the records): a thread's own records, then lane shuffles
+  //     inside the wave, then the waves' minima on wave 0 (two barriers, not log2 P); then every
+  //     node's pair scale in one pass, so the exponentials of all levels run side by side
+  auto lev = [&](int l) __attribute__((always_inline)) { return mlev + (2 * P - ((2 * P) >> l)); };
+  float mm = INFINITY;
+  int ml = 0;  // the level mm belongs to
+  if (tid < T) {  // (loads and their use in one branch: no load of it is pending past the join)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = tid * L + k;
+      if (k < L && r < n)
+        lm[k] = f.rec_m ? rec_load<RECS_WT>(f.rec_m + r) : (float)rec_load<RECS_WT>(recs + (size_t)r * E);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < L) lev(0)[tid * L + k] = lm[k];
+    if (L == 1) {
+      mm = lm[0];
+    } else if (L == 2) {
+      mm = fminf(lm[0], lm[1]);
+      lev(1)[tid] = mm;
+    } else {
+      const float m01 = fminf(lm[0], lm[1]), m23 = fminf(lm[2], lm[3]);
+      lev(1)[2 * tid] = m01;
+      lev(1)[2 * tid + 1] = m23;
+      mm = fminf(m01, m23);
+      lev(2)[tid] = mm;
+    }
+  }
+  ml = L == 1 ? 0 : (L == 2 ? 1 : 2);
+  // the items on the LAST waves (a column's groups in consecutive lanes), clear of the waves
+  // that load the minima where they fit: a wave's loads complete in order, and behind a branch
+  // the compiler waits for all of them (vmcnt(0)) before using the minima
   const int items = ncols * NG;  // <= FIN_THREADS (colfin_shape)
-  const int it_g = tid % NG, it_c = tid / NG;  // a column's groups in consecutive lanes
-  const bool has_item = tid < items;
+  const int item_base = FIN_THREADS - ((items + 63) & ~63);
+  const int it = max(tid - item_base, 0);
+  const int it_g = it % NG, it_c = it / NG;
+  const bool has_item = tid >= item_base && tid - item_base < items;
   const int col = (it_c < nc) ? c0 + it_c : 1;
   double v[16];
   if (has_item) {
@@ -2744,18 +2800,36 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
       v[i] = rec_load<RECS_WT>(recs + (size_t)r * E + col);
     }
   }
-  for (int i = tid; i < P; i += FIN_THREADS)
-    mlev[i] = (i < n) ? (float)rec_load<RECS_WT>(recs + (size_t)i * E) : INFINITY;
-  __syncthreads();
-  // (2) pair scales: first the node minima level by level (one fminf per node, the m that
-  //     pair_scale forms), then every node's pair scale in one pass, so the exponentials of
-  //     the log2(P) levels run side by side instead of one level after another
-  for (int l = 1; (P >> l) >= 1; ++l) {
-    const float* s = mlev + (2 * P - ((2 * P) >> (l - 1)));
-    float* d = mlev + (2 * P - ((2 * P) >> l));
-    for (int i = tid; i < (P >> l); i += FIN_THREADS) d[i] = fminf(s[2 * i], s[2 * i + 1]);
-    __syncthreads();
+  const int TW = min(T, 64);
+  for (int k = 1; k < TW; k *= 2) {  // (left child first in every fminf, as pair_scale forms m)
+    const float o = __shfl_xor(mm, k, 64);
+    mm = (tid & k) ? fminf(o, mm) : fminf(mm, o);
+    ++ml;
+    if (tid < T && (tid & (2 * k - 1)) == 0) lev(ml)[tid / (2 * k)] = mm;
   }
+#ifdef MPPI_STAMPS
+  if (blk == 0 && (tid & 63) == 0)  // each wave's arrival at the barrier: FINWG slot 3 of "workgroup" wave
+    g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + 64 + 4 * (tid >> 6) + 3] = __builtin_amdgcn_s_memrealtime();
+#endif
+  if (T > 64) {
+    __syncthreads();  // the waves' minima (level ml, T / 64 of them)
+    if (tid < 64) {
+      const int NW = T >> 6;
+      float x = tid < NW ? lev(ml)[tid] : INFINITY;
+      int l2 = ml;
+      for (int k = 1; k < NW; k *= 2) {
+        const float o = __shfl_xor(x, k, 64);
+        x = (tid & k) ? fminf(o, x) : fminf(x, o);
+        ++l2;
+        if (tid < NW && (tid & (2 * k - 1)) == 0) lev(l2)[tid / (2 * k)] = x;
+      }
+    }
+  }
+  __syncthreads();
+#ifdef MPPI_STAMPS
+  if (blk == 0) FIN_STAMP(16);
+  if (blk == 0) FIN_STAMP(17);
+#endif
   const int log2P = 31 - __clz(P);
   for (int g = tid; g < P - 1; g += FIN_THREADS) {
     const int r = P - g;  // level l holds nodes g with P >> (l + 1) < P - g <= P >> l
@@ -2835,53 +2909,56 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
     return;
   }
   const double S = extra_s ? part[nc * NG] : part[(1 - c0) * NG];
-  // u_opt of this slice (columns 2 + t), stored write-through at device scope, then the count
-  for (int c = tid; c < nc; c += FIN_THREADS) {
-    const int j = c0 + c;
-    if (j >= 2) {
-      const float u = (S > 0.0) ? (float)(part[c * NG] / S) : 0.0f;
-      __hip_atomic_store(reinterpret_cast<float*>(f.level1) + (j - 2), u, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if (nblk > 1) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // u_opt of this slice (columns 2 + t).  One workgroup: straight from its LDS.  Several: each
+  // stores its slice as tagged words {u, seq} (agent-scope atomic stores) and only the LAST
+  // workgroup (blk nblk - 1: in a fused launch the one with the last ticket) goes on: it polls the
+  // 2H words until each carries this step's seq.  Value and tag travel in one 64-bit word, so
+  // the handoff orders nothing across locations, and no workgroup waits for its stores to
+  // complete or counts itself in (round 2-3's store, vmcnt(0), barrier, counter add, barrier).
+  float ures = 0.0f;
+  if (nblk == 1) {
+    if (tid < 2 * H) ures = (S > 0.0) ? (float)(part[(tid + 2) * NG] / S) : 0.0f;
     __syncthreads();
-    int* flag = reinterpret_cast<int*>(mlev);
-    if (tid == 0) {
-#if MPPI_COLFIN_FENCED
-      // HIP memory model: the workgroup's u_opt stores (ordered before this thread by the barrier)
-      // released at agent scope with the count; the last workgroup acquires before reading them
-      const unsigned prev = __hip_atomic_fetch_add(f.level1_cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-#else
-      // the stores above are agent-scope atomics, written through the XCD's L2,
-      // and complete (vmcnt(0)) before the barrier, so a relaxed count suffices on gfx950
-      const unsigned prev = __hip_atomic_fetch_add(f.level1_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-      const int last = prev == (unsigned)nblk - 1;
-      if (last) {  // re-armed; every finish workgroup has passed its record wait (fused launch)
-        __hip_atomic_store(f.level1_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (RECS_WT) __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      flag[0] = last;
-    }
-    __syncthreads();
-    if (!flag[0]) return;
-#if MPPI_COLFIN_FENCED
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
+    if (RECS_WT && tid == 0) __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    const unsigned long long tag = (unsigned long long)f.seq << 32;
+    for (int c = tid; c < nc; c += FIN_THREADS) {
+      const int j = c0 + c;
+      if (j >= 2) {
+        const float u = (S > 0.0) ? (float)(part[c * NG] / S) : 0.0f;
+        __hip_atomic_store(f.uopt + (j - 2), tag | __builtin_bit_cast(unsigned, u), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+#ifdef MPPI_STAMPS
+    FINWG_STAMP(blk, 0);
+#endif
+    if (blk != nblk - 1) return;
+    int late = 0;
+    if (tid < 2 * H) {  // bounded (2 s of the 100 MHz clock): a lost slice cannot hang the device
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      unsigned long long w = __hip_atomic_load(f.uopt + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while ((unsigned)(w >> 32) != f.seq) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 >= kColfinPollTicks) {
+          late = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        w = __hip_atomic_load(f.uopt + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ures = __builtin_bit_cast(float, (unsigned)w);
+    }
+    // a slice that never came: publish nothing (the host's wait reports the step as failed)
+    if (__syncthreads_or(late)) return;
+#ifdef MPPI_STAMPS
+    FINWG_STAMP(blk, 1);
+#endif
+    // every finish workgroup has passed its record wait (fused launch): re-arm the count
     if (RECS_WT && tid == 0) __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #ifdef MPPI_STAMPS
   FIN_STAMP(13);
 #endif
-  const float ures = (tid < 2 * H)
-                         ? __hip_atomic_load(reinterpret_cast<const float*>(f.level1) + tid, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT)
-                         : 0.0f;
   __syncthreads();  // the tree's LDS is dead from here on
 #ifdef MPPI_STAMPS
   FIN_STAMP(6);
