@@ -396,6 +396,8 @@ def timed_run(torch, dist, run, proj, warmup, steps, step0, async_tail, kernel_t
         run.step(proj, step0 + i)
 
     def barrier():
+        for e in run.engines:  # cancels an armed next step (never part of the timed steps), then syncs
+            e.sync()
         for d in sorted({e.device for e in run.engines}):
             torch.cuda.synchronize(d)
         if dist is not None and run.world > 1:

@@ -62,6 +62,17 @@ struct Plan {
 
 }  // namespace
 
+// Host bookkeeping that enqueueing a sampled step changes (the armed next step is enqueued with
+// these advanced, then they are put back until the step is taken).
+struct Book {
+  unsigned seq = 0, wait_seq = 0;
+  int fin_kind = -1, fin_P = 0, fin_ncol = 0, fin_groups = 0;
+  bool last_fused = false;
+  int tail_par = 0;
+  bool tail_pending = false;
+  bool tail_inflight[kTailSlots] = {};
+};
+
 struct mppi_ctx {
   mppi_params p{};
   int device = 0;
@@ -164,6 +175,29 @@ struct mppi_ctx {
   size_t level1_cap = 0;
   unsigned* level1_cnt = nullptr;
   unsigned long long* uopt = nullptr;  // [2H] the column-split finish's tagged u_opt words
+  // Armed next step (pre-enqueue): after a sampled mppi_step has enqueued its launches, the next
+  // step's launches (step + 1, same projection) are enqueued behind mppi_arm_gate_kernel, which
+  // waits at most arm_ticks for the next call to store the robot state and its go word in pinned
+  // memory; the GPU then starts that step without a host launch on its path.  Any other call on
+  // the context, a different step / projection, or an expired gate cancels it (disarm), and the
+  // call runs the ordinary way.  Off by default (MPPI_ARM=1 / mppi_set_option("arm", 1)): on
+  // MI355X the gate is one more dependent kernel on the step's path (~6 us dispatch gap after the
+  // finish, ~4 us until it sees go, ~6 us to the rollout: 16.8 us from the finish's end to the next
+  // rollout's start) against 8.7 us for the host's own launch (kernel trace, profiles/r03_notes.md).
+  int arm = 0;
+  uint64_t arm_ticks = 50000;  // 500 us of the 100 MHz clock (mppi_set_option "arm_wait_us")
+  StepDyn* dyn_host = nullptr;  // pinned
+  StepDyn* dyn_dev = nullptr;
+  unsigned* gate_out = nullptr;  // pinned: the gate's decision (id, | kArmCancel [| kArmExpired])
+  const StepDyn* cur_dyn = nullptr;  // fill_rollout / fill_finish: set while the armed step is enqueued
+  bool armed = false;
+  bool arm_ready = false;  // the last sampled step enqueued with every buffer already allocated
+  unsigned arm_id = 0;
+  int arm_proj = 0;
+  uint64_t arm_step = 0;
+  Book arm_post;
+  unsigned wait_seq = 0;  // the completion word wait_done waits for
+  int64_t arm_taken = 0, arm_cancelled = 0, arm_expired = 0;
   uint64_t* clk = nullptr;  // [4] chain clock stamps of the last sampled rollout (RolloutArgs::clk)
   // tiled bilinear binning scratch
   int* bin_tile_of = nullptr;  // per-chunk tile histograms [chunks][tiles]
@@ -340,6 +374,32 @@ int ensure_nodes(mppi_ctx* c, int blocks) {
   return MPPI_OK;
 }
 
+// The rollout / finish fields that follow from the robot state (an armed step's StepDyn block, filled
+// at its call; fill_rollout the same way).
+void dyn_from_state(const mppi_params& p, const mppi_state& st, StepDyn& d) {
+  d.x0 = st.x;
+  d.y0 = st.y;
+  d.h0x = st.heading[0];
+  d.h0y = st.heading[1];
+  d.h0z = st.heading[2];
+  d.wl = st.left_wheel_speed;
+  d.wr = st.right_wheel_speed;
+  d.gx = st.goal_x;
+  d.gy = st.goal_y;
+  d.s1 = st.std_dev_u1;
+  d.s2 = st.std_dev_u2;
+  // _path_follow_critic / _maximise_speed scalar parts (critics_warp.py:111-123, :281-286)
+  const float xd = st.goal_x - st.x;
+  const float yd = st.goal_y - st.y;
+  const float dist = std::sqrt(xd * xd + yd * yd);
+  const float horizon = p.horizon;
+  d.pf_far = dist > horizon ? 1 : 0;
+  d.igx = st.x + (xd * horizon) / (dist + 1e-6f);
+  d.igy = st.y + (yd * horizon) / (dist + 1e-6f);
+  d.pf_scale = 1.0f + (2.0f * horizon) / dist;
+  d.speed_on = (dist < 2.0f) ? 0 : 1;
+}
+
 void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint64_t step,
                   const float* unom, RolloutArgs& a) {
   const mppi_params& p = c->p;
@@ -364,17 +424,24 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   a.cdiv_res = c->rinv_res != 0.0f;
   a.rinv_res_c = c->rinv_res_c;
   a.cdiv_res_c = c->rinv_res_c != 0.0f;
-  a.x0 = st.x;
-  a.y0 = st.y;
-  a.h0x = st.heading[0];
-  a.h0y = st.heading[1];
-  a.h0z = st.heading[2];
-  a.wl = st.left_wheel_speed;
-  a.wr = st.right_wheel_speed;
-  a.gx = st.goal_x;
-  a.gy = st.goal_y;
-  a.s1 = st.std_dev_u1;
-  a.s2 = st.std_dev_u2;
+  StepDyn d;
+  dyn_from_state(p, st, d);
+  a.x0 = d.x0;
+  a.y0 = d.y0;
+  a.h0x = d.h0x;
+  a.h0y = d.h0y;
+  a.h0z = d.h0z;
+  a.wl = d.wl;
+  a.wr = d.wr;
+  a.gx = d.gx;
+  a.gy = d.gy;
+  a.s1 = d.s1;
+  a.s2 = d.s2;
+  a.pf_far = d.pf_far;
+  a.igx = d.igx;
+  a.igy = d.igy;
+  a.pf_scale = d.pf_scale;
+  a.speed_on = d.speed_on;
   a.seed = p.seed;
   a.n_base = step * (uint64_t)((H + 1) / 2);
   a.u_nom1 = unom;
@@ -392,16 +459,6 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   a.wmax = p.v_max_angular;
   a.dt = p.dt;
   a.off = p.wheel_offset;
-  // _path_follow_critic / _maximise_speed scalar parts (critics_warp.py:111-123, :281-286)
-  const float xd = st.goal_x - st.x;
-  const float yd = st.goal_y - st.y;
-  const float dist = std::sqrt(xd * xd + yd * yd);
-  const float horizon = p.horizon;
-  a.pf_far = dist > horizon ? 1 : 0;
-  a.igx = st.x + (xd * horizon) / (dist + 1e-6f);
-  a.igy = st.y + (yd * horizon) / (dist + 1e-6f);
-  a.pf_scale = 1.0f + (2.0f * horizon) / dist;
-  a.speed_on = (dist < 2.0f) ? 0 : 1;
   a.w_path = p.w_path;
   a.w_slope = p.w_slope;
   a.w_speed = p.w_speed;
@@ -413,6 +470,7 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   a.clk = c->clk;
   a.nodes = c->nodes;
   a.rec_m = c->rec_m;
+  a.dyn = c->cur_dyn;
   a.ustore = c->ustore;
   a.inj_u1 = c->inj1;
   a.inj_u2 = c->inj2;
@@ -426,6 +484,7 @@ void fill_finish(const mppi_ctx* c, const Plan& pl, const mppi_state& st, Finish
   f.scratch0 = c->scratch0;
   f.scratch1 = c->scratch1;
   f.uopt = c->uopt;
+  f.dyn = c->cur_dyn;
   f.u_nom_next = c->u_nom[c->cur ^ 1];
   f.out = c->stage;
   f.Z = c->Z;
@@ -490,7 +549,9 @@ int sync_tail(mppi_ctx* c) {
   bool any = c->tail_pending;
   for (int i = 0; i < kTailSlots; ++i) any |= c->tail_inflight[i];
   if (!any) return MPPI_OK;
-  HIP_TRY(hipStreamSynchronize(c->tail_stream));
+  // the slots' own events, not the side stream: an armed next step's tail may be queued there
+  for (int i = 0; i < kTailSlots; ++i)
+    if (c->tail_inflight[i] || (c->tail_pending && i == c->tail_par)) HIP_TRY(hipEventSynchronize(c->ev_tail[i]));
   collect_tail_timing(c);
   for (int i = 0; i < kTailSlots; ++i) c->tail_inflight[i] = false;
   if (c->tail_pending) {
@@ -523,11 +584,11 @@ int wait_done(mppi_ctx* c) {
     HIP_TRY(hipStreamSynchronize(c->stream));
   }
   for (uint64_t i = 0;; ++i) {
-    if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == c->seq) return MPPI_OK;
+    if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == c->wait_seq) return MPPI_OK;
     if ((i & 255) == 255) {
       const hipError_t e = hipStreamQuery(c->stream);
       if (e == hipSuccess) {
-        if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == c->seq) return MPPI_OK;
+        if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == c->wait_seq) return MPPI_OK;
         // a finish that gave up waiting for records (fused launch) left its counters mid-count:
         // re-arm them (the stream is idle) so that the next step starts from zero
         rearm_counters(c);
@@ -722,6 +783,7 @@ int prepare_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, int mode, 
   if (mode >= 1) {
     f.done = c->done;
     f.seq = ++c->seq;
+    c->wait_seq = c->seq;
   }
   par = (c->tail_par + 1) % kTailSlots;
   if (mode == 2) {
@@ -992,28 +1054,146 @@ int enqueue_fused(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, i
   return MPPI_OK;
 }
 
+// The launches of one step (fused, or rollout + finish + tail), with the current state source.
+int enqueue_step(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
+  int fP = 0, fcol = 0, fgroups = 0;
+  size_t flds = 0;
+  c->last_fused = fused_shape(c, pl, mode, &fP, &fcol, &fgroups, &flds);
+  if (c->last_fused) {
+    int rc = enqueue_fused(c, proj, step, pl, fP, fcol, fgroups, flds);
+    if (rc) return rc;
+    if (c->trace) c->tr_t1 = now_us();
+    return MPPI_OK;
+  }
+  int rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr);
+  if (rc) return rc;
+  if (c->trace) c->tr_t1 = now_us();
+  rc = enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 1, nullptr, true);
+  if (rc) return rc;
+  return flush_speculation(c);
+}
+
+void book_save(const mppi_ctx* c, Book& b) {
+  b.seq = c->seq;
+  b.wait_seq = c->wait_seq;
+  b.fin_kind = c->fin_kind;
+  b.fin_P = c->fin_P;
+  b.fin_ncol = c->fin_ncol;
+  b.fin_groups = c->fin_groups;
+  b.last_fused = c->last_fused;
+  b.tail_par = c->tail_par;
+  b.tail_pending = c->tail_pending;
+  for (int i = 0; i < kTailSlots; ++i) b.tail_inflight[i] = c->tail_inflight[i];
+}
+
+void book_restore(mppi_ctx* c, const Book& b) {
+  c->seq = b.seq;
+  c->wait_seq = b.wait_seq;
+  c->fin_kind = b.fin_kind;
+  c->fin_P = b.fin_P;
+  c->fin_ncol = b.fin_ncol;
+  c->fin_groups = b.fin_groups;
+  c->last_fused = b.last_fused;
+  c->tail_par = b.tail_par;
+  c->tail_pending = b.tail_pending;
+  for (int i = 0; i < kTailSlots; ++i) c->tail_inflight[i] = b.tail_inflight[i];
+}
+
+// Cancel the armed step (its gate returns, its kernels return at once); the host bookkeeping is
+// already the one before it was armed.
+void disarm(mppi_ctx* c) {
+  if (!c || !c->armed) return;
+  __atomic_store_n(&c->dyn_host->go, c->arm_id | kArmCancel, __ATOMIC_RELEASE);
+  c->armed = false;
+  ++c->arm_cancelled;
+}
+
+// Any call on the context but mppi_step / mppi_set_state / mppi_get_outputs: cancel an armed step,
+// and the next step runs the ordinary way (it may allocate) before arming resumes.
+void quiesce(mppi_ctx* c) {
+  disarm(c);
+  c->arm_ready = false;
+}
+
+// Enqueue sampled step `step` behind the gate, reading the u_nom buffer the step before it writes,
+// then put the bookkeeping back as it was.  Only once the previous sampled step of the same plan
+// has been enqueued (its buffers are allocated: nothing here synchronizes behind the gate).
+int arm_next(mppi_ctx* c, int proj, uint64_t step, const Plan& pl) {
+  if (!c->arm || !c->arm_ready || c->timing || c->trace || c->noise_at != 0 || c->fused_noise_groups == -2 ||
+      !c->dyn_host || pl.blocks < 1)
+    return MPPI_OK;
+  Book pre;
+  book_save(c, pre);
+  unsigned id = (c->arm_id + 1) & kArmIdMask;
+  if (id == 0) id = 1;
+  HIP_TRY(launch_arm_gate(c->dyn_host, c->dyn_dev, c->gate_out, id, c->arm_ticks, c->stream));
+  c->arm_id = id;
+  c->cur ^= 1;
+  c->cur_dyn = c->dyn_dev;
+  const int rc = enqueue_step(c, proj, step, 0, pl);
+  c->cur_dyn = nullptr;
+  c->cur ^= 1;
+  book_save(c, c->arm_post);
+  book_restore(c, pre);
+  if (rc) {  // what was enqueued behind the gate is cancelled
+    __atomic_store_n(&c->dyn_host->go, id | kArmCancel, __ATOMIC_RELEASE);
+    return rc;
+  }
+  c->armed = true;
+  c->arm_proj = proj;
+  c->arm_step = step;
+  return MPPI_OK;
+}
+
+// Take the armed step: its robot state and go word to the gate, then the gate's decision (it is
+// spinning by now: a few microseconds).  false: the gate had expired (run the step the ordinary
+// way; its launches returned at once).
+bool take_armed(mppi_ctx* c) {
+  StepDyn d;
+  std::memset(&d, 0, sizeof(d));
+  dyn_from_state(c->p, c->st, d);
+  unsigned* hw = reinterpret_cast<unsigned*>(c->dyn_host);
+  const unsigned* sw = reinterpret_cast<const unsigned*>(&d);
+  for (int i = 0; i < kDynWords; ++i) __atomic_store_n(hw + i, sw[i], __ATOMIC_RELAXED);
+  __atomic_store_n(&c->dyn_host->go, c->arm_id, __ATOMIC_RELEASE);  // after the state words
+  c->armed = false;
+  const double t0 = now_us();
+  unsigned v;
+  while (((v = __atomic_load_n(c->gate_out, __ATOMIC_ACQUIRE)) & kArmIdMask) != c->arm_id) {
+    // the gate runs once the previous step's launches have retired; bounded by its own expiry
+    if (now_us() - t0 > 2e6) return false;
+    __builtin_ia32_pause();
+  }
+  if (v & kArmCancel) {
+    ++c->arm_expired;
+    return false;
+  }
+  book_restore(c, c->arm_post);
+  ++c->arm_taken;
+  return true;
+}
+
 int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out) {
   if (c && c->trace) c->tr_t0 = now_us();
   int rc = check_ready(c);
   if (rc) return rc;
   const Plan pl = make_plan(c);
-  int fP = 0, fcol = 0, fgroups = 0;
-  size_t flds = 0;
-  c->last_fused = fused_shape(c, pl, mode, &fP, &fcol, &fgroups, &flds);
-  if (c->last_fused) {
-    rc = enqueue_fused(c, proj, step, pl, fP, fcol, fgroups, flds);
+  if (c->armed) {
+    if (mode == 0 && proj == c->arm_proj && step == c->arm_step && take_armed(c)) {
+      remember(c, proj, step, mode, pl);
+      rc = arm_next(c, proj, step + 1, pl);  // the step after this one, behind it
+      if (rc) return rc;
+      return copy_outputs(c, out);
+    }
+    disarm(c);
+  }
+  rc = enqueue_step(c, proj, step, mode, pl);
+  if (rc) return rc;
+  remember(c, proj, step, mode, pl);
+  if (mode == 0) {
+    rc = arm_next(c, proj, step + 1, pl);
     if (rc) return rc;
-    if (c->trace) c->tr_t1 = now_us();
-    remember(c, proj, step, mode, pl);
-  } else {
-    rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr);
-    if (rc) return rc;
-    if (c->trace) c->tr_t1 = now_us();
-    remember(c, proj, step, mode, pl);
-    rc = enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 1, nullptr, true);
-    if (rc) return rc;
-    rc = flush_speculation(c);
-    if (rc) return rc;
+    c->arm_ready = true;  // this plan's buffers exist now: the next step may be armed
   }
   if (!c->trace) return copy_outputs(c, out);
   const double t2 = now_us();
@@ -1168,6 +1348,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   if (const char* e = std::getenv("MPPI_ROLES")) c->roles = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_NOISE_GPC")) c->noise_gpc = std::max(std::atoi(e), 0);
   if (const char* e = std::getenv("MPPI_FUSED")) c->fused = std::min(std::max(std::atoi(e), 0), 2);
+  if (const char* e = std::getenv("MPPI_ARM")) c->arm = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_FUSED_NOISE_GROUPS")) c->fused_noise_groups = std::max(std::atoi(e), -2);
   const char* ep = std::getenv("MPPI_STREAM_PRIO");
   const bool use_prio = !(ep && std::atoi(ep) == 0);
@@ -1191,6 +1372,9 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipMalloc(&c->cdiv_bad, sizeof(unsigned)) != hipSuccess ||
       hipMalloc(&c->level1_cnt, 128) != hipSuccess ||  // [0]: finish handoff, [16]: fused record count
       hipMalloc(&c->uopt, (size_t)2 * H * sizeof(unsigned long long)) != hipSuccess ||
+      hipHostMalloc(&c->dyn_host, sizeof(StepDyn), hipHostMallocDefault) != hipSuccess ||
+      hipMalloc(&c->dyn_dev, sizeof(StepDyn)) != hipSuccess ||
+      hipHostMalloc(&c->gate_out, 64, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->clk, (kClkBase + 2 * kClkBlocks) * sizeof(uint64_t)) != hipSuccess ||
       hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
@@ -1221,7 +1405,10 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   c->out_host = new float[16 * H]();
   std::memset(c->stage, 0, 16 * H * sizeof(float));
   *c->done = 0;
-  if (hipMemset(c->level1_cnt, 0, 128) != hipSuccess || hipMemset(c->uopt, 0, (size_t)2 * H * sizeof(unsigned long long)) != hipSuccess)
+  std::memset(c->dyn_host, 0, sizeof(StepDyn));
+  std::memset(c->gate_out, 0, 64);
+  if (hipMemset(c->level1_cnt, 0, 128) != hipSuccess || hipMemset(c->uopt, 0, (size_t)2 * H * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(c->dyn_dev, 0, sizeof(StepDyn)) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
   if (c->fused_noise_groups == -2 &&
       (hipMalloc(reinterpret_cast<void**>(&c->sig), 64) != hipSuccess || hipMemset(c->sig, 0, 64) != hipSuccess))
@@ -1234,6 +1421,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
 
 void mppi_destroy(mppi_ctx* c) {
   if (!c) return;
+  disarm(c);
   if (c->trace && c->tr_n > 0)
     std::fprintf(stderr, "mppi host trace (us/step over %ld steps): caller %.1f  enqueue rollout %.1f  "
                  "enqueue rest %.1f  wait+copy %.1f\n", c->tr_n, c->tr_sum[0] / c->tr_n, c->tr_sum[1] / c->tr_n,
@@ -1281,6 +1469,9 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->level1) hipFree(c->level1);
   if (c->level1_cnt) hipFree(c->level1_cnt);
   if (c->uopt) hipFree(c->uopt);
+  if (c->dyn_host) hipHostFree(c->dyn_host);
+  if (c->dyn_dev) hipFree(c->dyn_dev);
+  if (c->gate_out) hipHostFree(c->gate_out);
   if (c->clk) hipFree(c->clk);
   if (c->bin_counts) hipFree(c->bin_counts);
   if (c->bin_cursor) hipFree(c->bin_cursor);
@@ -1296,6 +1487,7 @@ void mppi_destroy(mppi_ctx* c) {
 
 int mppi_set_stream(mppi_ctx* c, void* s) {
   if (!c) return fail(MPPI_EINVAL, "null context");
+  quiesce(c);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   int rc = sync_tail(c);
@@ -1343,6 +1535,7 @@ static int build_normal_table(mppi_ctx* c) {
 int mppi_set_dem(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float x_min, float y_min,
                  float resolution) {
   if (!c || !z) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   int rc = check_grid(rows, cols, resolution);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
@@ -1372,6 +1565,7 @@ int mppi_set_dem(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float 
 int mppi_set_dem_device(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float x_min,
                         float y_min, float resolution) {
   if (!c || !z) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   int rc = check_grid(rows, cols, resolution);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
@@ -1394,6 +1588,7 @@ int mppi_set_dem_device(mppi_ctx* c, const float* z, int32_t rows, int32_t cols,
 
 int mppi_dem_updated(mppi_ctx* c) {
   if (!c) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   if (!c->Z || c->rows <= 0) return fail(MPPI_EINVAL, "no DEM bound");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());  // the in-place write may be on any stream of the device
@@ -1404,6 +1599,7 @@ int mppi_dem_updated(mppi_ctx* c) {
 
 int mppi_set_costmap(mppi_ctx* c, const float* cm, int32_t size, float half_width, float resolution) {
   if (!c || !cm) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   if (size < 1) return fail(MPPI_EINVAL, "costmap size must be >= 1");
   if (!(resolution > 0.0f)) return fail(MPPI_EINVAL, "costmap resolution must be > 0");
   HIP_TRY(hipSetDevice(c->device));
@@ -1432,6 +1628,7 @@ int mppi_set_state(mppi_ctx* c, const mppi_state* s) {
 
 int mppi_set_nominal(mppi_ctx* c, const float* u1, const float* u2) {
   if (!c || !u1 || !u2) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   HIP_TRY(hipSetDevice(c->device));
   const int H = H_of(c);
   HIP_TRY(hipMemcpyAsync(c->u_nom[c->cur], u1, H * sizeof(float), hipMemcpyHostToDevice, c->stream));
@@ -1442,6 +1639,7 @@ int mppi_set_nominal(mppi_ctx* c, const float* u1, const float* u2) {
 
 int mppi_get_nominal(mppi_ctx* c, float* u1, float* u2) {
   if (!c || !u1 || !u2) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   HIP_TRY(hipSetDevice(c->device));
   const int H = H_of(c);
   HIP_TRY(hipMemcpyAsync(u1, c->u_nom[c->cur], H * sizeof(float), hipMemcpyDeviceToHost, c->stream));
@@ -1457,6 +1655,7 @@ int mppi_step(mppi_ctx* c, int32_t proj, uint64_t step, mppi_outputs* out) {
 int mppi_step_injected(mppi_ctx* c, int32_t proj, const float* u1, const float* u2,
                        mppi_outputs* out) {
   if (!c || !u1 || !u2) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   HIP_TRY(hipSetDevice(c->device));
   const size_t n = (size_t)std::max<int64_t>(c->p.num_trajectories, 1) * H_of(c);
   if (!c->inj1) {
@@ -1472,6 +1671,8 @@ int mppi_step_injected(mppi_ctx* c, int32_t proj, const float* u1, const float* 
 int64_t mppi_record_len(mppi_ctx* c) { return c ? E_of(c) : -1; }
 
 int mppi_step_partial(mppi_ctx* c, int32_t proj, uint64_t step, double* record_dev) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  quiesce(c);
   int rc = check_ready(c);
   if (rc) return rc;
   if (!record_dev) return fail(MPPI_EINVAL, "null record buffer");
@@ -1484,6 +1685,8 @@ int mppi_step_partial(mppi_ctx* c, int32_t proj, uint64_t step, double* record_d
 }
 
 int mppi_step_finish(mppi_ctx* c, const double* records_dev, int32_t n, mppi_outputs* out) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  quiesce(c);
   int rc = check_ready(c);
   if (rc) return rc;
   if (!records_dev || n < 1) return fail(MPPI_EINVAL, "records required");
@@ -1497,6 +1700,7 @@ int mppi_step_finish(mppi_ctx* c, const double* records_dev, int32_t n, mppi_out
 
 int mppi_get_costs(mppi_ctx* c, float* costs, int64_t n) {
   if (!c || !costs) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   if (n < 0 || n > c->p.num_trajectories) return fail(MPPI_EINVAL, "n out of range");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipMemcpyAsync(costs, c->cost, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
@@ -1506,6 +1710,8 @@ int mppi_get_costs(mppi_ctx* c, float* costs, int64_t n) {
 
 int mppi_dump_rollouts(mppi_ctx* c, float* traj, float* hv, float* lw, float* rw, float* v, float* w,
                        float* u1, float* u2) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  quiesce(c);
   int rc = check_ready(c);
   if (rc) return rc;
   if (!c->have_last) return fail(MPPI_ESTATE, "no step to dump");
@@ -1546,7 +1752,17 @@ int mppi_dump_rollouts(mppi_ctx* c, float* traj, float* hv, float* lw, float* rw
 
 int mppi_set_option(mppi_ctx* c, const char* name, int64_t value) {
   if (!c || !name) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   const std::string n(name);
+  if (n == "arm") {  // the armed next step on (1) / off (0)
+    c->arm = value != 0;
+    return MPPI_OK;
+  }
+  if (n == "arm_wait_us") {  // how long an armed step's gate waits for the next call
+    if (value < 1 || value > 10000000) return fail(MPPI_EINVAL, "arm_wait_us must be in [1, 1e7]");
+    c->arm_ticks = (uint64_t)value * 100;
+    return MPPI_OK;
+  }
   if (n == "fused_wait_ticks") {
     if (value < 0) return fail(MPPI_EINVAL, "fused_wait_ticks must be >= 0");
     c->fused_wait_ticks = (uint64_t)value;
@@ -1557,6 +1773,7 @@ int mppi_set_option(mppi_ctx* c, const char* name, int64_t value) {
 
 int mppi_set_timing(mppi_ctx* c, int32_t enable) {
   if (!c) return fail(MPPI_EINVAL, "null context");
+  quiesce(c);
   int rc = sync_tail(c);
   if (rc) return rc;
   if (enable < 0 || enable > 2) return fail(MPPI_EINVAL, "timing mode must be 0, 1 or 2");
@@ -1578,6 +1795,7 @@ int mppi_get_tail_timing(mppi_ctx* c, double* tail_ms, int64_t* n) {
 
 int mppi_set_async_tail(mppi_ctx* c, int32_t enable) {
   if (!c) return fail(MPPI_EINVAL, "null context");
+  quiesce(c);
   HIP_TRY(hipSetDevice(c->device));
   int rc = sync_tail(c);
   if (rc) return rc;
@@ -1604,6 +1822,7 @@ int mppi_get_timing(mppi_ctx* c, double* roll, double* fin, int64_t* n) {
 
 int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
   if (!c || !out) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   std::vector<uint64_t> all((size_t)kClkBase + 2 * kClkBlocks, 0);
@@ -1641,14 +1860,16 @@ int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
 int mppi_get_launch_info(mppi_ctx* c, int64_t* info, int32_t n) {
   if (!c || !info) return fail(MPPI_EINVAL, "null argument");
   const Plan& pl = c->last_plan;
-  const int64_t v[12] = {0, pl.block, pl.blocks, pl.W, pl.Wr, (int64_t)pl.lds_bytes, c->fin_kind,
-                         c->fin_P, c->fin_ncol, c->fin_groups, pl.ucache_steps, c->last_fused ? 1 : 0};
-  for (int i = 0; i < n && i < 12; ++i) info[i] = v[i];
+  const int64_t v[15] = {0, pl.block, pl.blocks, pl.W, pl.Wr, (int64_t)pl.lds_bytes, c->fin_kind,
+                         c->fin_P, c->fin_ncol, c->fin_groups, pl.ucache_steps, c->last_fused ? 1 : 0,
+                         c->arm_taken, c->arm_cancelled, c->arm_expired};
+  for (int i = 0; i < n && i < 15; ++i) info[i] = v[i];
   return MPPI_OK;
 }
 
 int mppi_bilinear_query(mppi_ctx* c, const float* x, const float* y, float* h, int64_t n) {
   if (!c || !x || !y || !h) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   if (!c->Z) return fail(MPPI_ESTATE, "no DEM");
   if (n < 0) return fail(MPPI_EINVAL, "n < 0");
   HIP_TRY(hipSetDevice(c->device));
@@ -1668,6 +1889,7 @@ int mppi_bilinear_tiles(mppi_ctx* c, int32_t* ntiles) {
 int mppi_bin_queries(mppi_ctx* c, const float* x, const float* y, int64_t n, float* xs_out, float* ys_out,
                      int32_t* perm, int32_t* tile_off) {
   if (!c || !x || !y || !xs_out || !ys_out || !perm || !tile_off) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   if (!c->Z) return fail(MPPI_ESTATE, "no DEM");
   if (n < 0 || n > INT32_MAX) return fail(MPPI_EINVAL, "n out of range [0, 2^31)");
   HIP_TRY(hipSetDevice(c->device));
@@ -1697,6 +1919,7 @@ int mppi_bin_queries(mppi_ctx* c, const float* x, const float* y, int64_t n, flo
 
 int mppi_bilinear_tiled(mppi_ctx* c, const float* xs, const float* ys, const int32_t* tile_off, float* h) {
   if (!c || !xs || !ys || !tile_off || !h) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   if (!c->Z) return fail(MPPI_ESTATE, "no DEM");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(launch_bilinear_tiled(c->Z, c->rows, c->cols, c->x_min, c->y_min, c->res, c->rinv_res,
@@ -1706,6 +1929,7 @@ int mppi_bilinear_tiled(mppi_ctx* c, const float* xs, const float* ys, const int
 
 int mppi_sync(mppi_ctx* c) {
   if (!c) return fail(MPPI_EINVAL, "null context");
+  quiesce(c);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return MPPI_OK;
@@ -1713,6 +1937,7 @@ int mppi_sync(mppi_ctx* c) {
 
 int mppi_selftest(mppi_ctx* c, int32_t what, int64_t n, uint64_t seed, int64_t* mismatches) {
   if (!c || !mismatches) return fail(MPPI_EINVAL, "null argument");
+  quiesce(c);
   if (what < 0 || what > 3 || n < 0) return fail(MPPI_EINVAL, "bad selftest arguments");
   HIP_TRY(hipSetDevice(c->device));
   unsigned long long* d = nullptr;
@@ -1732,6 +1957,7 @@ int mppi_build_costmap(mppi_ctx* c, const double* obstacles, int32_t n, int32_t 
                        double origin_x, double origin_y, double r_robot, int32_t power, float* out_host,
                        int32_t metric) {
   if (!c) return fail(MPPI_EINVAL, "null context");
+  quiesce(c);
   int rc = costmap_check(obstacles, n, size, power, metric);
   if (rc) return rc;
   const float res = (float)(2 * half_width / size);  // Surface.costmap_resolution (MPPI_isaac.py:272)
@@ -1829,6 +2055,7 @@ int mppi_rollout_python25d(mppi_ctx* c, int64_t n, int32_t H, const double* x0, 
                            const double* heading, const double* lin_vel, const double* ang_vel, double dt,
                            double half_width, double resolution, double bound, double* traj, int32_t* valid) {
   if (!c) return fail(MPPI_EINVAL, "null context");
+  quiesce(c);
   if (n < 0 || H < 1) return fail(MPPI_EINVAL, "python25d: need n >= 0 and H >= 1");
   if (n == 0) return MPPI_OK;
   if (!x0 || !y0 || !heading || !lin_vel || !ang_vel || !traj || !valid)

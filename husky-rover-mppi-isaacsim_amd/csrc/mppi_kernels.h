@@ -7,6 +7,18 @@
 namespace mppi {
 
 // Everything one rollout launch needs, passed by value (uniform per launch).
+// An armed step's robot state (mppi_capi.cpp "armed next step"): the host fills it in pinned memory
+// at the step's call, mppi_arm_gate_kernel copies it to device memory ahead of the step's kernels,
+// which read these fields from it instead of their arguments.  go = the arm id, with kArmCancel
+// set when the step was cancelled (its kernels return at once) or expired (kArmExpired too).
+struct StepDyn {
+  float x0, y0, h0x, h0y, h0z, wl, wr, gx, gy, s1, s2, igx, igy, pf_scale;
+  int pf_far, speed_on;
+  unsigned go;
+  unsigned pad[15];
+};
+constexpr int kDynWords = 16;  // state words before go
+constexpr unsigned kArmCancel = 0x80000000u, kArmExpired = 0x40000000u, kArmIdMask = 0x3FFFFFFFu;
 struct FinishArgs {
   int H;
   int mode;  // 0: write root record, 1: finish (u_opt + optimal rollout),
@@ -14,6 +26,7 @@ struct FinishArgs {
   const double* recs;
   int n_recs;
   const float* rec_m;  // [n_recs] the records' m contiguous, or null (read from recs)
+  const StepDyn* dyn;  // armed step: the state fields from here (null: the arguments)
   unsigned long long* uopt;  // [2H] colfin: the u_opt handoff words {u bits, seq << 32} (zeroed once)
   double* scratch0;
   double* scratch1;
@@ -81,6 +94,7 @@ struct RolloutArgs {
   float* cost_out;   // [K]
   double* nodes;     // [blocks][2H+2]
   float* rec_m;      // [blocks] or null: each record's m again, contiguous (the finish's scale table)
+  const StepDyn* dyn; // armed step: the state fields from here (null: the arguments)
   float* ustore;     // [blocks][2][H][block] sampled controls kept for the weighted sum
   // injected controls (MODE 1), trajectory-major [K*H]
   const float* inj_u1;
@@ -152,6 +166,11 @@ hipError_t launch_step_fused(const RolloutArgs& a, const FusedArgs& z, size_t ld
 // one wave on `st` that returns once *sig >= seq (unsigned compare) or after `ticks` of the 100 MHz
 // clock: whatever `st` holds next runs after the fused launch's rollout part
 hipError_t launch_gate(const unsigned* sig, unsigned seq, uint64_t ticks, hipStream_t st);
+// The armed next step's gate (one wave on the context stream, ahead of the step's kernels): waits
+// for host->go to carry `id` (the host's go or cancel) for at most `ticks` of the 100 MHz clock,
+// copies the state words to dev, stores the decision to dev->go and to *host_out (pinned).
+hipError_t launch_arm_gate(const StepDyn* host, StepDyn* dev, unsigned* host_out, unsigned id, uint64_t ticks,
+                           hipStream_t st);
 // record tree finish (mppi_finish_kernel): the fallback where the column-split shape does not fit
 hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, int groups = 1);
 // column-split finish: every workgroup builds the pair-scale table and reduces ncol columns

@@ -846,6 +846,35 @@ __device__ __forceinline__ double pair_apply_sel(const PairScale& ps, double a, 
   return pair_apply_raw(ps, a, b, j);
 }
 
+// ---- armed step: the state fields from the StepDyn block (uniform scalar loads); false when the
+// step was cancelled or expired (every workgroup of the launch then returns at once)
+__device__ __forceinline__ bool dyn_rollout(RolloutArgs& a) {
+  const StepDyn* d = a.dyn;
+  if (!d) return true;
+  if (d->go & kArmCancel) return false;
+  a.x0 = d->x0;
+  a.y0 = d->y0;
+  a.h0x = d->h0x;
+  a.h0y = d->h0y;
+  a.h0z = d->h0z;
+  a.wl = d->wl;
+  a.wr = d->wr;
+  a.gx = d->gx;
+  a.gy = d->gy;
+  a.s1 = d->s1;
+  a.s2 = d->s2;
+  a.igx = d->igx;
+  a.igy = d->igy;
+  a.pf_scale = d->pf_scale;
+  a.pf_far = d->pf_far;
+  a.speed_on = d->speed_on;
+  return true;
+}
+// The finish reads its few state fields where it uses them (a copy of FinishArgs with them replaced
+// costs the fused launch 6 VGPRs): the armed step's block, else the arguments.
+__device__ __forceinline__ bool fin_cancelled(const FinishArgs& f) { return f.dyn && (f.dyn->go & kArmCancel); }
+#define FIN_STATE(f, fld) ((f).dyn ? (f).dyn->fld : (f).fld)
+
 // Subtree over an aligned group of G records (log2 G levels of the binary tree):
 // scales of its G-1 pairs, level by level (ps[0 .. G/2) first), from the members' m.
 template <int G>
@@ -1265,8 +1294,10 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
 }
 
 template <int TB, int PROJ, int MODE, bool DUMP>
-__global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const RolloutArgs a) {
+__global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const RolloutArgs a_in) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  RolloutArgs a = a_in;
+  if (!dyn_rollout(a)) return;
   constexpr int NT = 2 * TB;
   constexpr int NWC = TB / 64;
   constexpr int D = PAIR_D;
@@ -2044,7 +2075,9 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
 }
 
 template <int TB, int PROJ, int MODE, bool DUMP>
-__global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const RolloutArgs a) {
+__global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const RolloutArgs a_in) {
+  RolloutArgs a = a_in;
+  if (!dyn_rollout(a)) return;
   roles_body<TB, PROJ, MODE, DUMP, false>(a, nullptr);
 }
 
@@ -2076,8 +2109,8 @@ __device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>
   const float res_half_neg = (-f.res) / 2.0f;
   const float res_sq = f.res * f.res;
   Traj s;
-  s.x = f.x0;
-  s.y = f.y0;
+  s.x = FIN_STATE(f, x0);
+  s.y = FIN_STATE(f, y0);
   bool unused = false;
   float q[4];
   if (qpre) {  // the corners, loaded when the finish started (same cell: corners<false> of (x0, y0))
@@ -2092,8 +2125,9 @@ __device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>
   const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
   const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
   const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
-  const float d = (f.h0x * nx + f.h0y * ny) + f.h0z * nz;
-  const float tx = f.h0x - d * nx, ty = f.h0y - d * ny, tz = f.h0z - d * nz;
+  const float h0x = FIN_STATE(f, h0x), h0y = FIN_STATE(f, h0y), h0z = FIN_STATE(f, h0z);
+  const float d = (h0x * nx + h0y * ny) + h0z * nz;
+  const float tx = h0x - d * nx, ty = h0y - d * ny, tz = h0z - d * nz;
   const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
   s.hx = tx / tn;
   s.hy = ty / tn;
@@ -2368,7 +2402,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
       const f4* p = reinterpret_cast<const f4*>(uo + lane * PS);
       f4* q = reinterpret_cast<f4*>(lrp + lane * PS);
       const float a = f.oa;
-      float x = lane ? f.wr : f.wl;
+      float x = lane ? FIN_STATE(f, wr) : FIN_STATE(f, wl);
       f4 A[4], B[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) A[k] = p[k];
@@ -2424,7 +2458,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
 #endif
   } else if (wave == nthreads / 64 - 1 && f.mode == 2) {
     if (lane == 0) {  // step 0 of the optimal rollout needs only the first filter step
-      const float L0 = f.wl * f.oa + uo[0], R0 = f.wr * f.oa + uo[PS];
+      const float L0 = FIN_STATE(f, wl) * f.oa + uo[0], R0 = FIN_STATE(f, wr) * f.oa + uo[PS];
       const float v0 = clampf((L0 + R0) / 2.0f, f.vmin, f.vmax);
       const float w0 = clampf(((-L0) + R0) / f.rwheel, f.wmin, f.wmax);
       float sn0, cs0;
@@ -2472,6 +2506,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
 template <bool LDS>
 __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishArgs f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  if (fin_cancelled(f)) return;
 #if MPPI_FIN_PRIO
   __builtin_amdgcn_s_setprio(3);
 #endif
@@ -2730,7 +2765,7 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
       Dem<false> d0;
       d0.init(f.Z, nullptr, f.rows, f.grid, 0, 0, 1, 1, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
       bool unused = false;
-      d0.template corners<false>(f.x0, f.y0, qpre, unused);
+      d0.template corners<false>(FIN_STATE(f, x0), FIN_STATE(f, y0), qpre, unused);
     }
   }
   PairScale* lps = reinterpret_cast<PairScale*>(smem_raw);
@@ -2968,6 +3003,7 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
 }
 
 __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishArgs f, int P, int ncol) {
+  if (fin_cancelled(f)) return;
   colfin_body<false>(f, P, ncol, (int)blockIdx.x, (int)gridDim.x, nullptr);
 }
 
@@ -2976,6 +3012,7 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
 // next step's rollout kernel.  Bitwise identical to the mode-1 finish.
 __global__ __launch_bounds__(TAIL_THREADS) void mppi_tail_kernel(const FinishArgs f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  if (fin_cancelled(f)) return;
   const int tid = threadIdx.x;
   const int H = f.H;
   float* vb = reinterpret_cast<float*>(smem_raw);
@@ -3451,9 +3488,12 @@ __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t
 // at once, and every rollout workgroup not yet counted either runs or gets a slot as others
 // retire.  No kernel boundary between rollout and finish, no event between rollout and noise.
 template <int TB, int PROJ>
-__global__ __launch_bounds__(NROLES * TB) void mppi_step_fused_kernel(const RolloutArgs a, const FusedArgs z) {
+__global__ __launch_bounds__(NROLES * TB) void mppi_step_fused_kernel(const RolloutArgs a_in, const FusedArgs z_in) {
   const int b = (int)blockIdx.x;
-  if (b < z.nroll) {
+  const FusedArgs& z = z_in;
+  if (b < z.nroll) {  // (a cancelled armed step skips its rollout and finish; the noise below still runs)
+    RolloutArgs a = a_in;
+    if (!dyn_rollout(a)) return;
     __shared__ int sh[2];
     const int ticket = roles_body<TB, PROJ, 0, false, true>(a, z.rec_cnt, sh);
     const int blk = ticket - (z.nroll - z.fin_groups);
@@ -3485,7 +3525,7 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_fused_kernel(const Roll
   }
   const int nb = (int)gridDim.x - z.nroll;
   const int sub = threadIdx.x >> 8;  // NROLES * TB / 256 rows in flight per workgroup
-  noise_rows(a.seed, z.noise_n_base, a.k_offset, a.H, z.nroll, z.noise_eps,
+  noise_rows(a_in.seed, z.noise_n_base, a_in.k_offset, a_in.H, z.nroll, z.noise_eps,
              (int64_t)(b - z.nroll) * (NROLES * TB / 256) + sub, (int64_t)nb * (NROLES * TB / 256),
              threadIdx.x & 255);
 }
@@ -3509,6 +3549,39 @@ __global__ __launch_bounds__(64) void mppi_gate_kernel(const unsigned* sig, unsi
 
 hipError_t launch_gate(const unsigned* sig, unsigned seq, uint64_t ticks, hipStream_t st) {
   hipLaunchKernelGGL(mppi_gate_kernel, dim3(1), dim3(64), 0, st, sig, seq, ticks);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(64) void mppi_arm_gate_kernel(const StepDyn* host, StepDyn* dev, unsigned* host_out,
+                                                            unsigned id, uint64_t ticks) {
+  __shared__ unsigned decision;
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned v = __hip_atomic_load(&host->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    while ((v & kArmIdMask) != id) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 >= ticks) {
+        v = id | kArmCancel | kArmExpired;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(&host->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    decision = v;
+  }
+  __syncthreads();
+  // the host stores the state words, then go (release): read them after go (acquire, system scope)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const unsigned v = decision;
+  const unsigned* hw = reinterpret_cast<const unsigned*>(host);
+  unsigned* dw = reinterpret_cast<unsigned*>(dev);
+  if (threadIdx.x < kDynWords) dw[threadIdx.x] = __hip_atomic_load(hw + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == kDynWords) dw[kDynWords] = v;
+  if (threadIdx.x == 0) __hip_atomic_store(host_out, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_arm_gate(const StepDyn* host, StepDyn* dev, unsigned* host_out, unsigned id, uint64_t ticks,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(mppi_arm_gate_kernel, dim3(1), dim3(64), 0, st, host, dev, host_out, id, ticks);
   return hipGetLastError();
 }
 

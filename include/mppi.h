@@ -272,19 +272,35 @@ int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
  *                       finish workgroup of the fused step launch waits for the rollout
  *                       records (default 2e8 = 2 s).  A finish that gives up publishes
  *                       nothing: the step returns MPPI_EHIP and the counters are re-armed,
- *                       so the next step is correct (0: give up at once, the test hook). */
+ *                       so the next step is correct (0: give up at once, the test hook).
+ *   "arm"               0 (default; env MPPI_ARM=1 turns it on) / 1: the armed next step.
+ *                       After a sampled mppi_step has enqueued its launches, the launches of
+ *                       step + 1 (same projection) are enqueued too, behind a one-wave gate
+ *                       kernel that waits for the next mppi_step call to store the robot state
+ *                       (mppi_set_state's, read at that call) and a go word in pinned memory;
+ *                       that step then starts on the GPU without a host launch on its path.
+ *                       Results are bitwise those of the ordinary path.  A call with another
+ *                       step number or projection, any other call on the context (except
+ *                       mppi_set_state and mppi_get_outputs), or a gate that waited longer than
+ *                       "arm_wait_us" cancels it: its kernels return at once and the call runs
+ *                       the ordinary way.  A device-wide synchronize right after a step waits
+ *                       for the gate to expire (mppi_sync cancels it first).  Off by default:
+ *                       on MI355X the gate's extra dependent launch costs more (16.8 us from
+ *                       the finish's end to the next rollout) than the host's launch (8.7 us).
+ *   "arm_wait_us"       the gate's bound, microseconds (default 500). */
 int mppi_set_option(mppi_ctx* ctx, const char* name, int64_t value);
 int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_t* launches);
 /* HIP-event time of the deferred optimal-rollout kernels (side stream). */
 int mppi_get_tail_timing(mppi_ctx* ctx, double* tail_ms, int64_t* launches);
 
-/* Layout/launch facts for the last step (for tests and the bench), up to 12 values:
+/* Layout/launch facts for the last step (for tests and the bench), up to 15 values:
  * info[0]=0 (reserved), [1]=rollout block threads, [2]=rollout blocks, [3]/[4]=cols/rows of
  * the DEM window the step's lanes can touch, [5]=rollout LDS bytes, [6]=finish kind (1 =
  * column-split mppi_colfin_kernel, 0 = record tree mppi_finish_kernel), [7]=records padded
  * (column-split) or records (tree), [8]=columns per finish workgroup, [9]=finish workgroups,
  * [10]=steps whose sampled controls the rollout keeps in LDS, [11]=1 if the step ran as one
- * fused launch (mppi_step_fused_kernel), else 0. */
+ * fused launch (mppi_step_fused_kernel), else 0; [12]/[13]/[14] = armed steps taken /
+ * cancelled / expired so far (mppi_set_option "arm"). */
 int mppi_get_launch_info(mppi_ctx* ctx, int64_t* info, int32_t n);
 
 /* Shader clock of the last sampled 3D rollout, from the chain wave of trajectories 0..63
