@@ -290,15 +290,16 @@ COSTMAP_BYTES_PER_CELL = 23   # occ 1+1+1, g2 4+4, d2 4+4, out 4 (csrc/mppi_cost
 def costmap_bench(device_index, reps=20, cpu=True):
     """Surface.create_obstacles_costmap (MPPI_isaac.py:361-378) on the GPU: a 1024^2 costmap (the C5
     map, grid 8192 / 8) from 750 rocks, HIP-event device time per build, with the reference's metric
-    (cv2.distanceTransform(DIST_L2, 5): the 5x5 chamfer, two raster passes on one wave) and the exact
-    EDT option; the oracle (numpy restatement, 1 core) on the same input once for reference."""
+    (cv2.distanceTransform(DIST_L2, 5): the 5x5 chamfer as 16 line scans; "chamfer_raster" the same
+    map by the two row-serial raster passes on one workgroup) and the exact EDT option; the oracle
+    (numpy restatement, 1 core) on the same input once for reference."""
     from mppi_amd import _lib
     rng = np.random.RandomState(99)
     rocks = [[rng.uniform(-95, 95), rng.uniform(-95, 95), rng.uniform(0.0, 0.8)] for _ in range(750)]
     size, hw = 1024, 102.4
     b = _lib.CostmapBuilder(device_index)
     rec = {"workload": "1024^2 costmap @0.2 m from 750 rocks (power 20)"}
-    for metric in ("chamfer", "exact"):
+    for metric in ("chamfer", "chamfer_raster", "exact"):
         for _ in range(3):
             b.build(rocks, (0.0, 0.0), size, hw, 1.2, metric=metric)
         dev_ms, t0 = 0.0, time.perf_counter()

@@ -1224,6 +1224,7 @@ void costmap_free(CostmapScratch& sc) {
   if (sc.g2) hipFree(sc.g2);
   if (sc.d2) hipFree(sc.d2);
   if (sc.range) hipFree(sc.range);
+  if (sc.lines) hipFree(sc.lines);
   if (sc.obs) hipFree(sc.obs);
   if (sc.xs) hipFree(sc.xs);
   sc = CostmapScratch{};
@@ -1231,8 +1232,8 @@ void costmap_free(CostmapScratch& sc) {
 
 int costmap_check(const double* obstacles, int32_t n, int32_t size, int32_t power, int32_t metric) {
   if (n < 0 || (n > 0 && !obstacles)) return fail(MPPI_EINVAL, "obstacles: null pointer or negative count");
-  if (metric != MPPI_COSTMAP_CHAMFER5 && metric != MPPI_COSTMAP_EXACT)
-    return fail(MPPI_EINVAL, "costmap metric must be MPPI_COSTMAP_CHAMFER5 or MPPI_COSTMAP_EXACT");
+  if (metric != MPPI_COSTMAP_CHAMFER5 && metric != MPPI_COSTMAP_EXACT && metric != MPPI_COSTMAP_CHAMFER5_RASTER)
+    return fail(MPPI_EINVAL, "costmap metric must be MPPI_COSTMAP_CHAMFER5, MPPI_COSTMAP_EXACT or MPPI_COSTMAP_CHAMFER5_RASTER");
   if (size < 2 || size > COSTMAP_MAX_SIZE) return fail(MPPI_EINVAL, "costmap size must be in [2, 8192]");
   if (power < 0) return fail(MPPI_EINVAL, "costmap power must be >= 0");
   return MPPI_OK;
@@ -1249,19 +1250,21 @@ int costmap_stage(CostmapScratch& sc, const double* obstacles, int32_t n, int32_
   const size_t nseg = (size_t)(size + COSTMAP_SEG - 1) / COSTMAP_SEG;
   if (cells > sc.cells_cap) {
     HIP_TRY(hipStreamSynchronize(st));
-    for (void* p : {(void*)sc.occ, (void*)sc.first, (void*)sc.last, (void*)sc.g2, (void*)sc.d2})
+    for (void* p : {(void*)sc.occ, (void*)sc.first, (void*)sc.last, (void*)sc.g2, (void*)sc.d2, (void*)sc.lines})
       if (p) HIP_TRY(hipFree(p));
     sc.occ = nullptr;
     sc.first = sc.last = sc.g2 = sc.d2 = nullptr;
+    sc.lines = nullptr;
     sc.cells_cap = 0;
     HIP_TRY(hipMalloc(&sc.occ, cells));
     HIP_TRY(hipMalloc(&sc.first, nseg * size * sizeof(int32_t)));
     HIP_TRY(hipMalloc(&sc.last, nseg * size * sizeof(int32_t)));
     HIP_TRY(hipMalloc(&sc.g2, cells * sizeof(int32_t)));
     HIP_TRY(hipMalloc(&sc.d2, cells * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&sc.lines, 16 * cells * sizeof(uint32_t)));
     sc.cells_cap = cells;
   }
-  if (!sc.range) HIP_TRY(hipMalloc(&sc.range, 2 * sizeof(int32_t)));
+  if (!sc.range) HIP_TRY(hipMalloc(&sc.range, (2 + 2 * COSTMAP_MAX_SIZE) * sizeof(int32_t)));
   const size_t nobs = (size_t)std::max<int32_t>(n, 1);
   if (nobs > sc.obs_cap) {
     HIP_TRY(hipStreamSynchronize(st));

@@ -8,14 +8,19 @@
 //   scale    min-max normalise to [0, 1]                                           (:375)
 //   cost     (1 - d)^power                                                         (:376)
 //
-// DEFINED (oracle/costmap_ref.py): the distance is the exact Euclidean one (scipy's EDT), not
-// cv2's 5x5 chamfer approximation (cv2 is not available to pin it), the normalisation and
-// the power run in float64 and the result is rounded once to float32.  Squared distances are
-// integers, computed exactly: a column pass (vertical distance to the nearest obstacle, from
-// per-segment first/last occupied rows) and a row pass (min over x' of (x - x')^2 + g(x')^2,
-// searched outwards from x only while o^2 can still improve the best).  The arithmetic is
-// HBM/latency-light: ~22 B per cell in six short launches; see DESIGN.md §3.4.
+// Two distance metrics (oracle/costmap_ref.py):
+//   chamfer (default, the reference's cv2.distanceTransform(DIST_L2, 5)): OpenCV's published
+//     distanceTransform_5x5 in 16.16 fixed point, computed as 16 independent line scans (below;
+//     the row-serial raster passes remain for a map without obstacle cells), then cv2.normalize
+//     as OpenCV 4.x's float32 path and (1 - d)^power; parity unpinned (no cv2 here).
+//   exact: the exact Euclidean distance from integer squared distances: a column
+//     pass (vertical distance to the nearest obstacle, from per-segment first/last occupied rows)
+//     and a row pass (min over x' of (x - x')^2 + g(x')^2, searched outwards from x only while o^2
+//     can still improve the best), normalise and power in float64, one rounding to float32.
+// Both are integer-exact up to the normalisation; see DESIGN.md §3.6.
+#include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "mppi_costmap.h"
 
@@ -26,15 +31,10 @@ namespace {
 constexpr int CM_THREADS = 256;
 
 // One workgroup per obstacle: mark the cells of its (conservative) bounding box that pass the
-// reference's float64 disc test.  Workgroup 0 also re-arms the min/max cell.
+// reference's float64 disc test.
 __global__ __launch_bounds__(CM_THREADS) void costmap_raster_kernel(const double* __restrict__ obs, int n_obs,
                                                                     const double* __restrict__ xs, int size,
-                                                                    uint8_t* __restrict__ occ,
-                                                                    int32_t* __restrict__ range) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    range[0] = INT_MAX;
-    range[1] = -1;
-  }
+                                                                    uint8_t* __restrict__ occ) {
   if ((int)blockIdx.x >= n_obs) return;
   const double xl = obs[3 * blockIdx.x + 0];
   const double yl = obs[3 * blockIdx.x + 1];
@@ -184,8 +184,9 @@ __global__ __launch_bounds__(CM_THREADS) void costmap_row_kernel(const int32_t* 
       mn = min(mn, red[0][k]);
       mx = max(mx, red[1][k]);
     }
-    atomicMin(&range[0], mn);
-    atomicMax(&range[1], mx);
+    // the row's min / max in its own slot (no contended atomics; costmap_scale_kernel reduces them)
+    range[2 + blockIdx.x] = mn;
+    range[2 + COSTMAP_MAX_SIZE + blockIdx.x] = mx;
   }
 }
 
@@ -210,12 +211,30 @@ __device__ inline double pow_int_dd(double x, int n) {
   return rh;
 }
 
-// d = sqrt(d2); dn = (d - lo) / (hi - lo) (0 when hi == lo); out = float((1 - dn)^power).
+// d = sqrt(d2); dn = (d - lo) / (hi - lo) (0 when hi == lo); out = float((1 - dn)^power); lo / hi
+// from the `rows` per-row partials of costmap_row_kernel.
 __global__ __launch_bounds__(CM_THREADS) void costmap_scale_kernel(const int32_t* __restrict__ d2, int64_t n,
-                                                                   const int32_t* __restrict__ range, int power,
+                                                                   const int32_t* __restrict__ range, int rows, int power,
                                                                    float* __restrict__ out) {
-  const double lo = sqrt((double)range[0]);
-  const double hi = sqrt((double)range[1]);
+  __shared__ int red[2][CM_THREADS / 64];
+  int mn = INT_MAX, mx = -1;
+  for (int k = threadIdx.x; k < rows; k += CM_THREADS) {
+    mn = min(mn, range[2 + k]);
+    mx = max(mx, range[2 + COSTMAP_MAX_SIZE + k]);
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = mn;
+    red[1][threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  for (int k = 0; k < CM_THREADS / 64; ++k) {
+    mn = min(mn, red[0][k]);
+    mx = max(mx, red[1][k]);
+  }
+  const double lo = sqrt((double)mn);
+  const double hi = sqrt((double)mx);
   const double span = hi - lo;
   for (int64_t i = (int64_t)blockIdx.x * CM_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * CM_THREADS) {
     const double d = sqrt((double)d2[i]);
@@ -236,6 +255,8 @@ __global__ __launch_bounds__(CM_THREADS) void costmap_scale_kernel(const int32_t
 // chain across chunks, exact in integers (the sequential sums never exceed 2^32 at size <= 8192).
 constexpr uint32_t CV_HV = 65536u, CV_DIAG = 91750u, CV_LONG = 143976u, CV_INIT = 0x7FFFFFFFu;
 constexpr int CH_B = 2;  // border columns each side
+// min / max partials of the chamfer map (range[2 ..]), reduced by costmap_cv_scale_kernel
+constexpr int CL_PART = COSTMAP_PARTIALS;
 
 // Exclusive min-scans over the 64 lanes of a wave with DPP row shifts / broadcasts (no LDS):
 // up = min over lanes < lane, down = min over lanes > lane (the lane order reversed around an
@@ -290,9 +311,14 @@ constexpr int CH_PF = 4;
 template <int CM>
 __global__ __launch_bounds__(CH_T) void costmap_chamfer_kernel(const uint8_t* __restrict__ occ, int H, int W,
                                                                uint32_t* __restrict__ tmp, float* __restrict__ dist,
-                                                               int32_t* __restrict__ range) {
+                                                               int32_t* __restrict__ range, int only_if_empty) {
   extern __shared__ uint32_t srows[];  // [3][W + 4] rows, then [2][CH_W] wave totals
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // after the line scans: they already produced the map unless it has no obstacle cell (min 0)
+  if (only_if_empty) {
+    const int any0 = __syncthreads_or(tid < CL_PART && range[2 + tid] == 0);  // float bits of 0.0f
+    if (any0) return;
+  }
   const int S = W + 2 * CH_B;
   uint32_t* tot = srows + 3 * S;
   const int C = (W + CH_T - 1) / CH_T;
@@ -436,13 +462,303 @@ __global__ __launch_bounds__(CH_T) void costmap_chamfer_kernel(const uint8_t* __
     red[CH_W + wv] = dmax;
   }
   __syncthreads();
-  if (tid == 0) {
-    for (int k = 1; k < CH_W; ++k) {
-      dmin = fminf(dmin, red[k]);
-      dmax = fmaxf(dmax, red[CH_W + k]);
+  for (int k = 1; k < CH_W; ++k) {
+    dmin = fminf(dmin, red[k]);
+    dmax = fmaxf(dmax, red[CH_W + k]);
+  }
+  // every partial slot the normalisation reduces holds the map's min / max
+  if (tid < CL_PART) {
+    range[2 + tid] = __builtin_bit_cast(int32_t, dmin);
+    range[2 + CL_PART + tid] = __builtin_bit_cast(int32_t, dmax);
+  }
+}
+
+// ------------------------------------------------- the same chamfer as independent line scans
+// The two raster passes are min-plus linear in the initial map (0 on obstacles, INIT elsewhere),
+// so with at least one obstacle cell their result is min over obstacle cells q of the cost of a
+// cheapest path q -> p built from the 16 mask moves (the 2-pixel INIT border never wins: a real
+// distance is < 2^30).  The mask's moves in angular order, axial / diagonal (even) and knight
+// (odd), form a unimodular fan and the weights {65536, 91750, 143976} a convex chamfer norm, so a
+// cheapest path uses only the two moves bounding its sector: n1 knight moves k then n2 moves e of
+// a neighbouring axial/diagonal direction, in any order.  Hence
+//   d = min over the 8 axial/diagonal e of scan_e(min(scan_k(g), scan_k'(g)))
+// with k, k' the knight moves on either side of e and scan_m(h)(p) = min_n h(p - n m) + n w(m)
+// (a running minimum along the lines of direction m).  Every scan is integer min / add, so the
+// result is the raster passes' bit for bit (checked on random, single-cell-at-the-corner and
+// 1024^2 maps against oracle/costmap_ref.py chamfer_l2_5x5 and by the GPU costmap tests), and
+// every line of a scan is independent (below: 64 lines per workgroup, each split into 32-step
+// segments over the waves and stitched by the carry).  Two launches of
+// 8 scans each (knight scans of the occupancy, then the axial/diagonal scans of their pairwise
+// minima) replace 2 x H serial rows on one workgroup.  A map without any obstacle cell (all
+// distances measured from the INIT border) keeps the raster kernel above, which then runs alone.
+constexpr uint32_t CL_INF = 1u << 30;  // "no obstacle yet"; real distances < 1.4 * 8192 * 65536 < 2^30
+constexpr int CL_L = 32;               // steps per wave segment
+constexpr int CL_SEGS = 8;             // segments (waves) per workgroup: 256-step chunks, 2 workgroups per CU
+constexpr int CL_T = 64 * CL_SEGS;
+
+struct ClScan {
+  int8_t ax, ay;      // direction in the virtual frame (ax, ay >= 0; (1,0) (0,1) (1,1) (2,1) (1,2))
+  int8_t fx, fy;      // virtual -> physical mirror of x / y
+  uint32_t w;         // move weight
+  int32_t in_a, in_b; // phase 2: the two knight scans whose minimum is scanned (buffer indices)
+  int32_t nlines;     // lines of this scan
+};
+struct ClJobs {
+  ClScan s[8];
+};
+
+// Lines of direction (ax, ay) in an H x W map: ay == 0 -> the H rows; otherwise lines (u, phi),
+// phi in [0, ay), points (u + ax n, phi + ay n), n in [0, N_phi), N_phi = ceil((H - phi) / ay),
+// u in [-ax (N_phi - 1), W - 1] so that some point lies inside.
+__host__ __device__ inline int cl_nsteps(int H, int ay, int phi) { return (H - phi + ay - 1) / ay; }
+__host__ __device__ inline int cl_lines_phi(int H, int W, int ax, int ay, int phi) {
+  return W + ax * (cl_nsteps(H, ay, phi) - 1);
+}
+inline int cl_lines(int H, int W, int ax, int ay) {
+  if (ay == 0) return H;
+  int n = 0;
+  for (int phi = 0; phi < ay; ++phi) n += cl_lines_phi(H, W, ax, ay, phi);
+  return n;
+}
+
+// PHASE 1: h = occ ? 0 : INF, out = buf[job].  PHASE 2: h = min(buf[in_a], buf[in_b], INF), out =
+// buf[8 + job].  buf holds 16 planes of H x W words.
+//
+// One workgroup scans 64 consecutive lines (a wave's lanes, so every step of a wave reads one
+// contiguous run of a row) in chunks of CL_SEGS * CL_L steps; wave s takes steps [s CL_L, (s+1) CL_L)
+// of the chunk: all its loads issued at once, the running minimum over its segment with no input
+// (carry INF), the segment's last value to LDS, then the value entering the segment,
+//   C_0 = the chunk's carry, C_{s+1} = min(T_s, C_s + CL_L w)
+// (T_s the last local value of segment s), and v = min(local, C_seg + (k+1) w), which is the
+// serial recurrence's value exactly (integer min / add are associative).  Cells outside the map
+// read INF and are not stored; every value stays <= INF, so no sum overflows.
+__device__ inline __amdgpu_buffer_rsrc_t cl_rsrc(const void* p, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+// Horizontal scans (virtual (1, 0)): one wave per row, lane l holding 16 consecutive columns of a
+// 1024-column chunk (the row is contiguous, so lanes read it in order); the in-lane chain runs
+// serially and the chain across lanes as an exclusive min-scan of keys (value at the lane's last
+// column + (W - that column) w: a later column p then reads key - (W - p) w; keys < 2^32 as
+// INF + (W + 1) w < 1.9e9).  Backward (fx) mirrors it: right to left, keys v + column w.
+template <bool BACK>
+__device__ inline void cl_row_scan(__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t ro,
+                                   int y, int W, uint32_t w, int lane) {
+  constexpr int C = 16;
+  uint32_t carry = CL_INF;  // value at the column just before (after, BACK) the chunk
+  const int nch = (W + 64 * C - 1) / (64 * C);
+  for (int q = 0; q < nch; ++q) {
+    const int cb = (BACK ? nch - 1 - q : q) * 64 * C;
+    const int j0 = cb + lane * C;
+    uint32_t v[C];
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+      const int j = j0 + k;
+      const int off = (y * W + j) * 4;
+      v[k] = j < W ? min(min(__builtin_amdgcn_raw_buffer_load_b32(ra, off, 0, 0),
+                             __builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, 0)), CL_INF)
+                   : CL_INF;
     }
-    range[0] = __builtin_bit_cast(int32_t, dmin);
-    range[1] = __builtin_bit_cast(int32_t, dmax);
+    uint32_t run = CL_INF;
+    if (!BACK) {
+#pragma unroll
+      for (int k = 0; k < C; ++k) {
+        run = min(v[k], run + w);
+        v[k] = run;
+      }
+      const uint32_t key = run + (uint32_t)(W - (j0 + C - 1)) * w;  // j0 + C - 1 may pass W - 1: key still > every real
+      const uint32_t kin = carry + (uint32_t)(W - (cb - 1)) * w;
+      const uint32_t kc = min(wave_excl_min_scan_up(key), kin);
+#pragma unroll
+      for (int k = 0; k < C; ++k) {
+        const int j = j0 + k;
+        v[k] = min(v[k], kc - (uint32_t)(W - j) * w);
+        if (j < W) __builtin_amdgcn_raw_buffer_store_b32(v[k], ro, (y * W + j) * 4, 0, 0);
+      }
+      carry = (uint32_t)__builtin_amdgcn_readlane((int)v[C - 1], 63);
+    } else {
+#pragma unroll
+      for (int k = C - 1; k >= 0; --k) {
+        run = min(v[k], run + w);
+        v[k] = run;
+      }
+      const uint32_t key = run + (uint32_t)j0 * w;
+      const uint32_t kin = carry + (uint32_t)(cb + 64 * C) * w;
+      const uint32_t kc = min(wave_excl_min_scan_down(key, lane), kin);
+#pragma unroll
+      for (int k = 0; k < C; ++k) {
+        const int j = j0 + k;
+        v[k] = min(v[k], kc - (uint32_t)j * w);
+        if (j < W) __builtin_amdgcn_raw_buffer_store_b32(v[k], ro, (y * W + j) * 4, 0, 0);
+      }
+      carry = (uint32_t)__builtin_amdgcn_readlane((int)v[0], 0);
+    }
+  }
+}
+
+template <int PHASE>
+__global__ __launch_bounds__(CL_T, 4) void costmap_line_scan_kernel(const uint8_t* __restrict__ occ, int H, int W,
+                                                                 uint32_t* __restrict__ buf, ClJobs jobs) {
+  __shared__ uint32_t tails[CL_SEGS][64];
+  const ClScan sc = jobs.s[blockIdx.y];
+  const int lane = threadIdx.x & 63, seg = threadIdx.x >> 6;
+  const size_t plane = (size_t)H * W;
+  const auto ro = cl_rsrc(buf + (size_t)(PHASE == 1 ? blockIdx.y : 8 + blockIdx.y) * plane, plane * 4);
+  const auto ra = cl_rsrc(buf + (size_t)sc.in_a * plane, plane * 4);
+  const auto rb = cl_rsrc(buf + (size_t)sc.in_b * plane, plane * 4);
+  const auto rocc = cl_rsrc(occ, plane);
+  const int ax = sc.ax, ay = sc.ay;
+  if (ay == 0) {  // rows (PHASE 2 only): one wave per row
+    const int y = blockIdx.x * CL_SEGS + seg;
+    if (y >= H) return;
+    if (sc.fx)
+      cl_row_scan<true>(ra, rb, ro, y, W, sc.w, lane);
+    else
+      cl_row_scan<false>(ra, rb, ro, y, W, sc.w, lane);
+    return;
+  }
+  const int line0 = blockIdx.x * 64;
+  if (line0 >= sc.nlines) return;  // uniform over the workgroup
+  const int t = line0 + lane;
+  // this lane's line: start (x0, y0) in the virtual frame, step (ax, ay), valid n in [nlo, nhi]
+  int x0, y0, nlo, nhi;
+  auto line_of = [&](int tt, int& lx0, int& ly0, int& lo, int& hi) {
+    int phi = 0, u = tt;
+    const int l0 = cl_lines_phi(H, W, ax, ay, 0);
+    if (ay == 2 && u >= l0) {
+      phi = 1;
+      u -= l0;
+    }
+    const int N = cl_nsteps(H, ay, phi);
+    u -= ax * (N - 1);  // u in [-ax (N - 1), W - 1]
+    lx0 = u;
+    ly0 = phi;
+    lo = 0;
+    hi = N - 1;
+    if (ax > 0) {
+      if (u < 0) lo = (-u + ax - 1) / ax;  // first n with u + ax n >= 0
+      hi = min(N - 1, (W - 1 - u) / ax);   // last n with u + ax n <= W - 1 (W - 1 - u >= 0)
+    }
+  };
+  const bool live = t < sc.nlines;
+  line_of(live ? t : line0, x0, y0, nlo, nhi);
+  if (!live) {
+    nlo = 0;
+    nhi = -1;
+  }
+  // step range of the 64 lines (the same in every wave of the workgroup)
+  int wlo = live ? nlo : INT_MAX, whi = live ? nhi : -1;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    wlo = min(wlo, __shfl_xor(wlo, o, 64));
+    whi = max(whi, __shfl_xor(whi, o, 64));
+  }
+  // physical cell of step n: x' = x0 + ax n, y' = y0 + ay n, mirrored; 32-bit cell index (< 2^26)
+  const int sx = sc.fx ? -ax : ax, sy = sc.fy ? -ay : ay;
+  const int px0 = sc.fx ? W - 1 - x0 : x0, py0 = sc.fy ? H - 1 - y0 : y0;
+  const int ibase = py0 * W + px0;
+  const int istep = sy * W + sx;
+  const uint32_t w = sc.w, wl = (uint32_t)CL_L * sc.w;
+  uint32_t carry = CL_INF;  // the value at the step before the chunk
+  for (int c0 = wlo; c0 <= whi; c0 += CL_SEGS * CL_L) {
+    const int n0 = c0 + seg * CL_L;
+    uint32_t v[CL_L];
+#pragma unroll
+    for (int k = 0; k < CL_L; ++k) {
+      const int nn = n0 + k;
+      const bool in = nn >= nlo && nn <= nhi;
+      const int idx = ibase + istep * nn;
+      if (PHASE == 1) {
+        v[k] = in ? (__builtin_amdgcn_raw_buffer_load_b8(rocc, idx, 0, 0) ? 0u : CL_INF) : CL_INF;
+      } else {
+        v[k] = in ? min(min(__builtin_amdgcn_raw_buffer_load_b32(ra, idx * 4, 0, 0),
+                            __builtin_amdgcn_raw_buffer_load_b32(rb, idx * 4, 0, 0)), CL_INF)
+                  : CL_INF;
+      }
+    }
+    uint32_t run = CL_INF;
+#pragma unroll
+    for (int k = 0; k < CL_L; ++k) {
+      run = min(v[k], run + w);
+      v[k] = run;
+    }
+    tails[seg][lane] = run;
+    __syncthreads();
+    uint32_t cin = carry, cout = carry;
+#pragma unroll
+    for (int s = 0; s < CL_SEGS; ++s) {
+      if (s == seg) cin = cout;
+      cout = min(tails[s][lane], cout + wl);
+    }
+    __syncthreads();  // tails read before the next chunk writes them
+#pragma unroll
+    for (int k = 0; k < CL_L; ++k) {
+      const int nn = n0 + k;
+      if (nn >= nlo && nn <= nhi)
+        __builtin_amdgcn_raw_buffer_store_b32(min(v[k], cin + (uint32_t)(k + 1) * w), ro, (ibase + istep * nn) * 4, 0, 0);
+    }
+    carry = cout;
+  }
+}
+
+// dist = float(min over the 8 axial/diagonal scans) / 65536; workgroup b (of exactly CL_PART)
+// stores its min / max (float bits) in range[2 + b] / range[2 + CL_PART + b].
+__global__ __launch_bounds__(CM_THREADS) void costmap_line_min_kernel(const uint32_t* __restrict__ buf, int64_t n,
+                                                                      float* __restrict__ dist,
+                                                                      int32_t* __restrict__ range) {
+  __shared__ float red[2][CM_THREADS / 64];
+  const uint32_t* r = buf + 8 * n;
+  float dmin = INFINITY, dmax = -INFINITY;
+  auto one = [&](uint32_t v, int64_t i) __attribute__((always_inline)) {
+    const float d = (float)v * (1.0f / 65536.0f);
+    dist[i] = d;
+    dmin = fminf(dmin, d);
+    dmax = fmaxf(dmax, d);
+  };
+  const int64_t gsz = (int64_t)gridDim.x * CM_THREADS, tid = (int64_t)blockIdx.x * CM_THREADS + threadIdx.x;
+  if ((n & 3) == 0) {  // planes 16-byte aligned: four cells per load
+    const int64_t n4 = n >> 2;
+    for (int64_t i = tid; i < n4; i += gsz) {
+      uint4 v = reinterpret_cast<const uint4*>(r)[i];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) {
+        const uint4 u = reinterpret_cast<const uint4*>(r + k * n)[i];
+        v.x = min(v.x, u.x);
+        v.y = min(v.y, u.y);
+        v.z = min(v.z, u.z);
+        v.w = min(v.w, u.w);
+      }
+      one(v.x, 4 * i);
+      one(v.y, 4 * i + 1);
+      one(v.z, 4 * i + 2);
+      one(v.w, 4 * i + 3);
+    }
+  } else {
+    for (int64_t i = tid; i < n; i += gsz) {
+      uint32_t v = r[i];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) v = min(v, r[k * n + i]);
+      one(v, i);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    dmin = fminf(dmin, __shfl_xor(dmin, o, 64));
+    dmax = fmaxf(dmax, __shfl_xor(dmax, o, 64));
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][wv] = dmin;
+    red[1][wv] = dmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < CM_THREADS / 64; ++k) {
+      dmin = fminf(dmin, red[0][k]);
+      dmax = fmaxf(dmax, red[1][k]);
+    }
+    range[2 + blockIdx.x] = __builtin_bit_cast(int32_t, dmin);  // no contended atomics: one slot per workgroup
+    range[2 + CL_PART + blockIdx.x] = __builtin_bit_cast(int32_t, dmax);
   }
 }
 
@@ -453,8 +769,28 @@ __global__ __launch_bounds__(CH_T) void costmap_chamfer_kernel(const uint8_t* __
 __global__ __launch_bounds__(CM_THREADS) void costmap_cv_scale_kernel(const float* __restrict__ dist, int64_t n,
                                                                       const int32_t* __restrict__ range, int power,
                                                                       float* __restrict__ out) {
-  const double smin = (double)__builtin_bit_cast(float, range[0]);
-  const double smax = (double)__builtin_bit_cast(float, range[1]);
+  __shared__ float red[2][CM_THREADS / 64];
+  float pmin = INFINITY, pmax = -INFINITY;  // the CL_PART partials (chamfer line / raster kernels)
+  for (int k = threadIdx.x; k < CL_PART; k += CM_THREADS) {
+    pmin = fminf(pmin, __builtin_bit_cast(float, range[2 + k]));
+    pmax = fmaxf(pmax, __builtin_bit_cast(float, range[2 + CL_PART + k]));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    pmin = fminf(pmin, __shfl_xor(pmin, o, 64));
+    pmax = fmaxf(pmax, __shfl_xor(pmax, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = pmin;
+    red[1][threadIdx.x >> 6] = pmax;
+  }
+  __syncthreads();
+  for (int k = 0; k < CM_THREADS / 64; ++k) {
+    pmin = fminf(pmin, red[0][k]);
+    pmax = fmaxf(pmax, red[1][k]);
+  }
+  const double smin = (double)pmin;
+  const double smax = (double)pmax;
   const double scale = 1.0 * ((smax - smin > 2.220446049250313e-16) ? 1.0 / (smax - smin) : 0.0);
   const float a = (float)scale;
   const float b = 0.0f - (float)(smin * (double)a);
@@ -473,20 +809,77 @@ hipError_t launch_costmap_build(const CostmapScratch& sc, int n_obs, int size, i
   hipError_t e = hipMemsetAsync(sc.occ, 0, cells, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(costmap_raster_kernel, dim3(n_obs > 0 ? n_obs : 1), dim3(CM_THREADS), 0, st, sc.obs, n_obs,
-                     sc.xs, size, sc.occ, sc.range);
-  if (metric == COSTMAP_CHAMFER5) {
+                     sc.xs, size, sc.occ);
+  if (metric == COSTMAP_CHAMFER5 || metric == COSTMAP_CHAMFER5_RASTER) {
     float* dist = reinterpret_cast<float*>(sc.d2);
+    const int lines = metric == COSTMAP_CHAMFER5;
+    if (lines) {
+      // phase 1: the 8 knight scans of the occupancy -> planes 0..7
+      const int H = size, W = size;
+      ClJobs j1{}, j2{};
+      const int kn[8][2] = {{2, 1}, {-2, 1}, {2, -1}, {-2, -1}, {1, 2}, {-1, 2}, {1, -2}, {-1, -2}};
+      auto knight = [&](int mx, int my) {
+        for (int k = 0; k < 8; ++k)
+          if (kn[k][0] == mx && kn[k][1] == my) return k;
+        return -1;
+      };
+      auto fill = [&](ClScan& s, int mx, int my, uint32_t w) {
+        s.ax = (int8_t)std::abs(mx);
+        s.ay = (int8_t)std::abs(my);
+        s.fx = (int8_t)(mx < 0);
+        s.fy = (int8_t)(my < 0);
+        s.w = w;
+        s.nlines = cl_lines(H, W, s.ax, s.ay);
+      };
+      int most = 0;
+      for (int k = 0; k < 8; ++k) {
+        fill(j1.s[k], kn[k][0], kn[k][1], CV_LONG);
+        most = std::max(most, j1.s[k].nlines);
+      }
+      hipLaunchKernelGGL(costmap_line_scan_kernel<1>, dim3((most + 63) / 64, 8), dim3(CL_T), 0, st, sc.occ,
+                         H, W, sc.lines, j1);
+      // phase 2: each axial / diagonal direction e scans min of the knight scans on either side
+      const int ad[8][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}, {-1, 0}, {-1, -1}, {0, -1}, {1, -1}};
+      most = 0;
+      for (int k = 0; k < 8; ++k) {
+        const int mx = ad[k][0], my = ad[k][1];
+        fill(j2.s[k], mx, my, (mx != 0 && my != 0) ? CV_DIAG : CV_HV);
+        // the two knight moves angularly adjacent to e (the sectors on either side of e)
+        int a, b;
+        if (my == 0) {
+          a = knight(2 * mx, 1);
+          b = knight(2 * mx, -1);
+        } else if (mx == 0) {
+          a = knight(1, 2 * my);
+          b = knight(-1, 2 * my);
+        } else {
+          a = knight(2 * mx, my);
+          b = knight(mx, 2 * my);
+        }
+        j2.s[k].in_a = a;
+        j2.s[k].in_b = b;
+        most = std::max(most, my == 0 ? (H + CL_SEGS - 1) / CL_SEGS * 64 : j2.s[k].nlines);
+      }
+      hipLaunchKernelGGL(costmap_line_scan_kernel<2>, dim3((most + 63) / 64, 8), dim3(CL_T), 0, st, sc.occ,
+                         H, W, sc.lines, j2);
+      hipLaunchKernelGGL(costmap_line_min_kernel, dim3(CL_PART), dim3(CM_THREADS), 0, st, sc.lines, (int64_t)cells,
+                         dist, sc.range);
+    }
     const size_t lds = ((size_t)3 * (size + 2 * CH_B) + 2 * CH_W) * sizeof(uint32_t);
     uint32_t* t32 = reinterpret_cast<uint32_t*>(sc.g2);
     const int per = (size + CH_T - 1) / CH_T;  // columns per thread
     if (per <= 1)
-      hipLaunchKernelGGL(costmap_chamfer_kernel<1>, dim3(1), dim3(CH_T), lds, st, sc.occ, size, size, t32, dist, sc.range);
+      hipLaunchKernelGGL(costmap_chamfer_kernel<1>, dim3(1), dim3(CH_T), lds, st, sc.occ, size, size, t32, dist, sc.range,
+                         lines);
     else if (per <= 2)
-      hipLaunchKernelGGL(costmap_chamfer_kernel<2>, dim3(1), dim3(CH_T), lds, st, sc.occ, size, size, t32, dist, sc.range);
+      hipLaunchKernelGGL(costmap_chamfer_kernel<2>, dim3(1), dim3(CH_T), lds, st, sc.occ, size, size, t32, dist, sc.range,
+                         lines);
     else if (per <= 4)
-      hipLaunchKernelGGL(costmap_chamfer_kernel<4>, dim3(1), dim3(CH_T), lds, st, sc.occ, size, size, t32, dist, sc.range);
+      hipLaunchKernelGGL(costmap_chamfer_kernel<4>, dim3(1), dim3(CH_T), lds, st, sc.occ, size, size, t32, dist, sc.range,
+                         lines);
     else
-      hipLaunchKernelGGL(costmap_chamfer_kernel<8>, dim3(1), dim3(CH_T), lds, st, sc.occ, size, size, t32, dist, sc.range);
+      hipLaunchKernelGGL(costmap_chamfer_kernel<8>, dim3(1), dim3(CH_T), lds, st, sc.occ, size, size, t32, dist, sc.range,
+                         lines);
     const unsigned blocks = (unsigned)std::min<size_t>((cells + CM_THREADS - 1) / CM_THREADS, 256 * 8);
     hipLaunchKernelGGL(costmap_cv_scale_kernel, dim3(blocks), dim3(CM_THREADS), 0, st, dist, (int64_t)cells,
                        sc.range, power, out);
@@ -501,7 +894,7 @@ hipError_t launch_costmap_build(const CostmapScratch& sc, int n_obs, int size, i
                      size, sc.d2, sc.range);
   const unsigned blocks = (unsigned)std::min<size_t>((cells + CM_THREADS - 1) / CM_THREADS, 256 * 8);
   hipLaunchKernelGGL(costmap_scale_kernel, dim3(blocks), dim3(CM_THREADS), 0, st, sc.d2, (int64_t)cells, sc.range,
-                     power, out);
+                     size, power, out);
   return hipGetLastError();
 }
 

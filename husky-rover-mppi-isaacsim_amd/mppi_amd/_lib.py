@@ -161,7 +161,7 @@ def _obstacles(obstacles):
     return a, a.ctypes.data_as(_DP)
 
 
-COSTMAP_METRICS = {"chamfer": 0, "exact": 1}   # mppi_costmap_metric (include/mppi.h)
+COSTMAP_METRICS = {"chamfer": 0, "exact": 1, "chamfer_raster": 2}   # mppi_costmap_metric (include/mppi.h)
 
 
 def _metric(m):

@@ -142,9 +142,12 @@ int mppi_set_costmap(mppi_ctx* ctx, const float* costmap_host, int32_t size, flo
  * reference); then the distance to the nearest marked cell, min-max normalised,
  * (1 - d)^power (the reference: 20), float32.  metric MPPI_COSTMAP_CHAMFER5 (the
  * reference's cv2.distanceTransform(DIST_L2, 5), :374): OpenCV's published
- * 5x5 chamfer (distanceTransform_5x5, 16.16 fixed point), cv2.normalize
- * NORM_MINMAX in float64, (1 - d) in float32, the power correctly rounded
- * (oracle/costmap_ref.py; parity unpinned: cv2 is unavailable).
+ * 5x5 chamfer (distanceTransform_5x5, 16.16 fixed point; computed as 16
+ * independent line scans), cv2.normalize NORM_MINMAX as
+ * OpenCV 4.x's float32 path (float scale / shift, one fma), (1 - d) in
+ * float32, the power correctly rounded (oracle/costmap_ref.py; parity
+ * unpinned: cv2 is unavailable).  MPPI_COSTMAP_CHAMFER5_RASTER: the same map
+ * by the two row-serial raster passes on one workgroup (diagnostic / A-B).
  * MPPI_COSTMAP_EXACT: exact Euclidean distance, float64 normalise + power, one
  * rounding; no obstacle at all gives an all-1 map.
  * 2 <= size <= 8192.
@@ -157,6 +160,7 @@ int mppi_set_costmap(mppi_ctx* ctx, const float* costmap_host, int32_t size, flo
 enum mppi_costmap_metric {
   MPPI_COSTMAP_CHAMFER5 = 0, /* cv2.distanceTransform(DIST_L2, 5), MPPI_isaac.py:374 (default) */
   MPPI_COSTMAP_EXACT = 1,    /* exact Euclidean distance transform */
+  MPPI_COSTMAP_CHAMFER5_RASTER = 2, /* CHAMFER5 by the raster passes (same result, slower) */
 };
 typedef struct mppi_costmap_builder mppi_costmap_builder;
 int mppi_build_costmap(mppi_ctx* ctx, const double* obstacles, int32_t n, int32_t size,

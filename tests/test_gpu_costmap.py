@@ -41,10 +41,15 @@ CASES = {
     "none": ([], (0.0, 0.0), 96, 9.6, 1.2, 20),
     "all": ([[0.0, 0.0, 500.0]], (0.0, 0.0), 64, 6.4, 1.2, 20),
     "power0": (_rocks(10, 5.0, 5), (0.0, 0.0), 40, 6.0, 1.2, 0),
+    # one small disc in a corner of a 1024^2 map: the longest lines of every scan direction
+    "corner_1024": ([[-101.0, -101.0, 0.1]], (0.0, 0.0), 1024, 102.4, 0.05, 20),
+    "rect_edge": ([[12.7, -3.0, 0.2], [-12.0, 12.6, 0.3]], (0.0, 0.0), 255, 12.8, 0.1, 20),
 }
 
 
-ORACLE = {"chamfer": CR.create_obstacles_costmap_cv, "exact": CR.create_obstacles_costmap}
+# "chamfer" runs the 16 line scans, "chamfer_raster" the row-serial raster passes (same map)
+ORACLE = {"chamfer": CR.create_obstacles_costmap_cv, "chamfer_raster": CR.create_obstacles_costmap_cv,
+          "exact": CR.create_obstacles_costmap}
 
 
 @pytest.mark.parametrize("metric", list(ORACLE))
