@@ -170,6 +170,59 @@ def chamfer_l2_5x5_loops(occ):
     return out
 
 
+# The same distances as 16 independent line scans (the HIP builder's formulation,
+# husky-rover-mppi-isaacsim_amd/csrc/mppi_costmap.hip costmap_line_scan_kernel): with at least one
+# obstacle cell the raster passes give min over obstacle cells of the cheapest path made of mask
+# moves, and a cheapest path uses only the two moves bounding its sector (a knight move and an
+# axial/diagonal one), so d = min_e scan_e(min(scan_k(g), scan_k'(g))).  Checked against
+# chamfer_l2_5x5 by tests/test_costmap_oracle.py; an obstacle-free map is not covered (None).
+CL_INF = 1 << 30
+_CL_DIRS = [(1, 0), (2, 1), (1, 1), (1, 2), (0, 1), (-1, 2), (-1, 1), (-2, 1),
+            (-1, 0), (-2, -1), (-1, -1), (-1, -2), (0, -1), (1, -2), (1, -1), (2, -1)]
+
+
+def _cl_weight(m):
+    a, b = abs(m[0]), abs(m[1])
+    return CV_HV if a + b == 1 else CV_DIAG if a == b else CV_LONG
+
+
+def _cl_scan(h, m):
+    """out(p) = min_n h(p - n m) + n w(m), all lines of direction m at once (rows of cells)."""
+    H, W = h.shape
+    mx, my = m
+    w = _cl_weight(m)
+    out = h.copy()
+    if my == 0:
+        cols = range(W) if mx > 0 else range(W - 1, -1, -1)
+        for x in cols:
+            if 0 <= x - mx < W:
+                out[:, x] = np.minimum(out[:, x], np.minimum(out[:, x - mx] + w, CL_INF))
+        return out
+    for y in (range(H) if my > 0 else range(H - 1, -1, -1)):
+        if not 0 <= y - my < H:
+            continue
+        src = np.full(W, CL_INF, np.int64)
+        if mx >= 0:
+            src[mx:] = out[y - my, :W - mx]
+        else:
+            src[:W + mx] = out[y - my, -mx:]
+        out[y] = np.minimum(out[y], np.minimum(src + w, CL_INF))
+    return out
+
+
+def chamfer_l2_5x5_lines(occ):
+    """chamfer_l2_5x5 by knight scans then axial/diagonal scans of their pairwise minima."""
+    if not occ.any():
+        return None
+    g = np.where(occ, 0, CL_INF).astype(np.int64)
+    knight = {_CL_DIRS[i]: _cl_scan(g, _CL_DIRS[i]) for i in range(1, 16, 2)}
+    t = np.full(g.shape, CL_INF, np.int64)
+    for i in range(0, 16, 2):
+        h = np.minimum(knight[_CL_DIRS[i - 1]], knight[_CL_DIRS[(i + 1) % 16]])
+        t = np.minimum(t, _cl_scan(h, _CL_DIRS[i]))
+    return (t.astype(np.uint32).astype(np.float32) * np.float32(1.0 / 65536)).astype(np.float32)
+
+
 DBL_EPSILON = float(np.finfo(np.float64).eps)
 
 

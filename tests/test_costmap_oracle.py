@@ -106,3 +106,21 @@ def test_cv_normalize_float32_path():
     np.testing.assert_array_equal(out, exp)
     assert out.dtype == np.float32 and out.min() == 0.0
     np.testing.assert_array_equal(CR.cv_normalize_minmax(np.full((3, 3), 2.0, np.float32)), np.zeros((3, 3), np.float32))
+
+
+@pytest.mark.parametrize("shape,p,seed", [((1, 1), 1.0, 0), ((2, 9), 0.2, 1), ((37, 23), 0.01, 2),
+                                          ((64, 64), 0.002, 3), ((97, 130), 0.05, 4), ((130, 97), 0.3, 5)])
+def test_chamfer_line_scans_match_raster_passes(shape, p, seed):
+    """The HIP builder's formulation (16 line scans) gives the raster passes' map bit for bit."""
+    occ = np.random.default_rng(seed).random(shape) < p
+    occ.flat[seed % occ.size] = True
+    assert np.array_equal(CR.chamfer_l2_5x5_lines(occ).view(np.uint32), CR.chamfer_l2_5x5(occ).view(np.uint32))
+
+
+@pytest.mark.parametrize("cell", [(0, 0), (0, 79), (59, 0), (59, 79), (30, 41)])
+def test_chamfer_line_scans_single_cell(cell):
+    """One obstacle cell: the longest paths of every sector, from every corner."""
+    occ = np.zeros((60, 80), bool)
+    occ[cell] = True
+    assert np.array_equal(CR.chamfer_l2_5x5_lines(occ).view(np.uint32), CR.chamfer_l2_5x5(occ).view(np.uint32))
+    assert CR.chamfer_l2_5x5_lines(np.zeros((5, 5), bool)) is None
