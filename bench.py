@@ -470,8 +470,15 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # rank r on GPU r; MPPI_BENCH_BACKEND=gloo (host-memory exchange) lets a one-GPU box rehearse
+        # several ranks on its one device (RCCL refuses two ranks on one GPU)
+        backend = os.environ.get("MPPI_BENCH_BACKEND", "nccl")
+        local_rank %= max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
 
     run = Runner(args.config, local_rank, world, devices=devices)
     group_info = run.group.info() if run.group is not None else None
@@ -550,9 +557,11 @@ def main():
             c4["speedup_vs_1"] = round((c4_steps / t4) / solo_rate("c4", c4_steps), 3)
 
     if world > 1:
-        launcher = "torch.distributed.run: one process per GPU, ShardedMPPI, all_gather_into_tensor over RCCL"
-        parallelism = (f"K-sharded dp{world}, one RCCL all_gather of a {record_bytes}-byte record per rank "
-                       f"per step")
+        launcher = ("torch.distributed.run: one process per GPU, ShardedMPPI, all_gather_into_tensor over RCCL"
+                    if dist.get_backend() == "nccl" else
+                    f"torch.distributed.run, ShardedMPPI, {dist.get_backend()} exchange (rehearsal)")
+        parallelism = (f"K-sharded dp{world}, one {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} "
+                       f"all_gather of a {record_bytes}-byte record per rank per step")
     elif devices is not None:
         launcher = ("one process, C-ABI group (mppi_group_create), member threads" +
                     (", ncclCommInitAll + ncclAllGather" if group_info and group_info["rccl"] else
