@@ -205,6 +205,11 @@ struct mppi_ctx {
   int* bin_counts = nullptr;
   int* bin_cursor = nullptr;
   size_t bin_t_cap = 0;
+  // two-level binning: the tile-row-sorted queries [n] and the tile-row cursors [rows of tiles]
+  float* bin_cx = nullptr;
+  float* bin_cy = nullptr;
+  int32_t* bin_ci = nullptr;
+  size_t bin_q_cap = 0;
   // the finish the last step ran (mppi_get_launch_info): 1 column-split, 0 record tree
   int fin_kind = -1, fin_P = 0, fin_ncol = 0, fin_groups = 0;
   bool last_fused = false;  // the last step ran as one fused launch (mppi_get_launch_info info[11])
@@ -1478,6 +1483,9 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->clk) hipFree(c->clk);
   if (c->bin_counts) hipFree(c->bin_counts);
   if (c->bin_cursor) hipFree(c->bin_cursor);
+  if (c->bin_cx) hipFree(c->bin_cx);
+  if (c->bin_cy) hipFree(c->bin_cy);
+  if (c->bin_ci) hipFree(c->bin_ci);
   if (c->noise_stream) hipStreamDestroy(c->noise_stream);
   if (c->tail_stream) hipStreamDestroy(c->tail_stream);
   if (c->inj1) hipFree(c->inj1);
@@ -1909,13 +1917,24 @@ int mppi_bin_queries(mppi_ctx* c, const float* x, const float* y, int64_t n, flo
     if (c->bin_counts) HIP_TRY(hipFree(c->bin_counts));
     if (c->bin_cursor) HIP_TRY(hipFree(c->bin_cursor));
     c->bin_counts = c->bin_cursor = nullptr;
-    HIP_TRY(hipMalloc(&c->bin_counts, (size_t)nt * sizeof(int)));
+    // counts [nt], then the tile-row cursors of the two-level scatter [nt] (rows of tiles <= nt)
+    HIP_TRY(hipMalloc(&c->bin_counts, 2 * (size_t)nt * sizeof(int)));
     HIP_TRY(hipMalloc(&c->bin_cursor, (size_t)nt * sizeof(int)));
     c->bin_t_cap = (size_t)nt;
   }
+  if ((size_t)n > c->bin_q_cap) {
+    for (void* p : {(void*)c->bin_cx, (void*)c->bin_cy, (void*)c->bin_ci})
+      if (p) HIP_TRY(hipFree(p));
+    c->bin_cx = c->bin_cy = nullptr;
+    c->bin_ci = nullptr;
+    HIP_TRY(hipMalloc(&c->bin_cx, (size_t)n * sizeof(float)));
+    HIP_TRY(hipMalloc(&c->bin_cy, (size_t)n * sizeof(float)));
+    HIP_TRY(hipMalloc(&c->bin_ci, (size_t)n * sizeof(int32_t)));
+    c->bin_q_cap = (size_t)n;
+  }
   HIP_TRY(launch_bin_queries(x, y, n, c->x_min, c->y_min, c->res, c->rinv_res, c->rinv_res != 0.0f, c->rows,
                              c->cols, c->bin_tile_of, c->bin_counts, c->bin_cursor, tile_off, xs_out, ys_out,
-                             perm, c->stream));
+                             perm, c->stream, c->bin_cx, c->bin_cy, c->bin_ci, c->bin_counts + nt));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return MPPI_OK;
 }

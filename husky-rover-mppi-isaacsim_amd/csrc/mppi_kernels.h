@@ -196,12 +196,15 @@ hipError_t launch_bilinear(const float* Z, int rows, int grid, float x_min, floa
 // LDS-tiled lookup over queries binned by BIL_TILE x BIL_TILE-cell DEM tile (tile count =
 // ceil(rows/BIL_TILE) * ceil(cols/BIL_TILE) <= 16384 for rows * cols < 2^28).  Binning: G chunks of
 // the queries, each one workgroup with an LDS histogram (hist[G][ntiles] scratch), the tile
-// counts' exclusive scan, then each chunk scattered from the tile cursors; perm int32 (n < 2^31).
+// counts' exclusive scan, then the scatter: with <= 4096 tiles and the level-1 scratch (cx, cy, ci
+// [n], bcur [tile rows]) two levels of LDS-sorted runs (by tile row into cx/cy/ci, then by tile),
+// else each chunk straight from the tile cursors; perm int32 (n < 2^31).
 constexpr int BIL_TILE = 128;
 int bin_chunks(int64_t n, int ntiles);  // G for n queries
 hipError_t launch_bin_queries(const float* xs, const float* ys, int64_t n, float x_min, float y_min, float res,
                               float rinv, int cdiv, int rows, int grid, int* hist, int* counts, int* cursor,
-                              int* off, float* xs_out, float* ys_out, int32_t* perm, hipStream_t st);
+                              int* off, float* xs_out, float* ys_out, int32_t* perm, hipStream_t st,
+                              float* cx, float* cy, int32_t* ci, int* bcur);
 hipError_t launch_bilinear_tiled(const float* Z, int rows, int grid, float x_min, float y_min, float res,
                                  float rinv, int cdiv, const float* xs, const float* ys, float* hs,
                                  const int* tile_off, hipStream_t st);

@@ -3239,9 +3239,205 @@ __global__ __launch_bounds__(BIL_T) void mppi_bin_scatter_kernel(const float* __
   }
 }
 
+// Two-level scatter (ntiles <= BIN2_MAX_TILES).  The one-level scatter above writes every query to
+// a random one of the ~4096 open tile runs of its chunk (~16 queries per run), so each store
+// instruction touches 64 cache lines and every line is completed by several workgroups (1.34 ms of
+// the 1.5 ms binning at C5).  Here both levels sort a block of BIN2_S queries in LDS first and store
+// it as runs: (1) by bucket = tile row (<= 64 buckets at C5: runs of ~64 queries) into the bucket
+// regions of an intermediate array, (2) blocks of that array by tile (a block spans one or two
+// buckets, <= 2 x 64 tiles: runs of ~32-64) into the final tile runs.  Positions come from the
+// same tile counts and offsets (off) as the one-level path; the order inside a tile is arbitrary.
+constexpr int BIN2_S = 4096;            // queries per LDS-sorted block
+constexpr int BIN2_MAX_TILES = 4096;    // LDS bins of the fine level
+constexpr int BIN2_PER = BIN2_S / BIL_T;
+
+// exclusive scan of cnt[0..nb) into off[0..nb) by one 1024-thread workgroup (tmp: 1024 + 16 ints)
+__device__ inline void block_excl_scan(const int* cnt, int* off, int nb, int* tmp) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int per = (nb + BIL_T - 1) / BIL_T;
+  const int b0 = tid * per;
+  int s = 0;
+  for (int i = 0; i < per; ++i)
+    if (b0 + i < nb) s += cnt[b0 + i];
+  int x = s;  // inclusive scan inside the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) tmp[wv] = x;
+  __syncthreads();
+  int wbase = 0;
+  for (int w = 0; w < wv; ++w) wbase += tmp[w];
+  int run = wbase + x - s;
+  for (int i = 0; i < per; ++i)
+    if (b0 + i < nb) {
+      off[b0 + i] = run;
+      run += cnt[b0 + i];
+    }
+  __syncthreads();
+}
+
+// Sort up to BIN2_S (x, y, index) entries of this workgroup by key in LDS and store them as runs:
+// entry of key k at sorted position j goes to base[k] + (j - koff[k]).  kcnt/koff/base: [nk] LDS.
+struct Bin2Lds {
+  float* sx;
+  float* sy;
+  int* si;
+  unsigned short* sk;
+  int* kcnt;
+  int* koff;
+  int* base;
+  int* tmp;
+};
+
+__device__ inline Bin2Lds bin2_lds(unsigned char* sm, int nk) {
+  Bin2Lds L;
+  L.sx = reinterpret_cast<float*>(sm);
+  L.sy = L.sx + BIN2_S;
+  L.si = reinterpret_cast<int*>(L.sy + BIN2_S);
+  L.kcnt = L.si + BIN2_S;
+  L.koff = L.kcnt + nk;
+  L.base = L.koff + nk;
+  L.tmp = L.base + nk;
+  L.sk = reinterpret_cast<unsigned short*>(L.tmp + 16);
+  return L;
+}
+size_t bin2_lds_bytes(int nk) { return (size_t)BIN2_S * (3 * 4 + 2) + (size_t)(3 * nk + 16) * 4; }
+
+// place this thread's entries (key, rank inside the key) at their sorted LDS slots, then write
+// every slot to global memory at base[key] + (slot - koff[key]); kcnt must hold the block's counts
+__device__ inline void bin2_store(const Bin2Lds& L, int m, const int (&key)[BIN2_PER], const int (&rank)[BIN2_PER],
+                                  const float (&x)[BIN2_PER], const float (&y)[BIN2_PER],
+                                  const int (&idx)[BIN2_PER], float* __restrict__ ox, float* __restrict__ oy,
+                                  int32_t* __restrict__ oi) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < BIN2_PER; ++k) {
+    const int q = tid + k * BIL_T;
+    if (q < m) {
+      const int p = L.koff[key[k]] + rank[k];
+      L.sx[p] = x[k];
+      L.sy[p] = y[k];
+      L.si[p] = idx[k];
+      L.sk[p] = (unsigned short)key[k];
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < m; j += BIL_T) {
+    const int kk = L.sk[j];
+    const int pos = L.base[kk] + (j - L.koff[kk]);
+    ox[pos] = L.sx[j];
+    oy[pos] = L.sy[j];
+    oi[pos] = L.si[j];
+  }
+  __syncthreads();
+}
+
+// level 1: chunk g of the queries (the histogram kernel's chunking), blocks of BIN2_S sorted by
+// tile row into bucket regions [off[r ntx], off[(r + 1) ntx]) of (cx, cy, ci); the chunk claims its
+// share of every bucket once from bcur (initialised to the bucket starts)
+__global__ __launch_bounds__(BIL_T) void mppi_bin2_coarse_kernel(const float* __restrict__ xs,
+                                                                 const float* __restrict__ ys, int64_t n,
+                                                                 int64_t chunk, float x_min, float y_min, float res,
+                                                                 float rinv, int cdiv, int rows, int grid, int ntx,
+                                                                 int nty, int ntiles, const int* __restrict__ hist,
+                                                                 int* __restrict__ bcur, float* __restrict__ cx,
+                                                                 float* __restrict__ cy, int32_t* __restrict__ ci) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  const Bin2Lds L = bin2_lds(sm, nty);
+  const int tid = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * chunk, e = min(n, b0 + chunk);
+  for (int r = tid; r < nty; r += BIL_T) {
+    const int* gh = hist + (size_t)blockIdx.x * ntiles + (size_t)r * ntx;
+    int s = 0;
+    for (int i = 0; i < ntx; ++i) s += gh[i];
+    L.base[r] = s ? atomicAdd(&bcur[r], s) : 0;
+  }
+  for (int64_t s0 = b0; s0 < e; s0 += BIN2_S) {
+    const int m = (int)min((int64_t)BIN2_S, e - s0);
+    for (int r = tid; r < nty; r += BIL_T) L.kcnt[r] = 0;
+    __syncthreads();
+    int key[BIN2_PER], rank[BIN2_PER], idx[BIN2_PER];
+    float x[BIN2_PER], y[BIN2_PER];
+#pragma unroll
+    for (int k = 0; k < BIN2_PER; ++k) {
+      const int q = tid + k * BIL_T;
+      x[k] = q < m ? xs[s0 + q] : 0.0f;
+      y[k] = q < m ? ys[s0 + q] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < BIN2_PER; ++k) {
+      const int q = tid + k * BIL_T;
+      idx[k] = (int)(s0 + q);
+      key[k] = 0;
+      rank[k] = 0;
+      if (q < m) {
+        key[k] = query_tile(x[k], y[k], x_min, y_min, res, rinv, cdiv, rows, grid, ntx) / ntx;
+        rank[k] = atomicAdd(&L.kcnt[key[k]], 1);
+      }
+    }
+    __syncthreads();
+    block_excl_scan(L.kcnt, L.koff, nty, L.tmp);
+    bin2_store(L, m, key, rank, x, y, idx, cx, cy, ci);
+    for (int r = tid; r < nty; r += BIL_T) L.base[r] += L.kcnt[r];
+    __syncthreads();
+  }
+}
+
+// level 2: block b of the bucket-sorted array, sorted by tile and stored into the tile runs, each
+// tile's share claimed from the tile cursors (initialised to off)
+__global__ __launch_bounds__(BIL_T) void mppi_bin2_fine_kernel(const float* __restrict__ cx, const float* __restrict__ cy,
+                                                               const int32_t* __restrict__ ci, int64_t n, float x_min,
+                                                               float y_min, float res, float rinv, int cdiv, int rows,
+                                                               int grid, int ntx, int ntiles, int* __restrict__ cursor,
+                                                               float* __restrict__ xs_out, float* __restrict__ ys_out,
+                                                               int32_t* __restrict__ perm) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  const Bin2Lds L = bin2_lds(sm, ntiles);
+  const int tid = threadIdx.x;
+  const int64_t s0 = (int64_t)blockIdx.x * BIN2_S;
+  const int m = (int)min((int64_t)BIN2_S, n - s0);
+  for (int t = tid; t < ntiles; t += BIL_T) L.kcnt[t] = 0;
+  __syncthreads();
+  int key[BIN2_PER], rank[BIN2_PER], idx[BIN2_PER];
+  float x[BIN2_PER], y[BIN2_PER];
+#pragma unroll
+  for (int k = 0; k < BIN2_PER; ++k) {
+    const int q = tid + k * BIL_T;
+    x[k] = q < m ? cx[s0 + q] : 0.0f;
+    y[k] = q < m ? cy[s0 + q] : 0.0f;
+    idx[k] = q < m ? ci[s0 + q] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < BIN2_PER; ++k) {
+    const int q = tid + k * BIL_T;
+    key[k] = 0;
+    rank[k] = 0;
+    if (q < m) {
+      key[k] = query_tile(x[k], y[k], x_min, y_min, res, rinv, cdiv, rows, grid, ntx);
+      rank[k] = atomicAdd(&L.kcnt[key[k]], 1);
+    }
+  }
+  __syncthreads();
+  block_excl_scan(L.kcnt, L.koff, ntiles, L.tmp);
+  for (int t = tid; t < ntiles; t += BIL_T) {
+    const int c = L.kcnt[t];
+    L.base[t] = c ? atomicAdd(&cursor[t], c) : 0;
+  }
+  __syncthreads();
+  bin2_store(L, m, key, rank, x, y, idx, xs_out, ys_out, perm);
+}
+
+// bucket starts: bcur[r] = off[r ntx] (after the scan)
+__global__ void mppi_bin2_bucket_start_kernel(const int* __restrict__ off, int ntx, int nty, int* __restrict__ bcur) {
+  for (int r = threadIdx.x; r < nty; r += blockDim.x) bcur[r] = off[r * ntx];
+}
+
 hipError_t launch_bin_queries(const float* xs, const float* ys, int64_t n, float x_min, float y_min, float res,
                               float rinv, int cdiv, int rows, int grid, int* hist, int* counts, int* cursor,
-                              int* off, float* xs_out, float* ys_out, int32_t* perm, hipStream_t st) {
+                              int* off, float* xs_out, float* ys_out, int32_t* perm, hipStream_t st,
+                              float* cx, float* cy, int32_t* ci, int* bcur) {
   const int ntx = (grid + BIL_TS - 1) / BIL_TS, nty = (rows + BIL_TS - 1) / BIL_TS;
   const int ntiles = ntx * nty;
   hipError_t e = hipMemsetAsync(counts, 0, (size_t)ntiles * sizeof(int), st);
@@ -3253,9 +3449,17 @@ hipError_t launch_bin_queries(const float* xs, const float* ys, int64_t n, float
     hipLaunchKernelGGL(mppi_bin_hist_kernel, dim3(G), dim3(BIL_T), lds, st, xs, ys, n, chunk, x_min, y_min, res, rinv,
                        cdiv, rows, grid, ntx, ntiles, hist, counts);
   hipLaunchKernelGGL(mppi_bin_scan_kernel, dim3(1), dim3(1024), 0, st, counts, ntiles, off, cursor);
-  if (n > 0)
+  if (n > 0 && cx && ntiles <= BIN2_MAX_TILES) {  // two levels of LDS-sorted runs
+    hipLaunchKernelGGL(mppi_bin2_bucket_start_kernel, dim3(1), dim3(256), 0, st, off, ntx, nty, bcur);
+    hipLaunchKernelGGL(mppi_bin2_coarse_kernel, dim3(G), dim3(BIL_T), bin2_lds_bytes(nty), st, xs, ys, n, chunk, x_min,
+                       y_min, res, rinv, cdiv, rows, grid, ntx, nty, ntiles, hist, bcur, cx, cy, ci);
+    const unsigned nb = (unsigned)((n + BIN2_S - 1) / BIN2_S);
+    hipLaunchKernelGGL(mppi_bin2_fine_kernel, dim3(nb), dim3(BIL_T), bin2_lds_bytes(ntiles), st, cx, cy, ci, n, x_min,
+                       y_min, res, rinv, cdiv, rows, grid, ntx, ntiles, cursor, xs_out, ys_out, perm);
+  } else if (n > 0) {
     hipLaunchKernelGGL(mppi_bin_scatter_kernel, dim3(G), dim3(BIL_T), lds, st, xs, ys, n, chunk, x_min, y_min, res,
                        rinv, cdiv, rows, grid, ntx, ntiles, hist, cursor, xs_out, ys_out, perm);
+  }
   return hipGetLastError();
 }
 

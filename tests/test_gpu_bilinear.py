@@ -36,17 +36,20 @@ def _engine(Z, hw):
     return eng
 
 
-@pytest.mark.parametrize("which", ["c3", "odd"])
+@pytest.mark.parametrize("which", ["c3", "odd", "few_tiles"])
 def test_bilinear_query_and_tiled_match_oracle(which):
     import torch
-    if which == "c3":
-        Z, hw, _ = hp.c3_scene()
-    else:   # ragged map: rows/cols not multiples of the 128-cell tile
+    if which == "odd":   # ragged map: rows/cols not multiples of the 128-cell tile
         rng = np.random.default_rng(3)
         Z = rng.normal(size=(203, 203)).astype(np.float32)
         hw = 10.15
+    else:
+        Z, hw, _ = hp.c3_scene()
     n = 200_003
     x, y = _points(n, hw, seed=11)
+    if which == "few_tiles":   # every query in 4 tiles: long runs per sorted block
+        x = (x % np.float32(5.0)).astype(np.float32)
+        y = (y % np.float32(5.0)).astype(np.float32)
     want = _oracle_heights(Z, hw, x, y)
     eng = _engine(Z, hw)
     xd = torch.from_numpy(x).cuda()
