@@ -566,7 +566,9 @@ __device__ inline void cl_row_scan(__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rs
         run = min(v[k], run + w);
         v[k] = run;
       }
-      const uint32_t key = run + (uint32_t)(W - (j0 + C - 1)) * w;  // j0 + C - 1 may pass W - 1: key still > every real
+      // (a lane whose chunk passes column W - 1 may wrap its key; only later lanes, all past the
+      // map and never stored, read it)
+      const uint32_t key = run + (uint32_t)(W - (j0 + C - 1)) * w;
       const uint32_t kin = carry + (uint32_t)(W - (cb - 1)) * w;
       const uint32_t kc = min(wave_excl_min_scan_up(key), kin);
 #pragma unroll

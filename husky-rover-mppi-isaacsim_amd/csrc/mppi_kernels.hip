@@ -3336,7 +3336,8 @@ __device__ inline void bin2_store(const Bin2Lds& L, int m, const int (&key)[BIN2
 
 // level 1: chunk g of the queries (the histogram kernel's chunking), blocks of BIN2_S sorted by
 // tile row into bucket regions [off[r ntx], off[(r + 1) ntx]) of (cx, cy, ci); the chunk claims its
-// share of every bucket once from bcur (initialised to the bucket starts)
+// share of every bucket once from bcur (initialised to the bucket starts).  The next block's loads
+// are issued before the current block is sorted.
 __global__ __launch_bounds__(BIL_T) void mppi_bin2_coarse_kernel(const float* __restrict__ xs,
                                                                  const float* __restrict__ ys, int64_t n,
                                                                  int64_t chunk, float x_min, float y_min, float res,
@@ -3348,6 +3349,16 @@ __global__ __launch_bounds__(BIL_T) void mppi_bin2_coarse_kernel(const float* __
   const Bin2Lds L = bin2_lds(sm, nty);
   const int tid = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * chunk, e = min(n, b0 + chunk);
+  float xn[BIN2_PER], yn[BIN2_PER];
+  auto load = [&](int64_t s0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < BIN2_PER; ++k) {
+      const int64_t q = s0 + tid + k * BIL_T;
+      xn[k] = q < e ? xs[q] : 0.0f;
+      yn[k] = q < e ? ys[q] : 0.0f;
+    }
+  };
+  load(b0);
   for (int r = tid; r < nty; r += BIL_T) {
     const int* gh = hist + (size_t)blockIdx.x * ntiles + (size_t)r * ntx;
     int s = 0;
@@ -3357,15 +3368,15 @@ __global__ __launch_bounds__(BIL_T) void mppi_bin2_coarse_kernel(const float* __
   for (int64_t s0 = b0; s0 < e; s0 += BIN2_S) {
     const int m = (int)min((int64_t)BIN2_S, e - s0);
     for (int r = tid; r < nty; r += BIL_T) L.kcnt[r] = 0;
-    __syncthreads();
     int key[BIN2_PER], rank[BIN2_PER], idx[BIN2_PER];
     float x[BIN2_PER], y[BIN2_PER];
 #pragma unroll
     for (int k = 0; k < BIN2_PER; ++k) {
-      const int q = tid + k * BIL_T;
-      x[k] = q < m ? xs[s0 + q] : 0.0f;
-      y[k] = q < m ? ys[s0 + q] : 0.0f;
+      x[k] = xn[k];
+      y[k] = yn[k];
     }
+    load(s0 + BIN2_S);  // in flight while this block is sorted and stored
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < BIN2_PER; ++k) {
       const int q = tid + k * BIL_T;
@@ -3385,8 +3396,9 @@ __global__ __launch_bounds__(BIL_T) void mppi_bin2_coarse_kernel(const float* __
   }
 }
 
-// level 2: block b of the bucket-sorted array, sorted by tile and stored into the tile runs, each
-// tile's share claimed from the tile cursors (initialised to off)
+// level 2: blocks b = blockIdx.x, blockIdx.x + gridDim.x, ... of the bucket-sorted array, each
+// sorted by tile and stored into the tile runs, each tile's share claimed from the tile cursors
+// (initialised to off); the next block's loads issued before the current block is sorted
 __global__ __launch_bounds__(BIL_T) void mppi_bin2_fine_kernel(const float* __restrict__ cx, const float* __restrict__ cy,
                                                                const int32_t* __restrict__ ci, int64_t n, float x_min,
                                                                float y_min, float res, float rinv, int cdiv, int rows,
@@ -3396,37 +3408,53 @@ __global__ __launch_bounds__(BIL_T) void mppi_bin2_fine_kernel(const float* __re
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   const Bin2Lds L = bin2_lds(sm, ntiles);
   const int tid = threadIdx.x;
-  const int64_t s0 = (int64_t)blockIdx.x * BIN2_S;
-  const int m = (int)min((int64_t)BIN2_S, n - s0);
-  for (int t = tid; t < ntiles; t += BIL_T) L.kcnt[t] = 0;
-  __syncthreads();
-  int key[BIN2_PER], rank[BIN2_PER], idx[BIN2_PER];
-  float x[BIN2_PER], y[BIN2_PER];
+  const int64_t nblk = (n + BIN2_S - 1) / BIN2_S;
+  float xn[BIN2_PER], yn[BIN2_PER];
+  int in_[BIN2_PER];
+  auto load = [&](int64_t blk) __attribute__((always_inline)) {
 #pragma unroll
-  for (int k = 0; k < BIN2_PER; ++k) {
-    const int q = tid + k * BIL_T;
-    x[k] = q < m ? cx[s0 + q] : 0.0f;
-    y[k] = q < m ? cy[s0 + q] : 0.0f;
-    idx[k] = q < m ? ci[s0 + q] : 0;
-  }
-#pragma unroll
-  for (int k = 0; k < BIN2_PER; ++k) {
-    const int q = tid + k * BIL_T;
-    key[k] = 0;
-    rank[k] = 0;
-    if (q < m) {
-      key[k] = query_tile(x[k], y[k], x_min, y_min, res, rinv, cdiv, rows, grid, ntx);
-      rank[k] = atomicAdd(&L.kcnt[key[k]], 1);
+    for (int k = 0; k < BIN2_PER; ++k) {
+      const int64_t q = blk * BIN2_S + tid + k * BIL_T;
+      const bool ok = blk < nblk && q < n;
+      xn[k] = ok ? cx[q] : 0.0f;
+      yn[k] = ok ? cy[q] : 0.0f;
+      in_[k] = ok ? ci[q] : 0;
     }
+  };
+  load(blockIdx.x);
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t s0 = blk * BIN2_S;
+    const int m = (int)min((int64_t)BIN2_S, n - s0);
+    for (int t = tid; t < ntiles; t += BIL_T) L.kcnt[t] = 0;
+    int key[BIN2_PER], rank[BIN2_PER], idx[BIN2_PER];
+    float x[BIN2_PER], y[BIN2_PER];
+#pragma unroll
+    for (int k = 0; k < BIN2_PER; ++k) {
+      x[k] = xn[k];
+      y[k] = yn[k];
+      idx[k] = in_[k];
+    }
+    load(blk + gridDim.x);  // in flight while this block is sorted and stored
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < BIN2_PER; ++k) {
+      const int q = tid + k * BIL_T;
+      key[k] = 0;
+      rank[k] = 0;
+      if (q < m) {
+        key[k] = query_tile(x[k], y[k], x_min, y_min, res, rinv, cdiv, rows, grid, ntx);
+        rank[k] = atomicAdd(&L.kcnt[key[k]], 1);
+      }
+    }
+    __syncthreads();
+    block_excl_scan(L.kcnt, L.koff, ntiles, L.tmp);
+    for (int t = tid; t < ntiles; t += BIL_T) {
+      const int c = L.kcnt[t];
+      L.base[t] = c ? atomicAdd(&cursor[t], c) : 0;
+    }
+    __syncthreads();
+    bin2_store(L, m, key, rank, x, y, idx, xs_out, ys_out, perm);
   }
-  __syncthreads();
-  block_excl_scan(L.kcnt, L.koff, ntiles, L.tmp);
-  for (int t = tid; t < ntiles; t += BIL_T) {
-    const int c = L.kcnt[t];
-    L.base[t] = c ? atomicAdd(&cursor[t], c) : 0;
-  }
-  __syncthreads();
-  bin2_store(L, m, key, rank, x, y, idx, xs_out, ys_out, perm);
 }
 
 // bucket starts: bcur[r] = off[r ntx] (after the scan)
@@ -3453,7 +3481,8 @@ hipError_t launch_bin_queries(const float* xs, const float* ys, int64_t n, float
     hipLaunchKernelGGL(mppi_bin2_bucket_start_kernel, dim3(1), dim3(256), 0, st, off, ntx, nty, bcur);
     hipLaunchKernelGGL(mppi_bin2_coarse_kernel, dim3(G), dim3(BIL_T), bin2_lds_bytes(nty), st, xs, ys, n, chunk, x_min,
                        y_min, res, rinv, cdiv, rows, grid, ntx, nty, ntiles, hist, bcur, cx, cy, ci);
-    const unsigned nb = (unsigned)((n + BIN2_S - 1) / BIN2_S);
+    // persistent: one workgroup per CU (its LDS), each looping over blocks
+    const unsigned nb = (unsigned)std::min<int64_t>((n + BIN2_S - 1) / BIN2_S, 256);
     hipLaunchKernelGGL(mppi_bin2_fine_kernel, dim3(nb), dim3(BIL_T), bin2_lds_bytes(ntiles), st, cx, cy, ci, n, x_min,
                        y_min, res, rinv, cdiv, rows, grid, ntx, ntiles, cursor, xs_out, ys_out, perm);
   } else if (n > 0) {
