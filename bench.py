@@ -602,6 +602,10 @@ def main():
                 "parallelism": parallelism,
                 "launcher": launcher,
                 "group": group_info,
+                # ranks of the communicator the records travel over (torch.distributed's, or the
+                # C-ABI group's ncclCommCount; 0: device copies / one GPU)
+                "rccl_ranks": (dist.get_world_size() if dist is not None and world > 1 and dist.get_backend() == "nccl"
+                               else (group_info or {}).get("rccl_ranks", 0)),
                 "record_bytes_per_rank": record_bytes,
                 "speedup_vs_1": round(speedup, 3) if speedup is not None else None,
                 "rollout_kernel": info,
