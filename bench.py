@@ -48,6 +48,8 @@ HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 # name -> (K global, H, scene function name, start, goal, description)
 CONFIGS = {
+    "c2": (4096, 50, "scene_c3", (-60.0, -5.0), (65.0, 10.0),
+           "C2: K=4096, H=50, 1500^2 DEM @0.1 m, 750^2 costmap @0.2 m"),
     "c3": (65536, 100, "scene_c3", (-60.0, -5.0), (65.0, 10.0),
            "C3: K=65536, H=100, 1500^2 DEM @0.1 m, 750^2 costmap @0.2 m"),
     "c4": (1048576, 100, "scene_c3", (-60.0, -5.0), (65.0, 10.0),
@@ -646,6 +648,13 @@ def main():
             rec["c4"] = c4
         if world == 1 and devices is None and not args.no_bilinear:
             rec["bilinear_roofline"] = bilinear_bench(torch, torch.device("cuda", local_rank))
+        if world == 1 and devices is None and not args.no_c5 and args.config != "c2":
+            # C2 (SURVEY.md §8(d) reports C2-C5): the small config, latency-bound (the H-step chain)
+            r2 = Runner("c2", local_rank, 1, solo=True)
+            t2 = timed_run(torch, None, r2, args.proj, 20, 200, 0, not args.sync)
+            r2.close()
+            rec["c2"] = {"workload": CONFIGS["c2"][5], "steps_per_s": round(200 / t2, 3),
+                         "ms_per_step": round(t2 / 200 * 1e3, 4)}
         if world == 1 and devices is None and not args.no_c5 and args.config != "c5":
             r5 = Runner("c5", local_rank, 1, solo=True)
             t5 = timed_run(torch, None, r5, args.proj, 10, 50, 0, not args.sync)
