@@ -1074,6 +1074,9 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
         a.rec_m[blockIdx.x] = lm[0];
     }
   }
+#ifdef MPPI_STAMPS
+  LEAF_STAMP(5);
+#endif
 }
 
 // =====================================================================  pair-synchronised rollout kernel

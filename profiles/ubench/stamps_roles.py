@@ -42,6 +42,17 @@ def main():
         w = ww[:, 4 * r:4 * r + 4]
         print(f"  {nm:6s} work {w[..., 0].mean():8.1f}  wait {w[..., 1].mean():8.1f}  "
               f"LDS waits/step {cnt[:, 4 * r:4 * r + 4].mean():5.2f}")
+    # leaf_records stamps of thread 0 (the chain wave of group 0; s_memtime cycles):
+    # 0 entry, 1 after the weights (its first barrier waits for every role's last step),
+    # 4 after the rows (loads + float64 line sums), 5 after the record tree and stores
+    n2 = 64 * 16 * 6 + 1024 * 2 + 64 * 8
+    b2 = (C.c_uint64 * n2)()
+    assert lib.mppi_debug_stamps(b2, n2) == 0
+    lf = np.array(b2, dtype=np.float64)[64 * 16 * 6 + 1024 * 2:].reshape(64, 8)[:nb]
+    if lf[:, 5].max() > 0:
+        print(f"  leaf (cycles, mean over {nb} workgroups): barrier+weights {np.mean(lf[:, 1] - lf[:, 0]):7.0f}  "
+              f"rows {np.mean(lf[:, 4] - lf[:, 1]):7.0f}  record {np.mean(lf[:, 5] - lf[:, 4]):7.0f}  "
+              f"total {np.mean(lf[:, 5] - lf[:, 0]):7.0f}")
 
 
 if __name__ == "__main__":
