@@ -399,7 +399,7 @@ def timed_run(torch, dist, run, proj, warmup, steps, step0, async_tail, kernel_t
         run.step(proj, step0 + i)
 
     def barrier():
-        for e in run.engines:  # cancels an armed next step (never part of the timed steps), then syncs
+        for e in run.engines:  # stops a resident step server (mppi_sync), then syncs
             e.sync()
         for d in sorted({e.device for e in run.engines}):
             torch.cuda.synchronize(d)
@@ -506,6 +506,7 @@ def main():
     nt = max(args.steps // 4, 10)
     el = timed_run(torch, dist, run, args.proj, args.warmup, args.steps, s0, not args.sync,
                    kernel_timing=2 if args.timed_events else 0)
+    head_info = run.eng.launch_info()   # the schedule the timed steps ran on
     if not args.timed_events:
         timed_run(torch, dist, run, args.proj, args.warmup, nt, 2 * s0, not args.sync, kernel_timing=2)
     roll_ms, _, n_roll = run.eng.timing()
@@ -578,10 +579,10 @@ def main():
         k_avg_ms = roll_ms / max(n_roll, 1)
         alg_bytes = BYTES_PER_ROLLOUT_STEP * k_local * H
         achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9
-        # the rollout kernel the plan chose: role split (1024-thread workgroups) or pair (512), or
-        # the fused step launch (rollout + finish in one kernel)
-        kernel = ("mppi_step_fused_kernel" if info.get("fused") else
-                  "mppi_rollout_roles_kernel" if info.get("block") == 1024 else "mppi_rollout_pair_kernel")
+        # the rollout kernel the plan chose: role split (1024-thread workgroups) or pair (512); the
+        # headline steps run its body inside the resident step server, the kernel time comes from
+        # the separate-launch timing pass (the same rollout body, HIP events around each launch)
+        kernel = "mppi_rollout_roles_kernel" if info.get("block") == 1024 else "mppi_rollout_pair_kernel"
         traffic, traffic_src = pmc_traffic(args.pmc_json, kernel, k_local, H)
         rec = {
             "metric": "MPPI steps/sec at K=65536 H=100 on 750x750 costmap; 1/2/4/8-GPU scaling",
@@ -615,8 +616,10 @@ def main():
                 "prewarm": {"ms": args.prewarm_ms, "steps": prewarm_steps},
                 "sync_steps_per_s": round(args.steps / el_sync, 3) if el_sync else None,
                 "sync_ms_per_step": round(el_sync / args.steps * 1e3, 4) if el_sync else None,
-                # (a fused step launch has no separate finish kernel: it is inside the kernel timed above)
-                "finish_kernel_avg_ms": round(fin_ms / max(n_fin, 1), 5) if not info.get("fused") else None,
+                "schedule": ("resident step server (mppi_step_server_kernel)" if head_info.get("resident")
+                             else "separate launches (rollout, finish, deferred tail)"),
+                "server_launches": head_info.get("server_launches"),
+                "finish_kernel_avg_ms": round(fin_ms / max(n_fin, 1), 5),
                 "chain": {"instructions_per_step": chain_static(),
                           "cycles_per_step": round(clock["cycles_per_step"], 1),
                           "shader_clock_mhz": round(clock["shader_mhz"], 1),

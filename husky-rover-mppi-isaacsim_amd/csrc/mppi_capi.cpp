@@ -62,17 +62,6 @@ struct Plan {
 
 }  // namespace
 
-// Host bookkeeping that enqueueing a sampled step changes (the armed next step is enqueued with
-// these advanced, then they are put back until the step is taken).
-struct Book {
-  unsigned seq = 0, wait_seq = 0;
-  int fin_kind = -1, fin_P = 0, fin_ncol = 0, fin_groups = 0;
-  bool last_fused = false;
-  int tail_par = 0;
-  bool tail_pending = false;
-  bool tail_inflight[kTailSlots] = {};
-};
-
 struct mppi_ctx {
   mppi_params p{};
   int device = 0;
@@ -118,86 +107,48 @@ struct mppi_ctx {
   float* out_host = nullptr;  // [16H] last complete outputs (host memory)
   float* inj1 = nullptr;
   float* inj2 = nullptr;
-  // precomputed sampling normals (pair kernel, MODE 0): two slots, each tagged with the
-  // Philox step it holds; the next step's normals are generated speculatively on
-  // noise_stream while the GPU is otherwise idle (finish kernel, host gap)
-  // sampling normals, one slot per step in flight: the rollout's, the next step's and the
-  // one after (generated two steps ahead, so the noise kernel is never on the step's path)
+  // sampling normals, one slot per step in flight: the rollout's, the next step's and the one
+  // after (generated two steps ahead, so the noise kernel is never on the step's path)
   float* eps[kEpsSlots] = {nullptr, nullptr, nullptr};
   size_t eps_cap = 0;
   int64_t eps_step[kEpsSlots] = {-1, -1, -1};
   hipEvent_t eps_ev[kEpsSlots] = {nullptr, nullptr, nullptr};
   bool eps_pending[kEpsSlots] = {false, false, false};
-  int noise_ahead = 2;  // steps of normals generated ahead (env MPPI_NOISE_AHEAD=1: the next only)
-  // where the noise stream is handed the steps ahead: 0 = after the rollout launch (beside the
-  // finish), 1 = after the finish launch (env MPPI_NOISE_AT)
-  int noise_at = 0;
-  bool spec_pending = false;
-  bool prev_roll_valid = false;  // MPPI_NOISE_AT=2: ev_prev_roll marks the previous rollout
-  Plan spec_plan;
-  uint64_t spec_step = 0;
-  int spec_slot = 0;
   hipStream_t noise_stream = nullptr;
   int prio_least = 0, prio_greatest = 0;
   // finish: 1 = column-split kernel (mppi_colfin_kernel) where it applies, 0 = the record tree
-  // (env MPPI_COLFIN=0)
+  // (mppi_set_option "record_tree_finish")
   int colfin = 1;
-  // pair kernel: keep the first steps' sampled controls in spare LDS for the leaf reduction
-  // (env MPPI_UCACHE=0: re-read every normals row)
-  int ucache = 1;
   int num_cus = 256;  // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   // host-side step timeline (env MPPI_HOST_TRACE=1, printed by mppi_destroy): microseconds summed
-  // over steps of [previous done seen -> entry, entry -> rollout enqueued, -> all enqueued, wait]
+  // over steps of [previous done seen -> entry, entry -> launches enqueued, -> wait entered, wait]
   bool trace = false;
-  double tr_prev_done = 0, tr_sum[4] = {0, 0, 0, 0}, tr_t0 = 0, tr_t1 = 0, tr_mark[4] = {0, 0, 0, 0};
-  double tr_msum[4] = {0, 0, 0, 0};
+  double tr_prev_done = 0, tr_sum[4] = {0, 0, 0, 0}, tr_t0 = 0, tr_t1 = 0;
+  double tr_srv[4] = {0, 0, 0, 0};  // server steps: stop / relaunch, normals wait, tail-slot wait, side launches
   long tr_n = 0;
-  int wave_prio = 1;  // rollout waves raise their issue priority (env MPPI_WAVE_PRIO=0: off)
   int roles = -1;     // rollout kernel: -1 auto (role split at <= 1 workgroup per CU), 0 pair, 1 roles (MPPI_ROLES)
-  int fused = 1;               // one launch per step (mppi_step_fused_kernel): 0 never, 1 synchronous steps only,
-                               // 2 also with the deferred optimal rollout (MPPI_FUSED; 2 is faster on average but
-                               // unstable run to run: profiles/r03_notes.md)
-  int fused_noise_groups = -1; // noise of step + 2: -1 inside the launch on one workgroup per CU the finish leaves
-                               // (default), n > 0 on n workgroups, 0 before the launch on the context stream, -2
-                               // after the launch on the noise stream behind a gate kernel that waits for the
-                               // launch's rollout part (MPPI_FUSED_NOISE_GROUPS)
-  // fused launch: the noise of step + 2 on the noise stream behind a one-wave gate kernel that
-  // waits for this word, which the launch writes when its rollout part is done
-  // (MPPI_FUSED_NOISE_GROUPS=-2); nullptr otherwise
-  unsigned* sig = nullptr;
-  unsigned sig_seq = 0;
-  uint64_t fused_wait_ticks = 200000000ull;  // fused finish's record wait bound (2 s at 100 MHz; mppi_set_option)
-  int noise_gpc = 0;  // noise kernel workgroups per CU: 0 auto = 4 (measured: profiles/r02_notes.md) (MPPI_NOISE_GPC)
-  hipEvent_t ev_roll_done = nullptr;
+  // Resident step server (mppi_step_server_kernel): sampled steps of the role-split plan run on one
+  // resident launch that polls the command block `cmd` (pinned) instead of one launch per step
+  // (mppi_set_option "resident", env MPPI_RESIDENT; default on).  It exits after srv_idle_us without a
+  // command, on cmd->stop (every other call on the context stops it first: quiesce) or on a failed
+  // step; the host relaunches it when the last command is older than half the idle limit.
+  int resident = 1;
+  ServerCmd* cmd = nullptr;   // pinned
+  unsigned* sigs = nullptr;   // pinned: [0] roll_done (noise gate), [16] fin_done (tail gate)
+  unsigned* relay = nullptr;  // device [64]: workgroup 0's relay of the command (ServerArgs::relay)
+  bool srv_running = false;
+  int srv_proj = 0;
+  double srv_last_us = 0;     // host time of the last command
+  uint64_t srv_idle_us = 2000;
+  int64_t srv_launches = 0, srv_steps = 0, srv_failed = 0;
+  uint64_t fin_wait_ticks = 200000000ull;  // a finish's record wait bound (2 s at 100 MHz; mppi_set_option)
   hipEvent_t ev_prev_roll = nullptr;  // recorded after the last rollout that read an eps slot
   // finish: column-split u_opt slice records / first tree level, arrival counter
   double* level1 = nullptr;       // finish kernel first-level records
   size_t level1_cap = 0;
-  unsigned* level1_cnt = nullptr;
+  unsigned* level1_cnt = nullptr;  // [0]: finish handoff, [16]: the server's record count
   unsigned long long* uopt = nullptr;  // [2H] the column-split finish's tagged u_opt words
-  // Armed next step (pre-enqueue): after a sampled mppi_step has enqueued its launches, the next
-  // step's launches (step + 1, same projection) are enqueued behind mppi_arm_gate_kernel, which
-  // waits at most arm_ticks for the next call to store the robot state and its go word in pinned
-  // memory; the GPU then starts that step without a host launch on its path.  Any other call on
-  // the context, a different step / projection, or an expired gate cancels it (disarm), and the
-  // call runs the ordinary way.  Off by default (MPPI_ARM=1 / mppi_set_option("arm", 1)): on
-  // MI355X the gate is one more dependent kernel on the step's path (~6 us dispatch gap after the
-  // finish, ~4 us until it sees go, ~6 us to the rollout: 16.8 us from the finish's end to the next
-  // rollout's start) against 8.7 us for the host's own launch (kernel trace, profiles/r03_notes.md).
-  int arm = 0;
-  uint64_t arm_ticks = 50000;  // 500 us of the 100 MHz clock (mppi_set_option "arm_wait_us")
-  StepDyn* dyn_host = nullptr;  // pinned
-  StepDyn* dyn_dev = nullptr;
-  unsigned* gate_out = nullptr;  // pinned: the gate's decision (id, | kArmCancel [| kArmExpired])
-  const StepDyn* cur_dyn = nullptr;  // fill_rollout / fill_finish: set while the armed step is enqueued
-  bool armed = false;
-  bool arm_ready = false;  // the last sampled step enqueued with every buffer already allocated
-  unsigned arm_id = 0;
-  int arm_proj = 0;
-  uint64_t arm_step = 0;
-  Book arm_post;
   unsigned wait_seq = 0;  // the completion word wait_done waits for
-  int64_t arm_taken = 0, arm_cancelled = 0, arm_expired = 0;
   uint64_t* clk = nullptr;  // [4] chain clock stamps of the last sampled rollout (RolloutArgs::clk)
   // tiled bilinear binning scratch
   int* bin_tile_of = nullptr;  // per-chunk tile histograms [chunks][tiles]
@@ -212,7 +163,7 @@ struct mppi_ctx {
   size_t bin_q_cap = 0;
   // the finish the last step ran (mppi_get_launch_info): 1 column-split, 0 record tree
   int fin_kind = -1, fin_P = 0, fin_ncol = 0, fin_groups = 0;
-  bool last_fused = false;  // the last step ran as one fused launch (mppi_get_launch_info info[11])
+  bool last_resident = false;  // the last step ran on the resident server (mppi_get_launch_info info[11])
   // last step (for dump)
   bool have_last = false;
   int last_proj = 3, last_mode = 0;
@@ -331,7 +282,7 @@ Plan make_plan(const mppi_ctx* c) {
                  (size_t)((2 * H + 3) & ~3) * sizeof(float) + scratch;
   // only at one workgroup per CU: the cache takes the CU's spare LDS, which at larger K
   // (C5: 4 workgroups per CU) would cost a co-resident rollout workgroup instead
-  if (c->ucache && pl.blocks <= c->num_cus) {
+  if (pl.blocks <= c->num_cus) {
     // the rest of the CU's LDS keeps the sampled controls of the first steps ([2][T][TB]
     // floats, 16-byte aligned after the scratch), so the leaf reduction re-reads only the
     // other steps' normals from HBM (all workgroups reduce at once: a bandwidth burst)
@@ -339,7 +290,7 @@ Plan make_plan(const mppi_ctx* c) {
     // 15H floats), which runs beside a rollout workgroup on one CU
     const size_t base = (pl.lds_bytes + 15) / 16 * 16;
     const size_t row2 = (size_t)2 * (TB + 4) * sizeof(float);  // UCACHE_ROW: one float4 of bank skew
-    // (1 KiB more: the fused step launch's static ticket words and LDS allocation granularity)
+    // (1 KiB more: the server kernel's static command / ticket words and LDS allocation granularity)
     const size_t budget = kLdsBytes - ((size_t)15 * H * sizeof(float) + 2047) / 1024 * 1024 - 1024;
     pl.ucache_steps = base < budget ? (int)std::min<size_t>((size_t)H, (budget - base) / row2) : 0;
     if (pl.ucache_steps > 0) pl.lds_bytes = base + (size_t)pl.ucache_steps * row2;
@@ -352,14 +303,10 @@ Plan make_plan(const mppi_ctx* c) {
   return pl;
 }
 
-// Noise grid: a few 4-wave workgroups per CU.  The noise of step i+2 runs beside the finish of
-// step i and the start of rollout i+1.  4 per CU measured best at C3 with the rollout's side roles
-// at priority 0 (10095 steps/s against 9920 at 3 and 9730 at 2, alternating runs:
-// profiles/r02_notes.md); MPPI_NOISE_GPC overrides.
-int noise_groups(const mppi_ctx* c, const Plan& pl) {
-  const int gpc = c->noise_gpc > 0 ? c->noise_gpc : 4;
-  return std::max(c->num_cus, 1) * gpc;
-}
+// Noise grid: 4 four-wave workgroups per CU.  The noise of step i+2 runs beside the finish of
+// step i and the start of rollout i+1 (4 per CU measured best at C3: 10095 steps/s against 9920 at
+// 3 and 9730 at 2, alternating runs, profiles/r02_notes.md).
+int noise_groups(const mppi_ctx* c) { return std::max(c->num_cus, 1) * 4; }
 
 int ensure_nodes(mppi_ctx* c, int blocks) {
   const size_t need = (size_t)std::max(blocks, 1) * E_of(c);
@@ -379,9 +326,9 @@ int ensure_nodes(mppi_ctx* c, int blocks) {
   return MPPI_OK;
 }
 
-// The rollout / finish fields that follow from the robot state (an armed step's StepDyn block, filled
-// at its call; fill_rollout the same way).
-void dyn_from_state(const mppi_params& p, const mppi_state& st, StepDyn& d) {
+// The rollout / finish fields that follow from the robot state, in the server command's layout
+// (fill_rollout copies them into the launch arguments).
+void state_fields(const mppi_params& p, const mppi_state& st, ServerCmd& d) {
   d.x0 = st.x;
   d.y0 = st.y;
   d.h0x = st.heading[0];
@@ -429,8 +376,8 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   a.cdiv_res = c->rinv_res != 0.0f;
   a.rinv_res_c = c->rinv_res_c;
   a.cdiv_res_c = c->rinv_res_c != 0.0f;
-  StepDyn d;
-  dyn_from_state(p, st, d);
+  ServerCmd d;
+  state_fields(p, st, d);
   a.x0 = d.x0;
   a.y0 = d.y0;
   a.h0x = d.h0x;
@@ -475,10 +422,10 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   a.clk = c->clk;
   a.nodes = c->nodes;
   a.rec_m = c->rec_m;
-  a.dyn = c->cur_dyn;
   a.ustore = c->ustore;
   a.inj_u1 = c->inj1;
   a.inj_u2 = c->inj2;
+  a.wave_prio = 1;
 }
 
 void fill_finish(const mppi_ctx* c, const Plan& pl, const mppi_state& st, FinishArgs& f) {
@@ -489,7 +436,6 @@ void fill_finish(const mppi_ctx* c, const Plan& pl, const mppi_state& st, Finish
   f.scratch0 = c->scratch0;
   f.scratch1 = c->scratch1;
   f.uopt = c->uopt;
-  f.dyn = c->cur_dyn;
   f.u_nom_next = c->u_nom[c->cur ^ 1];
   f.out = c->stage;
   f.Z = c->Z;
@@ -527,7 +473,7 @@ void fill_finish(const mppi_ctx* c, const Plan& pl, const mppi_state& st, Finish
 void collect_timing(mppi_ctx* c) {
   float ms = 0.f;
   // mode 2: the host spun on the completion word, which the finish (enqueued after ev[1])
-  // publishes, so ev[1] has retired already (a fused launch publishes before its end: wait)
+  // publishes, so ev[1] has retired already
   if (c->ev_roll_pending && hipEventSynchronize(c->ev[1]) == hipSuccess &&
       hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) {
     c->t_roll += ms;
@@ -554,7 +500,6 @@ int sync_tail(mppi_ctx* c) {
   bool any = c->tail_pending;
   for (int i = 0; i < kTailSlots; ++i) any |= c->tail_inflight[i];
   if (!any) return MPPI_OK;
-  // the slots' own events, not the side stream: an armed next step's tail may be queued there
   for (int i = 0; i < kTailSlots; ++i)
     if (c->tail_inflight[i] || (c->tail_pending && i == c->tail_par)) HIP_TRY(hipEventSynchronize(c->ev_tail[i]));
   collect_tail_timing(c);
@@ -567,47 +512,75 @@ int sync_tail(mppi_ctx* c) {
   return MPPI_OK;
 }
 
-// The signal word at the latest sequence number the noise stream may wait for: a launch that did
-// not write it (failed step, context teardown) must not leave the noise stream waiting.
-void release_signal(mppi_ctx* c) {
-  if (!c->sig) return;
-  const unsigned v = c->sig_seq;
-  if (hipMemcpy(c->sig, &v, sizeof(v), hipMemcpyHostToDevice) != hipSuccess) (void)hipGetLastError();
+// The gates of the noise / tail launches waiting on a step that will not publish (failed step,
+// stopped server): open them at the latest sequence number.
+void release_gates(mppi_ctx* c) {
+  if (!c->sigs) return;
+  __atomic_store_n(c->sigs, c->seq, __ATOMIC_RELEASE);
+  __atomic_store_n(c->sigs + 16, c->seq, __ATOMIC_RELEASE);
 }
 
-// Zero the finish handoff counters (level1_cnt[0]) and the fused launch's record counter
-// ([16]) after a step that did not complete them; the context stream must be idle.
+// Stop the resident server (it finishes the step it runs, sees cmd->stop and exits): every call on
+// the context but mppi_step / set_state / get_outputs / get_timing starts with this.
+void quiesce(mppi_ctx* c) {
+  if (!c || !c->srv_running) return;
+  __atomic_store_n(&c->cmd->stop, 1u, __ATOMIC_RELEASE);
+  hipSetDevice(c->device);
+  if (hipStreamSynchronize(c->stream) != hipSuccess) (void)hipGetLastError();
+  __atomic_store_n(&c->cmd->stop, 0u, __ATOMIC_RELEASE);
+  c->srv_running = false;
+}
+
+// Zero the finish handoff counter (level1_cnt[0]) and the server's record counter ([16]) after a
+// step that did not complete them; no launch of the context may be running.
 void rearm_counters(mppi_ctx* c) {
   if (hipMemsetAsync(c->level1_cnt, 0, 128, c->stream) == hipSuccess) hipStreamSynchronize(c->stream);
-  release_signal(c);
+  release_gates(c);
 }
 
-// Spin until the finish kernel has published c->seq (all outputs in pinned host
-// memory); a fault surfaces through hipStreamQuery.
+// Spin until the finish has published c->wait_seq (all outputs in pinned host memory).  A finish
+// that gave up (done | kDoneFail), a launch that retired without publishing, a stream error or
+// 10 s without completion fail the step; the server is stopped and the counters re-armed.
 int wait_done(mppi_ctx* c) {
   if (c->timing == 1) {  // the finish's timing events need the stream to retire
     HIP_TRY(hipStreamSynchronize(c->stream));
   }
+  const unsigned want = c->wait_seq;
+  const double t0 = now_us();
+  std::string why;
   for (uint64_t i = 0;; ++i) {
-    if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == c->wait_seq) return MPPI_OK;
+    const unsigned v = __atomic_load_n(c->done, __ATOMIC_ACQUIRE);
+    if (v == want) return MPPI_OK;
+    if (v == (want | kDoneFail)) {
+      why = "the finish gave up waiting for the step's records";
+      break;
+    }
     if ((i & 255) == 255) {
       const hipError_t e = hipStreamQuery(c->stream);
       if (e == hipSuccess) {
-        if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == c->wait_seq) return MPPI_OK;
-        // a finish that gave up waiting for records (fused launch) left its counters mid-count:
-        // re-arm them (the stream is idle) so that the next step starts from zero
-        rearm_counters(c);
-        return fail(MPPI_EHIP, "finish kernel retired without publishing its outputs");
+        if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == want) return MPPI_OK;
+        why = "the step's launch retired without publishing its outputs";
+        c->srv_running = false;  // (an idle server has exited: the stream is empty)
+        break;
       }
       if (e != hipErrorNotReady) return fail(MPPI_EHIP, std::string("step failed: ") + hipGetErrorString(e));
+      if (now_us() - t0 > 10e6) {
+        why = "the step did not complete within 10 s";
+        break;
+      }
     }
     __builtin_ia32_pause();
   }
+  ++c->srv_failed;
+  quiesce(c);
+  rearm_counters(c);
+  return fail(MPPI_EHIP, why);
 }
 
-// Normals of Philox step `step` in an eps slot, generated on the context stream if no
-// slot holds them (first step, or a step counter that did not advance by one).
-int eps_for_step(mppi_ctx* c, const Plan& pl, uint64_t step, int* slot_out) {
+// Normals of Philox step `step` in an eps slot, generated on `st` if no slot holds them (first
+// step, or a step counter that did not advance by one).  sync: wait for the slot on the host (the
+// server reads it without stream order) instead of ordering `st` after it.
+int eps_for_step(mppi_ctx* c, const Plan& pl, uint64_t step, hipStream_t st, bool sync, int* slot_out) {
   const size_t need = (size_t)pl.blocks * 2 * H_of(c) * 256;
   if (need > c->eps_cap) {
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -622,84 +595,75 @@ int eps_for_step(mppi_ctx* c, const Plan& pl, uint64_t step, int* slot_out) {
     c->eps_cap = need;
   }
   const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
-  for (int i = 0; i < kEpsSlots; ++i) {
-    if (c->eps_step[i] == (int64_t)step) {
-      if (c->eps_pending[i]) {  // generated on noise_stream: order it before this rollout
-        const hipError_t q = hipEventQuery(c->eps_ev[i]);
-        if (q == hipErrorNotReady) HIP_TRY(hipStreamWaitEvent(c->stream, c->eps_ev[i], 0));
-        else if (q != hipSuccess) return fail(MPPI_EHIP, std::string("noise: ") + hipGetErrorString(q));
+  int slot = -1;
+  for (int i = 0; i < kEpsSlots; ++i)
+    if (c->eps_step[i] == (int64_t)step) slot = i;
+  if (slot < 0) {
+    // not precomputed: any in-flight fill must finish before a slot is reused
+    for (int i = 0; i < kEpsSlots; ++i)
+      if (c->eps_pending[i]) {
+        HIP_TRY(sync ? hipEventSynchronize(c->eps_ev[i]) : hipStreamWaitEvent(st, c->eps_ev[i], 0));
         c->eps_pending[i] = false;
       }
-      *slot_out = i;
-      return MPPI_OK;
-    }
+    slot = 0;
+    for (int i = 0; i < kEpsSlots; ++i) c->eps_step[i] = -1;
+    HIP_TRY(launch_noise(c->p.seed, step * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[slot], st, noise_groups(c)));
+    c->eps_step[slot] = (int64_t)step;
+    if (sync) HIP_TRY(hipStreamSynchronize(st));
+  } else if (c->eps_pending[slot]) {  // generated on noise_stream: before this rollout
+    const hipError_t q = hipEventQuery(c->eps_ev[slot]);
+    if (q == hipErrorNotReady) HIP_TRY(sync ? hipEventSynchronize(c->eps_ev[slot]) : hipStreamWaitEvent(st, c->eps_ev[slot], 0));
+    else if (q != hipSuccess) return fail(MPPI_EHIP, std::string("noise: ") + hipGetErrorString(q));
+    c->eps_pending[slot] = false;
   }
-  // not precomputed: any in-flight speculative fill must finish before a slot is reused
-  for (int i = 0; i < kEpsSlots; ++i)
-    if (c->eps_pending[i]) {
-      HIP_TRY(hipStreamWaitEvent(c->stream, c->eps_ev[i], 0));
-      c->eps_pending[i] = false;
-    }
-  const int slot = 0;
-  HIP_TRY(launch_noise(c->p.seed, step * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[slot], c->stream,
-                       noise_groups(c, pl)));
-  for (int i = 0; i < kEpsSlots; ++i) c->eps_step[i] = -1;
-  c->eps_step[slot] = (int64_t)step;
   *slot_out = slot;
   return MPPI_OK;
 }
 
-// A slot other than `used` that holds none of the steps in (step, step + ahead]: the
-// stalest one (its last reader is a rollout enqueued before the current one).
-int eps_victim(const mppi_ctx* c, int used, uint64_t step, int ahead) {
+// A slot other than `used` that holds none of the steps in (step, step + 2]: the stalest one (its
+// last reader is a rollout enqueued before the current one).
+int eps_victim(const mppi_ctx* c, int used, uint64_t step) {
   for (int i = 0; i < kEpsSlots; ++i) {
     if (i == used) continue;
     const int64_t s = c->eps_step[i];
-    if (s > (int64_t)step && s <= (int64_t)step + ahead) continue;
+    if (s > (int64_t)step && s <= (int64_t)step + 2) continue;
     return i;
   }
   return -1;
 }
 
-// After the rollout of `step` (which reads slot `used`) is enqueued: make sure the normals
-// of steps step + 1 .. step + noise_ahead are generated or in flight, on noise_stream and
-// ordered after this rollout (every earlier reader of a reused slot precedes it on the
-// context stream).  In steady state that is one launch, of step + 2's normals, which then
-// has the finish, the host round trip and the whole next step to complete, so the next
-// rollout never waits for it (with one step ahead it raced the finish: profiles/r01_notes.md).
-// The noise workgroups run on the CUs the rollout kernel has released.
-int speculate_eps(mppi_ctx* c, const Plan& pl, uint64_t step, int used) {
+// After the rollout of `step` (which reads slot `used`) is enqueued or commanded: make sure the
+// normals of steps step + 1 and step + 2 are generated or in flight, on noise_stream.  In steady
+// state that is one launch, of step + 2's normals, which then has the finish, the host round trip
+// and the whole next step to complete, so no rollout waits for it.  It is ordered after the current
+// rollout (gate: a wait on the stream's event `after`, or a gate kernel polling *gate_sig for
+// gate_seq, the server's rollout-done word), so its workgroups run beside the finish and the next
+// rollout rather than this one.  A missing step + 1 (first steps, a step counter that jumped) is
+// generated at once.  Every earlier reader of a reused slot has completed (server) or precedes the
+// gate on the context stream.
+int speculate_eps(mppi_ctx* c, const Plan& pl, uint64_t step, int used, hipEvent_t after, const unsigned* gate_sig,
+                  unsigned gate_seq) {
   const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
-  bool waited = false;
-  for (int d = 1; d <= c->noise_ahead; ++d) {
+  bool gated = false;
+  for (int d = 1; d <= 2; ++d) {
     const uint64_t target = step + (uint64_t)d;
     bool have = false;
     for (int i = 0; i < kEpsSlots; ++i) have |= c->eps_step[i] == (int64_t)target;
     if (have) continue;
-    const int slot = eps_victim(c, used, step, c->noise_ahead);
+    const int slot = eps_victim(c, used, step);
     if (slot < 0) return fail(MPPI_ESTATE, "no free noise slot");
-    if (!waited) {
-      HIP_TRY(hipStreamWaitEvent(c->noise_stream, c->ev_prev_roll, 0));
-      waited = true;
+    if (!gated && (d == 2 || after)) {
+      if (after) HIP_TRY(hipStreamWaitEvent(c->noise_stream, after, 0));
+      else HIP_TRY(launch_gate(gate_sig, gate_seq, c->fin_wait_ticks, c->noise_stream));
+      gated = true;
     }
-    HIP_TRY(launch_noise(c->p.seed, target * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[slot],
-                         c->noise_stream, noise_groups(c, pl)));
+    HIP_TRY(launch_noise(c->p.seed, target * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[slot], c->noise_stream,
+                         noise_groups(c)));
     HIP_TRY(hipEventRecord(c->eps_ev[slot], c->noise_stream));
     c->eps_step[slot] = (int64_t)target;
     c->eps_pending[slot] = true;
   }
   return MPPI_OK;
-}
-
-// MPPI_NOISE_AT=1: the normals of the steps ahead are generated after the step's finish
-// rather than beside it, so the finish's serial phase (one wave) shares no SIMD with the
-// noise waves; with two steps of look-ahead the noise still has the host round trip and the
-// whole next rollout (at low priority, beside it) before it is needed.
-int flush_speculation(mppi_ctx* c) {
-  if (!c->spec_pending) return MPPI_OK;
-  c->spec_pending = false;
-  HIP_TRY(hipEventRecord(c->ev_prev_roll, c->stream));
-  return speculate_eps(c, c->spec_plan, c->spec_step, c->spec_slot);
 }
 
 // Enqueue the rollout kernel for the current state / nominal sequence.
@@ -709,7 +673,7 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   int rc = ensure_nodes(c, pl.blocks);
   if (rc) return rc;
   const size_t ucount = (size_t)pl.blocks * pl.traj_per_block * 2 * H_of(c);
-  if (ucount > c->ustore_cap) {
+  if (mode == 1 && ucount > c->ustore_cap) {  // injected controls: the leaf reads them back from here
     if (c->ustore) HIP_TRY(hipFree(c->ustore));
     c->ustore = nullptr;
     HIP_TRY(hipMalloc(&c->ustore, ucount * sizeof(float)));
@@ -717,13 +681,9 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   }
   RolloutArgs a;
   fill_rollout(c, pl, st, step, unom, a);
-  a.wave_prio = c->wave_prio;
   int eps_slot = -1;
-  rc = flush_speculation(c);  // a speculation no finish has flushed (dump / injected paths)
-  if (rc) return rc;
-  if (c->trace) c->tr_mark[0] = now_us();
   if (mode == 0 && pl.blocks > 0) {
-    rc = eps_for_step(c, pl, step, &eps_slot);
+    rc = eps_for_step(c, pl, step, c->stream, false, &eps_slot);
     if (rc) return rc;
     a.eps = c->eps[eps_slot];
   }
@@ -739,46 +699,21 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   }
   if (pl.blocks == 0) return MPPI_OK;
   if (c->timing && !dump_args) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-  if (c->trace) c->tr_mark[1] = now_us();
   HIP_TRY(launch_rollout_pair(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr, pl.roles));
-  if (c->trace) c->tr_mark[2] = now_us();
   if (c->timing && !dump_args) {
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     c->ev_roll_pending = true;
   }
-  if (c->noise_at == 2) {
-    // MPPI_NOISE_AT=2: the steps ahead go to the noise stream ordered after the PREVIOUS
-    // rollout only (the last reader of a reused slot; ev_prev_roll still marks it here), so
-    // the noise kernel runs beside this rollout, in its idle issue slots, instead of beside
-    // the finish.  The host calls come after the rollout launch (they are not on its path).
-    bool spec_done = false;
-    if (eps_slot >= 0 && !dump_args && c->prev_roll_valid) {
-      rc = speculate_eps(c, pl, step, eps_slot);
-      if (rc) return rc;
-      spec_done = true;
-    }
-    HIP_TRY(hipEventRecord(c->ev_prev_roll, c->stream));  // the last reader for the next call
-    c->prev_roll_valid = true;
-    if (spec_done) return MPPI_OK;
-  }
-  if (eps_slot >= 0 && !dump_args) {
-    // the next steps' normals on the noise stream after this rollout
-    if (c->noise_at == 1) {  // ... after the finish the caller enqueues next (flush_speculation)
-      c->spec_pending = true;
-      c->spec_plan = pl;
-      c->spec_step = step;
-      c->spec_slot = eps_slot;
-      return MPPI_OK;
-    }
+  if (eps_slot >= 0 && !dump_args) {  // the next steps' normals on the noise stream after this rollout
     HIP_TRY(hipEventRecord(c->ev_prev_roll, c->stream));
-    return speculate_eps(c, pl, step, eps_slot);
+    return speculate_eps(c, pl, step, eps_slot, c->ev_prev_roll, nullptr, 0);
   }
   return MPPI_OK;
 }
 
 // Finish arguments for `mode` (0: rank record, 1: finish; 1 becomes 2 with the deferred
 // optimal rollout): claims the completion sequence number and the tail buffers of the
-// next parity, ordering the context stream after the tail that last used them.
+// next slot, ordering the context stream after the tail that last used them.
 int prepare_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, int mode, double* record_out,
                    FinishArgs& f, int& par) {
   fill_finish(c, pl, st, f);
@@ -806,10 +741,13 @@ int prepare_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, int mode, 
   return MPPI_OK;
 }
 
-// The deferred optimal rollout on the side stream, after what the context stream holds.
+// The deferred optimal rollout on the side stream: after the context stream's finish (event), or,
+// for the resident server, behind the in-kernel gate on fin_done (f.gate).
 int enqueue_tail(mppi_ctx* c, const FinishArgs& f, int par) {
-  HIP_TRY(hipEventRecord(c->ev_fin_done, c->stream));
-  HIP_TRY(hipStreamWaitEvent(c->tail_stream, c->ev_fin_done, 0));
+  if (!f.gate) {
+    HIP_TRY(hipEventRecord(c->ev_fin_done, c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->tail_stream, c->ev_fin_done, 0));
+  }
   if (c->timing == 1) {  // (collecting waits for the previous tail: mode 2 leaves the tail untimed)
     collect_tail_timing(c);
     HIP_TRY(hipEventRecord(c->ev[4], c->tail_stream));
@@ -845,14 +783,6 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
   int cf_P = 0, cf_ncol = 0, cf_groups = 0;
   size_t cf_lds = 0;
   if (c->colfin && colfin_shape(n, H_of(c), &cf_P, &cf_ncol, &cf_groups, &cf_lds)) {
-    const size_t need = (size_t)E_of(c);  // f.level1 carries the 2H u_opt floats
-    if (c->level1_cap < 1 || c->level1_cap * (size_t)E_of(c) < need) {
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      if (c->level1) HIP_TRY(hipFree(c->level1));
-      c->level1 = nullptr;
-      HIP_TRY(hipMalloc(&c->level1, need * sizeof(double)));
-      c->level1_cap = 1;
-    }
     f.level1 = c->level1;
     f.level1_cnt = c->level1_cnt;
     c->fin_kind = 1;
@@ -911,7 +841,10 @@ void fill_outputs(const float* o, int H, mppi_outputs* out) {
 int copy_outputs(mppi_ctx* c, mppi_outputs* out) {
   const int H = H_of(c);
   int rc = wait_done(c);
-  if (rc) return rc;
+  if (rc) {
+    c->tail_pending = false;  // a failed step's tail (if any) has nothing to merge
+    return rc;
+  }
   if (c->async_tail) {
     // controls + the first optimal-rollout row now; rows 1.. arrive with the tail
     const float* stage = c->stage;
@@ -933,7 +866,7 @@ int copy_outputs(mppi_ctx* c, mppi_outputs* out) {
   }
   std::memcpy(c->out_host, c->stage, (size_t)16 * H * sizeof(float));
   collect_timing(c);
-  c->cur ^= 1;  // the finish kernel wrote the new nominal sequence into u_nom[cur^1]
+  c->cur ^= 1;  // the finish wrote the new nominal sequence into u_nom[cur^1]
   if (out) fill_outputs(c->out_host, H, out);
   return MPPI_OK;
 }
@@ -948,234 +881,137 @@ void remember(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
   c->last_plan = pl;
 }
 
-// The fused step launch (mppi_step_fused_kernel): rollout, column-split finish and the noise of
-// step + noise_ahead in one kernel on the context stream.  Applies to sampled steps of the role-split
-// plan whose records fit the column-split finish and whose LDS fits one workgroup per CU.
-// By default only for synchronous steps (no deferred optimal rollout): there the finish (with the
-// ~50 us serial optimal rollout) covers the noise workgroups.  With the deferred tail the finish is
-// shorter than the noise (~25 us of the whole chip), which the three-launch schedule hides beside the
-// finish, the host round trip and the next rollout instead (measured: 8820 vs 8050 steps/s at C3).
-bool fused_shape(const mppi_ctx* c, const Plan& pl, int mode, int* P, int* ncol, int* groups, size_t* lds) {
-  if (!c->fused || (c->async_tail && c->fused < 2)) return false;
-  if (mode != 0 || !pl.roles || !c->colfin || c->noise_at != 0 || pl.blocks < 1) return false;
+// ---- resident step server (mppi_step_server_kernel) ----
+// Sampled steps of the role-split plan whose records fit the column-split finish in the rollout
+// workgroups (C1-C3).  Per step the host waits (normally not at all) for the step's normals and the
+// tail slot it reuses, writes the command (state, slots, nominal buffer, then seq), launches the
+// server if it is not running, enqueues the noise of step + 2 (gate kernel on roll_done) and the
+// deferred optimal rollout (in-kernel gate on fin_done), and spins on the completion word.  No
+// launch and no kernel boundary on the step's path: the gap between two steps is the host's round
+// trip (completion word seen -> next command) plus one poll of pinned memory.
+bool server_shape(const mppi_ctx* c, const Plan& pl, int mode, int* P, int* ncol, int* groups, size_t* lds) {
+  if (!c->resident || mode != 0 || !pl.roles || !c->colfin || c->timing != 0 || pl.blocks < 1) return false;
   size_t cf_lds = 0;
   // the finish runs in the workgroups holding the last `groups` tickets: at most one per rollout workgroup
   if (!colfin_shape(pl.blocks, H_of(c), P, ncol, groups, &cf_lds, pl.blocks)) return false;
   *lds = std::max({pl.lds_bytes, cf_lds, pl.fin_lds_bytes});
-  return *lds + 64 <= kLdsBytes;  // + the kernel's static ticket words
+  return *lds + 256 <= kLdsBytes;  // + the kernel's static words (command, ticket)
 }
 
-int enqueue_fused(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int ncol, int groups, size_t lds) {
+int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int ncol, int groups, size_t lds) {
   if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
+  const double tq = c->trace ? now_us() : 0.0;
+  // a server idle for more than half its limit may be exiting: stop it and start a fresh one
+  if (c->srv_running && (proj != c->srv_proj || now_us() - c->srv_last_us > 0.5 * (double)c->srv_idle_us))
+    quiesce(c);
+  // (first step: the buffers are allocated before the server holds pointers to them)
+  if (c->srv_running && (c->nodes_cap < (size_t)pl.blocks * E_of(c) || c->eps_cap < (size_t)pl.blocks * 2 * H_of(c) * 256))
+    quiesce(c);
   int rc = ensure_nodes(c, pl.blocks);
   if (rc) return rc;
-  rc = flush_speculation(c);
-  if (rc) return rc;
   int slot = -1;
-  rc = eps_for_step(c, pl, step, &slot);
+  const double te = c->trace ? now_us() : 0.0;
+  rc = eps_for_step(c, pl, step, c->noise_stream, true, &slot);
   if (rc) return rc;
-  RolloutArgs a;
-  fill_rollout(c, pl, c->st, step, c->u_nom[c->cur], a);
-  a.wave_prio = c->wave_prio;
-  a.eps = c->eps[slot];
-  FusedArgs z;
-  std::memset(&z, 0, sizeof(z));
-  // normals of steps step + 1 .. step + noise_ahead.  Steady state: the farthest (step + 2) inside
-  // the launch, on the CUs the rollout releases, beside the finish (MPPI_FUSED_NOISE_GROUPS = 0:
-  // before the launch on the context stream).  Any other missing step (first steps, a jump of the
-  // step counter) is generated before the launch on the context stream.
-  const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
-  const bool gated = c->sig != nullptr;  // MPPI_FUSED_NOISE_GROUPS=-2
-  int gated_slot = -1;
-  uint64_t gated_target = 0;
-  for (int d = 1; d <= c->noise_ahead; ++d) {
-    const uint64_t target = step + (uint64_t)d;
-    bool have = false;
-    for (int i = 0; i < kEpsSlots; ++i) have |= c->eps_step[i] == (int64_t)target;
-    if (have) continue;
-    const bool last = d == c->noise_ahead;
-    const int v = eps_victim(c, slot, step, c->noise_ahead);
-    if (v < 0) return fail(MPPI_ESTATE, "no free noise slot");
-    if (c->eps_pending[v]) {  // a stale speculation still writing the victim slot on the noise stream
-      HIP_TRY(hipStreamWaitEvent(c->stream, c->eps_ev[v], 0));
-      c->eps_pending[v] = false;
+  const double tt = c->trace ? now_us() : 0.0;
+  const int par = (c->tail_par + 1) % kTailSlots;
+  if (c->async_tail && c->tail_inflight[par]) {  // the tail of three steps ago: long done
+    HIP_TRY(hipEventSynchronize(c->ev_tail[par]));
+    c->tail_inflight[par] = false;
+  }
+  const double tc = c->trace ? now_us() : 0.0;
+  const unsigned seq = ++c->seq;
+  c->wait_seq = seq;
+  // the command: every field, then seq (release: the server reads the fields after seeing it)
+  ServerCmd* cmd = c->cmd;
+  ServerCmd d;
+  std::memset(&d, 0, sizeof(d));
+  state_fields(c->p, c->st, d);
+  d.eps_slot = slot;
+  d.cur = c->cur;
+  d.tail_slot = par;
+  d.mode = c->async_tail ? 2 : 1;
+  unsigned* cw = reinterpret_cast<unsigned*>(cmd);
+  const unsigned* dw = reinterpret_cast<const unsigned*>(&d);
+  for (int i = 2; i < kCmdWords; ++i) __atomic_store_n(cw + i, dw[i], __ATOMIC_RELAXED);
+  __atomic_store_n(&cmd->seq, seq, __ATOMIC_RELEASE);
+  if (!c->srv_running) {
+    HIP_TRY(hipMemsetAsync(c->relay, 0, 64 * sizeof(unsigned), c->stream));
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->relay), seq - 1, 1, c->stream));
+    RolloutArgs a;
+    fill_rollout(c, pl, c->st, step, c->u_nom[c->cur], a);
+    ServerArgs z;
+    std::memset(&z, 0, sizeof(z));
+    fill_finish(c, pl, c->st, z.f);
+    z.f.recs = c->nodes;
+    z.f.rec_m = c->rec_m;
+    z.f.n_recs = pl.blocks;
+    z.f.level1 = c->level1;
+    z.f.level1_cnt = c->level1_cnt;
+    z.f.done = c->done;
+    z.f.fin_done = c->sigs + 16;
+    z.nroll = pl.blocks;
+    z.fin_P = P;
+    z.fin_ncol = ncol;
+    z.fin_groups = groups;
+    z.rec_cnt = c->level1_cnt + 16;
+    z.cmd = c->cmd;
+    z.relay = c->relay;
+    z.clk = c->clk;
+    z.roll_done = c->sigs;
+    for (int i = 0; i < kEpsSlots; ++i) z.eps[i] = c->eps[i];
+    z.u_nom[0] = c->u_nom[0];
+    z.u_nom[1] = c->u_nom[1];
+    for (int i = 0; i < kTailSlots; ++i) {
+      z.tail_in[i] = c->tail_in[i];
+      z.tail_out[i] = c->tail_host[i];
     }
-    if (last && gated) {  // after the launch, on the noise stream, gated on its rollout part
-      gated_slot = v;
-      gated_target = target;
-    } else if (last && (c->fused_noise_groups > 0 || c->fused_noise_groups == -1)) {
-      z.noise_eps = c->eps[v];
-      z.noise_n_base = target * nb;
-      z.noise_groups = c->fused_noise_groups > 0 ? c->fused_noise_groups : std::max(c->num_cus - groups, 1);
-    } else {
-      HIP_TRY(launch_noise(c->p.seed, target * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[v], c->stream,
-                           noise_groups(c, pl)));
-    }
-    c->eps_step[v] = (int64_t)target;
+    z.first_seq = seq;
+    z.wait_ticks = c->fin_wait_ticks;
+    z.idle_ticks = c->srv_idle_us * 100;
+    HIP_TRY(launch_step_server(a, z, lds, c->stream, proj));
+    c->srv_running = true;
+    c->srv_proj = proj;
+    ++c->srv_launches;
   }
-  int par = 0;
-  rc = prepare_finish(c, pl, c->st, 1, nullptr, z.f, par);
-  if (rc) return rc;
-  z.f.recs = c->nodes;
-  z.f.rec_m = c->rec_m;
-  z.f.n_recs = pl.blocks;
-  if (c->level1_cap < 1 || c->level1_cap * (size_t)E_of(c) < (size_t)E_of(c)) {
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->level1) HIP_TRY(hipFree(c->level1));
-    c->level1 = nullptr;
-    HIP_TRY(hipMalloc(&c->level1, (size_t)E_of(c) * sizeof(double)));
-    c->level1_cap = 1;
+  c->srv_last_us = now_us();
+  if (c->trace) {
+    c->tr_t1 = c->srv_last_us;
+    c->tr_srv[0] += te - tq + (c->srv_last_us - tc);
+    c->tr_srv[1] += tt - te;
+    c->tr_srv[2] += tc - tt;
   }
-  z.f.level1 = c->level1;
-  z.f.level1_cnt = c->level1_cnt;
-  z.nroll = pl.blocks;
-  z.fin_P = P;
-  z.fin_ncol = ncol;
-  z.fin_groups = groups;
-  z.rec_cnt = c->level1_cnt + 16;
-  z.wait_ticks = c->fused_wait_ticks;
-  if (gated_slot >= 0) {
-    z.roll_done = c->sig;
-    z.roll_seq = ++c->sig_seq;
-  }
+  ++c->srv_steps;
   c->fin_kind = 1;
   c->fin_P = P;
   c->fin_ncol = ncol;
   c->fin_groups = groups;
-  if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-  HIP_TRY(launch_step_fused(a, z, lds, c->stream, proj));
-  if (c->timing) {
-    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-    c->ev_roll_pending = true;
+  // the normals of step + 2 beside this step's finish and the next rollout (gated on roll_done)
+  const double tl = c->trace ? now_us() : 0.0;
+  rc = speculate_eps(c, pl, step, slot, nullptr, c->sigs, seq);
+  if (rc) return rc;
+  if (c->async_tail) {  // rows 1.. of the optimal rollout beside the next step (gated on fin_done)
+    FinishArgs f;
+    fill_finish(c, pl, c->st, f);
+    f.mode = 2;
+    f.seq = seq;
+    f.tail_in = c->tail_in[par];
+    f.tail_out = c->tail_host[par];
+    f.gate = c->sigs + 16;
+    f.gate_seq = seq;
+    rc = enqueue_tail(c, f, par);
+    if (rc) return rc;
   }
-  if (gated_slot >= 0) {
-    HIP_TRY(launch_gate(c->sig, z.roll_seq, c->fused_wait_ticks, c->noise_stream));
-    HIP_TRY(launch_noise(c->p.seed, gated_target * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[gated_slot],
-                         c->noise_stream, noise_groups(c, pl)));
-    HIP_TRY(hipEventRecord(c->eps_ev[gated_slot], c->noise_stream));
-    c->eps_pending[gated_slot] = true;
-  }
-  if (z.f.mode == 2) return enqueue_tail(c, z.f, par);
+  if (c->trace) c->tr_srv[3] += now_us() - tl;
   return MPPI_OK;
 }
 
-// The launches of one step (fused, or rollout + finish + tail), with the current state source.
+// The launches of one step (rollout + finish + tail) outside the server.
 int enqueue_step(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
-  int fP = 0, fcol = 0, fgroups = 0;
-  size_t flds = 0;
-  c->last_fused = fused_shape(c, pl, mode, &fP, &fcol, &fgroups, &flds);
-  if (c->last_fused) {
-    int rc = enqueue_fused(c, proj, step, pl, fP, fcol, fgroups, flds);
-    if (rc) return rc;
-    if (c->trace) c->tr_t1 = now_us();
-    return MPPI_OK;
-  }
   int rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr);
   if (rc) return rc;
   if (c->trace) c->tr_t1 = now_us();
-  rc = enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 1, nullptr, true);
-  if (rc) return rc;
-  return flush_speculation(c);
-}
-
-void book_save(const mppi_ctx* c, Book& b) {
-  b.seq = c->seq;
-  b.wait_seq = c->wait_seq;
-  b.fin_kind = c->fin_kind;
-  b.fin_P = c->fin_P;
-  b.fin_ncol = c->fin_ncol;
-  b.fin_groups = c->fin_groups;
-  b.last_fused = c->last_fused;
-  b.tail_par = c->tail_par;
-  b.tail_pending = c->tail_pending;
-  for (int i = 0; i < kTailSlots; ++i) b.tail_inflight[i] = c->tail_inflight[i];
-}
-
-void book_restore(mppi_ctx* c, const Book& b) {
-  c->seq = b.seq;
-  c->wait_seq = b.wait_seq;
-  c->fin_kind = b.fin_kind;
-  c->fin_P = b.fin_P;
-  c->fin_ncol = b.fin_ncol;
-  c->fin_groups = b.fin_groups;
-  c->last_fused = b.last_fused;
-  c->tail_par = b.tail_par;
-  c->tail_pending = b.tail_pending;
-  for (int i = 0; i < kTailSlots; ++i) c->tail_inflight[i] = b.tail_inflight[i];
-}
-
-// Cancel the armed step (its gate returns, its kernels return at once); the host bookkeeping is
-// already the one before it was armed.
-void disarm(mppi_ctx* c) {
-  if (!c || !c->armed) return;
-  __atomic_store_n(&c->dyn_host->go, c->arm_id | kArmCancel, __ATOMIC_RELEASE);
-  c->armed = false;
-  ++c->arm_cancelled;
-}
-
-// Any call on the context but mppi_step / mppi_set_state / mppi_get_outputs: cancel an armed step,
-// and the next step runs the ordinary way (it may allocate) before arming resumes.
-void quiesce(mppi_ctx* c) {
-  disarm(c);
-  c->arm_ready = false;
-}
-
-// Enqueue sampled step `step` behind the gate, reading the u_nom buffer the step before it writes,
-// then put the bookkeeping back as it was.  Only once the previous sampled step of the same plan
-// has been enqueued (its buffers are allocated: nothing here synchronizes behind the gate).
-int arm_next(mppi_ctx* c, int proj, uint64_t step, const Plan& pl) {
-  if (!c->arm || !c->arm_ready || c->timing || c->trace || c->noise_at != 0 || c->fused_noise_groups == -2 ||
-      !c->dyn_host || pl.blocks < 1)
-    return MPPI_OK;
-  Book pre;
-  book_save(c, pre);
-  unsigned id = (c->arm_id + 1) & kArmIdMask;
-  if (id == 0) id = 1;
-  HIP_TRY(launch_arm_gate(c->dyn_host, c->dyn_dev, c->gate_out, id, c->arm_ticks, c->stream));
-  c->arm_id = id;
-  c->cur ^= 1;
-  c->cur_dyn = c->dyn_dev;
-  const int rc = enqueue_step(c, proj, step, 0, pl);
-  c->cur_dyn = nullptr;
-  c->cur ^= 1;
-  book_save(c, c->arm_post);
-  book_restore(c, pre);
-  if (rc) {  // what was enqueued behind the gate is cancelled
-    __atomic_store_n(&c->dyn_host->go, id | kArmCancel, __ATOMIC_RELEASE);
-    return rc;
-  }
-  c->armed = true;
-  c->arm_proj = proj;
-  c->arm_step = step;
-  return MPPI_OK;
-}
-
-// Take the armed step: its robot state and go word to the gate, then the gate's decision (it is
-// spinning by now: a few microseconds).  false: the gate had expired (run the step the ordinary
-// way; its launches returned at once).
-bool take_armed(mppi_ctx* c) {
-  StepDyn d;
-  std::memset(&d, 0, sizeof(d));
-  dyn_from_state(c->p, c->st, d);
-  unsigned* hw = reinterpret_cast<unsigned*>(c->dyn_host);
-  const unsigned* sw = reinterpret_cast<const unsigned*>(&d);
-  for (int i = 0; i < kDynWords; ++i) __atomic_store_n(hw + i, sw[i], __ATOMIC_RELAXED);
-  __atomic_store_n(&c->dyn_host->go, c->arm_id, __ATOMIC_RELEASE);  // after the state words
-  c->armed = false;
-  const double t0 = now_us();
-  unsigned v;
-  while (((v = __atomic_load_n(c->gate_out, __ATOMIC_ACQUIRE)) & kArmIdMask) != c->arm_id) {
-    // the gate runs once the previous step's launches have retired; bounded by its own expiry
-    if (now_us() - t0 > 2e6) return false;
-    __builtin_ia32_pause();
-  }
-  if (v & kArmCancel) {
-    ++c->arm_expired;
-    return false;
-  }
-  book_restore(c, c->arm_post);
-  ++c->arm_taken;
-  return true;
+  return enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 1, nullptr, true);
 }
 
 int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out) {
@@ -1183,23 +1019,14 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   int rc = check_ready(c);
   if (rc) return rc;
   const Plan pl = make_plan(c);
-  if (c->armed) {
-    if (mode == 0 && proj == c->arm_proj && step == c->arm_step && take_armed(c)) {
-      remember(c, proj, step, mode, pl);
-      rc = arm_next(c, proj, step + 1, pl);  // the step after this one, behind it
-      if (rc) return rc;
-      return copy_outputs(c, out);
-    }
-    disarm(c);
-  }
-  rc = enqueue_step(c, proj, step, mode, pl);
+  int sP = 0, scol = 0, sgroups = 0;
+  size_t slds = 0;
+  const bool resident = server_shape(c, pl, mode, &sP, &scol, &sgroups, &slds);
+  if (!resident) quiesce(c);
+  rc = resident ? server_step(c, proj, step, pl, sP, scol, sgroups, slds) : enqueue_step(c, proj, step, mode, pl);
   if (rc) return rc;
+  c->last_resident = resident;
   remember(c, proj, step, mode, pl);
-  if (mode == 0) {
-    rc = arm_next(c, proj, step + 1, pl);
-    if (rc) return rc;
-    c->arm_ready = true;  // this plan's buffers exist now: the next step may be armed
-  }
   if (!c->trace) return copy_outputs(c, out);
   const double t2 = now_us();
   rc = copy_outputs(c, out);
@@ -1209,10 +1036,6 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
     c->tr_sum[1] += c->tr_t1 - c->tr_t0;
     c->tr_sum[2] += t2 - c->tr_t1;
     c->tr_sum[3] += t3 - t2;
-    c->tr_msum[0] += c->tr_mark[0] - c->tr_t0;
-    c->tr_msum[1] += c->tr_mark[1] - c->tr_mark[0];
-    c->tr_msum[2] += c->tr_mark[2] - c->tr_mark[1];
-    c->tr_msum[3] += c->tr_t1 - c->tr_mark[2];
     ++c->tr_n;
   }
   c->tr_prev_done = t3;
@@ -1347,19 +1170,11 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
       c->num_cus = cus;
   }
+  // runtime environment knobs: MPPI_HOST_TRACE, MPPI_ROLES, MPPI_RESIDENT (and
+  // MPPI_GROUP_RCCL for groups)
   if (const char* e = std::getenv("MPPI_HOST_TRACE")) c->trace = std::atoi(e) != 0;
-  if (const char* e = std::getenv("MPPI_COLFIN")) c->colfin = std::atoi(e) != 0;
-  if (const char* e = std::getenv("MPPI_UCACHE")) c->ucache = std::atoi(e) != 0;
-  if (const char* e = std::getenv("MPPI_NOISE_AHEAD")) c->noise_ahead = std::atoi(e) == 1 ? 1 : 2;
-  if (const char* e = std::getenv("MPPI_NOISE_AT")) c->noise_at = std::min(std::max(std::atoi(e), 0), 2);
-  if (const char* e = std::getenv("MPPI_WAVE_PRIO")) c->wave_prio = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_ROLES")) c->roles = std::atoi(e) != 0;
-  if (const char* e = std::getenv("MPPI_NOISE_GPC")) c->noise_gpc = std::max(std::atoi(e), 0);
-  if (const char* e = std::getenv("MPPI_FUSED")) c->fused = std::min(std::max(std::atoi(e), 0), 2);
-  if (const char* e = std::getenv("MPPI_ARM")) c->arm = std::atoi(e) != 0;
-  if (const char* e = std::getenv("MPPI_FUSED_NOISE_GROUPS")) c->fused_noise_groups = std::max(std::atoi(e), -2);
-  const char* ep = std::getenv("MPPI_STREAM_PRIO");
-  const bool use_prio = !(ep && std::atoi(ep) == 0);
+  if (const char* e = std::getenv("MPPI_RESIDENT")) c->resident = std::atoi(e) != 0;
   const int H = p.num_iterations;
   auto cleanup = [&](int rc) {
     mppi_destroy(c);
@@ -1368,7 +1183,6 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   // the rollout stream outranks the speculative noise stream at dispatch
   if (hipDeviceGetStreamPriorityRange(&c->prio_least, &c->prio_greatest) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipDeviceGetStreamPriorityRange failed"));
-  if (!use_prio) c->prio_least = c->prio_greatest = 0;
   if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, c->prio_greatest) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipStreamCreate failed"));
   c->own_stream = true;
@@ -1378,12 +1192,12 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipHostMalloc(&c->stage, 16 * H * sizeof(float), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&c->done, 64, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->cdiv_bad, sizeof(unsigned)) != hipSuccess ||
-      hipMalloc(&c->level1_cnt, 128) != hipSuccess ||  // [0]: finish handoff, [16]: fused record count
+      hipMalloc(&c->level1_cnt, 128) != hipSuccess ||  // [0]: finish handoff, [16]: the server's record count
       hipMalloc(&c->uopt, (size_t)2 * H * sizeof(unsigned long long)) != hipSuccess ||
-      hipHostMalloc(&c->dyn_host, sizeof(StepDyn), hipHostMallocDefault) != hipSuccess ||
-      hipMalloc(&c->dyn_dev, sizeof(StepDyn)) != hipSuccess ||
-      hipHostMalloc(&c->gate_out, 64, hipHostMallocDefault) != hipSuccess ||
-      hipMalloc(&c->clk, (kClkBase + 2 * kClkBlocks) * sizeof(uint64_t)) != hipSuccess ||
+      hipHostMalloc(&c->cmd, sizeof(ServerCmd), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&c->sigs, 128, hipHostMallocDefault) != hipSuccess ||
+      hipMalloc(&c->relay, 64 * sizeof(unsigned)) != hipSuccess ||
+      hipMalloc(&c->clk, kClkWords * sizeof(uint64_t)) != hipSuccess ||
       hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
       hipMalloc(&c->tail_in[1], 3 * H * sizeof(float)) != hipSuccess ||
@@ -1404,7 +1218,6 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipEventCreateWithFlags(&c->ev_tail[2], hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->tail_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithPriority(&c->noise_stream, hipStreamNonBlocking, c->prio_least) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_roll_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_prev_roll, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->eps_ev[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->eps_ev[1], hipEventDisableTiming) != hipSuccess ||
@@ -1413,15 +1226,11 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   c->out_host = new float[16 * H]();
   std::memset(c->stage, 0, 16 * H * sizeof(float));
   *c->done = 0;
-  std::memset(c->dyn_host, 0, sizeof(StepDyn));
-  std::memset(c->gate_out, 0, 64);
-  if (hipMemset(c->level1_cnt, 0, 128) != hipSuccess || hipMemset(c->uopt, 0, (size_t)2 * H * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(c->dyn_dev, 0, sizeof(StepDyn)) != hipSuccess)
+  std::memset(c->cmd, 0, sizeof(ServerCmd));
+  std::memset(c->sigs, 0, 128);
+  if (hipMemset(c->level1_cnt, 0, 128) != hipSuccess ||
+      hipMemset(c->uopt, 0, (size_t)2 * H * sizeof(unsigned long long)) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
-  if (c->fused_noise_groups == -2 &&
-      (hipMalloc(reinterpret_cast<void**>(&c->sig), 64) != hipSuccess || hipMemset(c->sig, 0, 64) != hipSuccess))
-    return cleanup(fail(MPPI_EHIP, "signal word allocation failed"));
-
   if (hipDeviceSynchronize() != hipSuccess) return cleanup(fail(MPPI_EHIP, "device sync failed"));
   *out = c;
   return MPPI_OK;
@@ -1429,19 +1238,21 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
 
 void mppi_destroy(mppi_ctx* c) {
   if (!c) return;
-  disarm(c);
-  if (c->trace && c->tr_n > 0)
+  quiesce(c);
+  if (c->trace && c->tr_n > 0) {
     std::fprintf(stderr, "mppi host trace (us/step over %ld steps): caller %.1f  enqueue rollout %.1f  "
                  "enqueue rest %.1f  wait+copy %.1f\n", c->tr_n, c->tr_sum[0] / c->tr_n, c->tr_sum[1] / c->tr_n,
                  c->tr_sum[2] / c->tr_n, c->tr_sum[3] / c->tr_n);
-  if (c->trace && c->tr_n > 0)
-    std::fprintf(stderr, "mppi host trace, enqueue rollout (us/step): plan+args %.1f  noise slot %.1f  launch %.1f  "
-                 "events+noise launch %.1f\n", c->tr_msum[0] / c->tr_n, c->tr_msum[1] / c->tr_n,
-                 c->tr_msum[2] / c->tr_n, c->tr_msum[3] / c->tr_n);
+    if (c->srv_steps > 0)
+      std::fprintf(stderr, "mppi host trace, server steps (us/step over %ld): stop+relaunch %.1f  normals wait %.1f  "
+                   "tail slot wait %.1f  noise+tail launches %.1f  (server launches %ld)\n", (long)c->srv_steps,
+                   c->tr_srv[0] / c->srv_steps, c->tr_srv[1] / c->srv_steps, c->tr_srv[2] / c->srv_steps,
+                   c->tr_srv[3] / c->srv_steps, (long)c->srv_launches);
+  }
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->tail_stream) hipStreamSynchronize(c->tail_stream);
-  release_signal(c);
+  release_gates(c);
   if (c->noise_stream) hipStreamSynchronize(c->noise_stream);
   if (c->Z_owned && c->Z) hipFree(c->Z);
   if (c->ntab) hipFree(c->ntab);
@@ -1459,7 +1270,6 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->stage) hipHostFree(c->stage);
   if (c->done) hipHostFree(c->done);
   if (c->cdiv_bad) hipFree(c->cdiv_bad);
-  if (c->sig) hipFree(c->sig);
   delete[] c->out_host;
   for (int i = 0; i < kTailSlots; ++i) {
     if (c->tail_in[i]) hipFree(c->tail_in[i]);
@@ -1471,15 +1281,14 @@ void mppi_destroy(mppi_ctx* c) {
     if (c->eps[i]) hipFree(c->eps[i]);
     if (c->eps_ev[i]) hipEventDestroy(c->eps_ev[i]);
   }
-  if (c->ev_roll_done) hipEventDestroy(c->ev_roll_done);
   if (c->ev_prev_roll) hipEventDestroy(c->ev_prev_roll);
   if (c->bin_tile_of) hipFree(c->bin_tile_of);
   if (c->level1) hipFree(c->level1);
   if (c->level1_cnt) hipFree(c->level1_cnt);
   if (c->uopt) hipFree(c->uopt);
-  if (c->dyn_host) hipHostFree(c->dyn_host);
-  if (c->dyn_dev) hipFree(c->dyn_dev);
-  if (c->gate_out) hipHostFree(c->gate_out);
+  if (c->cmd) hipHostFree(c->cmd);
+  if (c->sigs) hipHostFree(c->sigs);
+  if (c->relay) hipFree(c->relay);
   if (c->clk) hipFree(c->clk);
   if (c->bin_counts) hipFree(c->bin_counts);
   if (c->bin_cursor) hipFree(c->bin_cursor);
@@ -1688,7 +1497,7 @@ int mppi_step_partial(mppi_ctx* c, int32_t proj, uint64_t step, double* record_d
   if (rc) return rc;
   if (!record_dev) return fail(MPPI_EINVAL, "null record buffer");
   const Plan pl = make_plan(c);
-  c->last_fused = false;
+  c->last_resident = false;
   rc = enqueue_rollout(c, proj, step, 0, pl, c->u_nom[c->cur], c->st, nullptr);
   if (rc) return rc;
   remember(c, proj, step, 0, pl);
@@ -1703,8 +1512,6 @@ int mppi_step_finish(mppi_ctx* c, const double* records_dev, int32_t n, mppi_out
   if (!records_dev || n < 1) return fail(MPPI_EINVAL, "records required");
   const Plan pl = c->have_last ? c->last_plan : make_plan(c);
   rc = enqueue_finish(c, pl, c->st, records_dev, n, 1, nullptr, true);
-  if (rc) return rc;
-  rc = flush_speculation(c);
   if (rc) return rc;
   return copy_outputs(c, out);
 }
@@ -1765,18 +1572,22 @@ int mppi_set_option(mppi_ctx* c, const char* name, int64_t value) {
   if (!c || !name) return fail(MPPI_EINVAL, "null argument");
   quiesce(c);
   const std::string n(name);
-  if (n == "arm") {  // the armed next step on (1) / off (0)
-    c->arm = value != 0;
+  if (n == "resident") {  // the resident step server on (1, default) / off (0: one launch per kernel)
+    c->resident = value != 0;
     return MPPI_OK;
   }
-  if (n == "arm_wait_us") {  // how long an armed step's gate waits for the next call
-    if (value < 1 || value > 10000000) return fail(MPPI_EINVAL, "arm_wait_us must be in [1, 1e7]");
-    c->arm_ticks = (uint64_t)value * 100;
+  if (n == "resident_idle_us") {  // how long an idle server stays resident
+    if (value < 100 || value > 1000000) return fail(MPPI_EINVAL, "resident_idle_us must be in [100, 1e6]");
+    c->srv_idle_us = (uint64_t)value;
     return MPPI_OK;
   }
-  if (n == "fused_wait_ticks") {
-    if (value < 0) return fail(MPPI_EINVAL, "fused_wait_ticks must be >= 0");
-    c->fused_wait_ticks = (uint64_t)value;
+  if (n == "record_tree_finish") {  // 1: the record-tree finish (mppi_finish_kernel) at any record count
+    c->colfin = value == 0;
+    return MPPI_OK;
+  }
+  if (n == "finish_wait_ticks") {  // the server finish's record wait bound (100 MHz ticks; 0: give up at once)
+    if (value < 0) return fail(MPPI_EINVAL, "finish_wait_ticks must be >= 0");
+    c->fin_wait_ticks = (uint64_t)value;
     return MPPI_OK;
   }
   return fail(MPPI_EINVAL, "unknown option '" + n + "'");
@@ -1836,7 +1647,7 @@ int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
   quiesce(c);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  std::vector<uint64_t> all((size_t)kClkBase + 2 * kClkBlocks, 0);
+  std::vector<uint64_t> all((size_t)kClkWords, 0);
   HIP_TRY(hipMemcpy(all.data(), c->clk, all.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
   const uint64_t* v = all.data();
   // per-workgroup start / end of the last role-split rollout (its plan's blocks)
@@ -1865,6 +1676,12 @@ int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
   // then, per workgroup b, the time from the first workgroup start to b's record (microseconds)
   for (int b = 0; b < nb && 10 + b < n; ++b)
     out[10 + b] = wg_ok ? (double)(v[kClkBase + 2 * b + 1] - s_lo) / 100.0 : 0.0;
+  // then (resident server) microseconds from workgroup 0's poll start to: the command seen, the last
+  // rollout ticket, the completion word
+  for (int k = 0; k < 3 && 10 + nb + k < n; ++k) {
+    const uint64_t p0 = v[kClkServer + 3], pk = v[kClkServer + k];
+    out[10 + nb + k] = p0 && pk >= p0 ? (double)(pk - p0) / 100.0 : 0.0;
+  }
   return MPPI_OK;
 }
 
@@ -1872,8 +1689,8 @@ int mppi_get_launch_info(mppi_ctx* c, int64_t* info, int32_t n) {
   if (!c || !info) return fail(MPPI_EINVAL, "null argument");
   const Plan& pl = c->last_plan;
   const int64_t v[15] = {0, pl.block, pl.blocks, pl.W, pl.Wr, (int64_t)pl.lds_bytes, c->fin_kind,
-                         c->fin_P, c->fin_ncol, c->fin_groups, pl.ucache_steps, c->last_fused ? 1 : 0,
-                         c->arm_taken, c->arm_cancelled, c->arm_expired};
+                         c->fin_P, c->fin_ncol, c->fin_groups, pl.ucache_steps, c->last_resident ? 1 : 0,
+                         c->srv_launches, c->srv_steps, c->srv_failed};
   for (int i = 0; i < n && i < 15; ++i) info[i] = v[i];
   return MPPI_OK;
 }
@@ -1906,6 +1723,12 @@ int mppi_bin_queries(mppi_ctx* c, const float* x, const float* y, int64_t n, flo
   HIP_TRY(hipSetDevice(c->device));
   int32_t nt = 0;
   mppi_bilinear_tiles(c, &nt);
+  // the histogram and scatter kernels keep one counter per tile in LDS: a skinny DEM (one side
+  // under 128 cells) can have more tiles than that holds
+  if ((size_t)nt * sizeof(int) > kLdsBytes - 1024)
+    return fail(MPPI_EINVAL, "bin_queries: " + std::to_string(nt) + " tiles of 128 x 128 cells exceed the LDS "
+                             "histogram (at most " + std::to_string((kLdsBytes - 1024) / sizeof(int)) +
+                             "); use mppi_bilinear_query for this DEM");
   const size_t hist = (size_t)bin_chunks(n, nt) * nt;  // [chunks][tiles] per-chunk histograms
   if (std::max<size_t>(hist, 1) > c->bin_n_cap) {
     if (c->bin_tile_of) HIP_TRY(hipFree(c->bin_tile_of));
@@ -2239,9 +2062,7 @@ int group_finish(mppi_group* g, int i, mppi_outputs* out) {
   mppi_ctx* c = g->ctx[i];
   HIP_TRY(hipSetDevice(g->dev[i]));
   const Plan pl = c->have_last ? c->last_plan : make_plan(c);
-  int rc = enqueue_finish(c, pl, c->st, g->gathered[i], g->n, 1, nullptr, true);
-  if (rc) return rc;
-  rc = flush_speculation(c);
+  const int rc = enqueue_finish(c, pl, c->st, g->gathered[i], g->n, 1, nullptr, true);
   if (rc) return rc;
   return copy_outputs(c, out);
 }
@@ -2256,12 +2077,20 @@ int group_member_step(mppi_group* g, int i) {
     while (g->recorded.load(std::memory_order_acquire) < g->n) __builtin_ia32_pause();
     if (rc) return rc;
     rc = group_copy_in(g, i);
-  } else if (rc == MPPI_OK) {
+  } else {
+    // every member enqueues its all-gather, also after a failed partial step (its record buffer
+    // exists): the collective needs every rank, and a missing one would leave the other members'
+    // gathers, finishes and completion waits pending (the step fails on this member's error)
     std::string why;
     const RcclApi* api = rccl_api(why);
     if (!api) return fail(MPPI_EHIP, "group: " + why);
+    const std::string saved = g_err;
     const ncclResult_t r = api->all_gather(g->rec[i], g->gathered[i], (size_t)g->E, ncclFloat64, g->comm[i],
                                            g->ctx[i]->stream);
+    if (rc) {
+      g_err = saved;
+      return rc;
+    }
     if (r != ncclSuccess)
       return fail(MPPI_EHIP, std::string("group: ncclAllGather: ") + (api->error_string ? api->error_string(r) : "error"));
   }
@@ -2383,9 +2212,8 @@ int mppi_group_create(const mppi_params* params, int32_t n, const int32_t* devic
     }
     g->use_rccl = true;
   }
-  // member threads (MPPI_GROUP_THREADS=0: every member enqueued from the caller's thread)
-  const char* et = std::getenv("MPPI_GROUP_THREADS");
-  g->threaded = n > 1 && !(et && std::atoi(et) == 0);
+  // member threads (n > 1): every member enqueues its own step
+  g->threaded = n > 1;
   g->rc.assign(n, MPPI_OK);
   g->err.assign(n, std::string());
   if (g->threaded) {
@@ -2495,9 +2323,7 @@ int mppi_group_step(mppi_group* g, int32_t proj, uint64_t step, mppi_outputs* ou
     mppi_ctx* c = g->ctx[i];
     HIP_TRY(hipSetDevice(g->dev[i]));
     const Plan pl = c->have_last ? c->last_plan : make_plan(c);
-    int rc = enqueue_finish(c, pl, c->st, g->gathered[i], n, 1, nullptr, true);
-    if (rc) return rc;
-    rc = flush_speculation(c);
+    const int rc = enqueue_finish(c, pl, c->st, g->gathered[i], n, 1, nullptr, true);
     if (rc) return rc;
   }
   for (int i = 0; i < n; ++i) {

@@ -6,19 +6,23 @@
 
 namespace mppi {
 
-// Everything one rollout launch needs, passed by value (uniform per launch).
-// An armed step's robot state (mppi_capi.cpp "armed next step"): the host fills it in pinned memory
-// at the step's call, mppi_arm_gate_kernel copies it to device memory ahead of the step's kernels,
-// which read these fields from it instead of their arguments.  go = the arm id, with kArmCancel
-// set when the step was cancelled (its kernels return at once) or expired (kArmExpired too).
-struct StepDyn {
-  float x0, y0, h0x, h0y, h0z, wl, wr, gx, gy, s1, s2, igx, igy, pf_scale;
+// The resident step server's command block (mppi_capi.cpp "resident step server"): pinned host
+// memory the host fills for every step (every field, then seq with release order); the server's
+// workgroups poll seq and read the rest with system-scope loads.  stop != 0 ends the server.
+struct ServerCmd {
+  unsigned seq;    // the step's completion sequence number (written last)
+  unsigned stop;   // (same 8-byte word as seq: one poll reads both)
+  int eps_slot;    // normals slot of the step
+  int cur;         // nominal buffer the step reads (the finish writes the other one)
+  int tail_slot;   // deferred optimal rollout slot (mode 2)
+  int mode;        // 1: finish with the whole optimal rollout, 2: step 0 only (the rest deferred)
+  int pad0[2];
+  float x0, y0, h0x, h0y, h0z, wl, wr, gx, gy, s1, s2, igx, igy, pf_scale;  // robot / goal state
   int pf_far, speed_on;
-  unsigned go;
-  unsigned pad[15];
+  unsigned pad1[8];
 };
-constexpr int kDynWords = 16;  // state words before go
-constexpr unsigned kArmCancel = 0x80000000u, kArmExpired = 0x40000000u, kArmIdMask = 0x3FFFFFFFu;
+constexpr int kCmdWords = 24;                 // the words a step reads (seq .. speed_on)
+constexpr unsigned kDoneFail = 0x80000000u;   // done | kDoneFail: the step's finish gave up
 struct FinishArgs {
   int H;
   int mode;  // 0: write root record, 1: finish (u_opt + optimal rollout),
@@ -26,7 +30,6 @@ struct FinishArgs {
   const double* recs;
   int n_recs;
   const float* rec_m;  // [n_recs] the records' m contiguous, or null (read from recs)
-  const StepDyn* dyn;  // armed step: the state fields from here (null: the arguments)
   unsigned long long* uopt;  // [2H] colfin: the u_opt handoff words {u bits, seq << 32} (zeroed once)
   double* scratch0;
   double* scratch1;
@@ -52,6 +55,11 @@ struct FinishArgs {
   // memory, system scope, release) so the host can spin on it instead of a stream sync
   unsigned* done;
   unsigned seq;
+  // resident server: after `done`, the finish stores seq to *fin_done (its tail inputs are
+  // complete); mppi_tail_kernel with gate != null waits for *gate >= gate_seq before reading them
+  unsigned* fin_done;
+  const unsigned* gate;
+  unsigned gate_seq;
   // multi-workgroup first tree level (launch_finish with groups > 1)
   double* level1;         // [groups][2H+2]
   unsigned* level1_cnt;   // zero-initialised, re-armed in-kernel
@@ -94,7 +102,6 @@ struct RolloutArgs {
   float* cost_out;   // [K]
   double* nodes;     // [blocks][2H+2]
   float* rec_m;      // [blocks] or null: each record's m again, contiguous (the finish's scale table)
-  const StepDyn* dyn; // armed step: the state fields from here (null: the arguments)
   float* ustore;     // [blocks][2][H][block] sampled controls kept for the weighted sum
   // injected controls (MODE 1), trajectory-major [K*H]
   const float* inj_u1;
@@ -113,6 +120,9 @@ struct RolloutArgs {
 // clk layout: [0..8) the stamps above, then (role-split kernel) [kClkBase + 2 b], [.. + 1] =
 // s_memrealtime when workgroup b (< kClkBlocks) starts and when its record is written
 constexpr int kClkBase = 8, kClkBlocks = 4096;
+// then (resident server, last step) s_memrealtime at [kClkServer + k]: 0 workgroup 0 saw the command,
+// 1 the last rollout ticket, 2 the completion word stored, 3 workgroup 0 started polling for it
+constexpr int kClkServer = kClkBase + 2 * kClkBlocks, kClkWords = kClkServer + 8;
 // The finish's phase-2 LDS (finish_phase2): uo[2][PS] v w sin cos[H] chain[12H] out[16H]
 // lr[2][PS] floats, PS = the filter rows' stride (a multiple of 4 floats, >= H + 32 for the
 // filter's read-ahead); the DEM window (LDS finish) starts at fin_phase2_floats(H) floats.
@@ -142,35 +152,36 @@ hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hip
 // workgroup over 1024 threads, one wave per role (chain, producer, wheel, cost) and 64
 // trajectories; rings [D][4 + 4][TB] + cost[TB] + slope[TB] in LDS.
 constexpr int ROLES_WAVES_PER_TRAJ_WAVE = 4;
-// One launch per step (mppi_step_fused_kernel): the role-split rollout's nroll workgroups, then
-// noise_groups workgroups generating the normals of Philox block base noise_n_base into noise_eps
-// (none when noise_groups == 0).  The rollout workgroups holding the last fin_groups tickets of
-// rec_cnt (fin_groups <= nroll) then run the column-split finish (colfin_shape), each after
-// rec_cnt reaches nroll (records written through) or wait_ticks of the 100 MHz clock (then it
-// publishes nothing).  rec_cnt: zeroed, re-armed in-kernel (and by the host after a failed step).
-struct FusedArgs {
+// The resident step server (mppi_step_server_kernel): one workgroup per 256 trajectories of the
+// role-split rollout, resident across steps.  Per step every workgroup waits for cmd->seq to reach
+// the next sequence number (or cmd->stop, or idle_ticks of the 100 MHz clock without a command:
+// then it exits), runs its rollout and writes its record through, and takes a ticket from rec_cnt;
+// the workgroups holding the last fin_groups tickets run the column-split finish (each after rec_cnt
+// reaches nroll, or wait_ticks: then the step publishes done | kDoneFail).  The workgroup taking the
+// last ticket stores seq to *roll_done (pinned: the gate of the noise of a later step).  Only workgroup
+// 0 polls the pinned command (256 workgroups polling host memory cost ~30 us per step, one ~4 us:
+// profiles/ubench/server.hip); it relays the command words and seq / stop through device memory.
+struct ServerArgs {
   FinishArgs f;
   int nroll, fin_P, fin_ncol, fin_groups;
-  unsigned* rec_cnt;
-  float* noise_eps;
-  uint64_t noise_n_base;
-  int noise_groups;
-  uint64_t wait_ticks;
-  // optional: the workgroup taking the last ticket (every record counted, the rollout part done)
-  // stores roll_seq to *roll_done (system scope); a stream memory wait gates the noise of a later
-  // step on it (noise beside the finish, as the three-launch schedule places it)
-  unsigned* roll_done;
-  unsigned roll_seq;
+  unsigned* rec_cnt;          // zeroed, re-armed by the finish
+  const ServerCmd* cmd;       // pinned host memory (polled by workgroup 0 only)
+  unsigned* relay;            // device: [0] seq, [1] stop as relayed by workgroup 0, [16, 16 + kCmdWords) the
+                              // command words (zeroed before the launch)
+  unsigned* roll_done;        // pinned host memory
+  float* eps[3];              // the normals slots
+  float* u_nom[2];            // the nominal double buffer, [2H] each
+  float* tail_in[3];          // deferred optimal rollout inputs per slot (device)
+  float* tail_out[3];         // its outputs per slot (pinned)
+  unsigned first_seq;
+  uint64_t wait_ticks;        // a finish's record wait bound
+  uint64_t idle_ticks;        // exit after this long without a command
+  uint64_t* clk;              // optional: the server stamps [kClkServer, kClkServer + 4) of RolloutArgs::clk
 };
-hipError_t launch_step_fused(const RolloutArgs& a, const FusedArgs& z, size_t lds, hipStream_t st, int proj);
-// one wave on `st` that returns once *sig >= seq (unsigned compare) or after `ticks` of the 100 MHz
-// clock: whatever `st` holds next runs after the fused launch's rollout part
+hipError_t launch_step_server(const RolloutArgs& a, const ServerArgs& z, size_t lds, hipStream_t st, int proj);
+// one wave on `st` that returns once *sig >= seq (wrap-safe compare) or after `ticks` of the 100 MHz
+// clock: whatever `st` holds next runs after the server's rollout part of step seq
 hipError_t launch_gate(const unsigned* sig, unsigned seq, uint64_t ticks, hipStream_t st);
-// The armed next step's gate (one wave on the context stream, ahead of the step's kernels): waits
-// for host->go to carry `id` (the host's go or cancel) for at most `ticks` of the 100 MHz clock,
-// copies the state words to dev, stores the decision to dev->go and to *host_out (pinned).
-hipError_t launch_arm_gate(const StepDyn* host, StepDyn* dev, unsigned* host_out, unsigned id, uint64_t ticks,
-                           hipStream_t st);
 // record tree finish (mppi_finish_kernel): the fallback where the column-split shape does not fit
 hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, int groups = 1);
 // column-split finish: every workgroup builds the pair-scale table and reduces ncol columns
@@ -194,7 +205,8 @@ hipError_t launch_noise(uint64_t seed, uint64_t n_base, int64_t k_offset, int bl
 hipError_t launch_bilinear(const float* Z, int rows, int grid, float x_min, float y_min, float res,
                            const float* xs, const float* ys, float* hs, int64_t n, hipStream_t st);
 // LDS-tiled lookup over queries binned by BIL_TILE x BIL_TILE-cell DEM tile (tile count =
-// ceil(rows/BIL_TILE) * ceil(cols/BIL_TILE) <= 16384 for rows * cols < 2^28).  Binning: G chunks of
+// ceil(rows/BIL_TILE) * ceil(cols/BIL_TILE); the binning keeps one LDS counter per tile, so
+// mppi_bin_queries refuses DEMs with more than ~40 000 tiles, e.g. a skinny 2 x 2^24 grid).  Binning: G chunks of
 // the queries, each one workgroup with an LDS histogram (hist[G][ntiles] scratch), the tile
 // counts' exclusive scan, then the scatter: with <= 4096 tiles and the level-1 scratch (cx, cy, ci
 // [n], bcur [tile rows]) two levels of LDS-sorted runs (by tile row into cx/cy/ci, then by tile),

@@ -846,35 +846,6 @@ __device__ __forceinline__ double pair_apply_sel(const PairScale& ps, double a, 
   return pair_apply_raw(ps, a, b, j);
 }
 
-// ---- armed step: the state fields from the StepDyn block (uniform scalar loads); false when the
-// step was cancelled or expired (every workgroup of the launch then returns at once)
-__device__ __forceinline__ bool dyn_rollout(RolloutArgs& a) {
-  const StepDyn* d = a.dyn;
-  if (!d) return true;
-  if (d->go & kArmCancel) return false;
-  a.x0 = d->x0;
-  a.y0 = d->y0;
-  a.h0x = d->h0x;
-  a.h0y = d->h0y;
-  a.h0z = d->h0z;
-  a.wl = d->wl;
-  a.wr = d->wr;
-  a.gx = d->gx;
-  a.gy = d->gy;
-  a.s1 = d->s1;
-  a.s2 = d->s2;
-  a.igx = d->igx;
-  a.igy = d->igy;
-  a.pf_scale = d->pf_scale;
-  a.pf_far = d->pf_far;
-  a.speed_on = d->speed_on;
-  return true;
-}
-// The finish reads its few state fields where it uses them (a copy of FinishArgs with them replaced
-// costs the fused launch 6 VGPRs): the armed step's block, else the arguments.
-__device__ __forceinline__ bool fin_cancelled(const FinishArgs& f) { return f.dyn && (f.dyn->go & kArmCancel); }
-#define FIN_STATE(f, fld) ((f).dyn ? (f).dyn->fld : (f).fld)
-
 // Subtree over an aligned group of G records (log2 G levels of the binary tree):
 // scales of its G-1 pairs, level by level (ps[0 .. G/2) first), from the members' m.
 template <int G>
@@ -908,32 +879,45 @@ __device__ __forceinline__ double group_apply(const PairScale* ps, const double 
   return cur[0];
 }
 
+// threadIdx.x, and for the resident server (FRESH) laundered through an empty asm once per step: the
+// thread-derived addresses of a step then cannot be hoisted out of the server's step loop and stay
+// live across the whole loop (they raised it from ~96 to ~125 VGPRs); the range stays known.
+template <bool FRESH, int NT = 1024>
+__device__ __forceinline__ int thread_id() {
+  int t = threadIdx.x;
+  if constexpr (FRESH) asm volatile("" : "+v"(t));
+  __builtin_assume(t >= 0 && t < NT);
+  return t;
+}
+
 // LDS row stride (floats) of the pair kernel's control cache: 256 trajectories + one float4 of
 // skew, so the leaf's lanes (one row each) hit different banks
 constexpr int UCACHE_ROW = 256 + 4;
 template <int TB, int NT, bool EPS = false, bool WT = false>
 __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
                                              unsigned char* scratch, const float* ub_block,
-                                             const float* ucache = nullptr, int uc_steps = 0);
+                                             const float* unom = nullptr, const float* ucache = nullptr,
+                                             int uc_steps = 0);
 
 // =====================================================================  leaf records (shared)
 // Softmax leaf records (DEFINED replacement of critics_warp.py:338-376) for the
 // TB trajectories of a workgroup, whose costs are in cost_lds[TB] and sampled
-// controls in ustore rows [2H][TB].  Leaf = 256 trajectories.
+// controls in ustore rows [2H][TB] (EPS: the normals rows, with the nominal sequence at `unom`
+// [2H] in LDS and the first uc_steps steps' sampled controls at `ucache`).  Leaf = 256 trajectories.
 //   m = leaf min, w = dm_expf(-(c - m)/T),
 //   record [m, S, V1[H], V2[H]], each sum over the leaf's 256 trajectories the
 //   pairwise tree in index order ((x0+x1)+(x2+x3)) + ... (float64);
 // then the workgroup's subtree over its TB/256 leaves (tree_reduce order).
 // Called by all NT threads; `scratch` is LDS of at least
 // TB*4 + TB/64*4 (rounded to 16) + TB/256*(2H+2)*8 bytes.  WT: the record is stored
-// write-through (agent-scope atomic stores) for the finish workgroups of a fused launch.
+// write-through (agent-scope atomic stores) for the finish workgroups of the resident server.
 template <int TB, int NT, bool EPS, bool WT>
 __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
                                              unsigned char* scratch, const float* ub_block,
-                                             const float* ucache, int uc_steps) {
+                                             const float* unom, const float* ucache, int uc_steps) {
   constexpr int NL = TB / 256;
   constexpr int NWL = TB / 64;   // waves' worth of trajectories
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = thread_id<WT, NT>(), lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.H, E = 2 * H + 2;
   float* wbuf = reinterpret_cast<float*>(scratch);                           // [TB]
@@ -989,7 +973,7 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
         const int c = (j - 2) >= H ? 1 : 0;
         const int t = max(j - 2, 0) - c * H;
         const int ti = min(t + 1, H - 1);
-        nom = c ? a.u_nom2[ti] : a.u_nom1[ti];
+        nom = unom[c * H + ti];
         sg = c ? a.s2 : a.s1;
         lo = c ? a.min_u2 : a.min_u1;
         hi = c ? a.max_u2 : a.max_u1;
@@ -1300,7 +1284,6 @@ template <int TB, int PROJ, int MODE, bool DUMP>
 __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const RolloutArgs a_in) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   RolloutArgs a = a_in;
-  if (!dyn_rollout(a)) return;
   constexpr int NT = 2 * TB;
   constexpr int NWC = TB / 64;
   constexpr int D = PAIR_D;
@@ -1351,7 +1334,9 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   // load there would make every wait for it (vmcnt is in order) also wait for the normals
   // prefetched just before it
   if constexpr (MODE == 0)
-    for (int i = tid; i < 2 * H; i += NT) unom_lds[i] = i < H ? a.u_nom1[i] : a.u_nom2[i - H];
+    for (int i = tid; i < 2 * H; i += NT)  // agent-scope: written through by the resident server's finish
+      unom_lds[i] = __hip_atomic_load(i < H ? a.u_nom1 + i : a.u_nom2 + (i - H), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
 
   // ---------------- per-role state
   Traj s;                       // chain
@@ -1659,7 +1644,7 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 #endif
   __syncthreads();
   if constexpr (MODE == 0)  // rows hold the normals; the leaf recomputes the sampled controls
-    leaf_records<TB, NT, true>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB, ucache,
+    leaf_records<TB, NT, true>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB, unom_lds, ucache,
                                a.ucache_steps);
   else
     leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
@@ -1733,7 +1718,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
   float* ucache = reinterpret_cast<float*>(
       smem_raw + ((size_t)(scratch - smem_raw) + ((TB + TB / 64) * 4 + 15) / 16 * 16 +
                   (size_t)(TB / 256) * (2 * a.H + 2) * sizeof(double) + 15) / 16 * 16);
-  const int tid = threadIdx.x;
+  const int tid = thread_id<FUSED, NT>();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int role = wave / NG;
   const int grp = wave - role * NG;
@@ -1762,7 +1747,9 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
   if (clk_any) a.clk[kClkBase + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();  // every workgroup
   if (tid < 4 * NG) flags[tid] = 0;
   if constexpr (MODE == 0)
-    for (int i = tid; i < 2 * H; i += NT) unom_lds[i] = i < H ? a.u_nom1[i] : a.u_nom2[i - H];
+    for (int i = tid; i < 2 * H; i += NT)  // agent-scope: written through by the resident server's finish
+      unom_lds[i] = __hip_atomic_load(i < H ? a.u_nom1 + i : a.u_nom2 + (i - H), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();  // flags and nominal sequence initialised
 
 #ifdef MPPI_STAMPS
@@ -2055,8 +2042,8 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
   }
   __syncthreads();
   if constexpr (MODE == 0)  // rows hold the normals; the leaf recomputes the sampled controls
-    leaf_records<TB, NT, true, FUSED>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB, ucache,
-                                      a.ucache_steps);
+    leaf_records<TB, NT, true, FUSED>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB, unom_lds,
+                                      ucache, a.ucache_steps);
   else
     leaf_records<TB, NT, false, FUSED>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
   if (clk_wg) a.clk[6] = __builtin_amdgcn_s_memrealtime();  // workgroup 0's leaf record written
@@ -2080,7 +2067,6 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
 template <int TB, int PROJ, int MODE, bool DUMP>
 __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const RolloutArgs a_in) {
   RolloutArgs a = a_in;
-  if (!dyn_rollout(a)) return;
   roles_body<TB, PROJ, MODE, DUMP, false>(a, nullptr);
 }
 
@@ -2112,8 +2098,8 @@ __device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>
   const float res_half_neg = (-f.res) / 2.0f;
   const float res_sq = f.res * f.res;
   Traj s;
-  s.x = FIN_STATE(f, x0);
-  s.y = FIN_STATE(f, y0);
+  s.x = f.x0;
+  s.y = f.y0;
   bool unused = false;
   float q[4];
   if (qpre) {  // the corners, loaded when the finish started (same cell: corners<false> of (x0, y0))
@@ -2128,7 +2114,7 @@ __device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>
   const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
   const float nn = sqrtf((vx * vx + vy * vy) + res_sq * res_sq);
   const float nx = vx / nn, ny = vy / nn, nz = res_sq / nn;
-  const float h0x = FIN_STATE(f, h0x), h0y = FIN_STATE(f, h0y), h0z = FIN_STATE(f, h0z);
+  const float h0x = f.h0x, h0y = f.h0y, h0z = f.h0z;
   const float d = (h0x * nx + h0y * ny) + h0z * nz;
   const float tx = h0x - d * nx, ty = h0y - d * ny, tz = h0z - d * nz;
   const float tn = sqrtf((tx * tx + ty * ty) + tz * tz);
@@ -2338,10 +2324,13 @@ __device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem<L
 __device__ __forceinline__ void store_out(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Every wave's stores (outputs, nominal sequence, tail inputs; all write-through) complete, then the
+// completion word and, for a resident server's gated tail, fin_done.
 __device__ __forceinline__ void signal_done(const FinishArgs& f) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0 && f.done) __hip_atomic_store(f.done, f.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0 && f.fin_done) __hip_atomic_store(f.fin_done, f.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Phase 2 of the finish (MPPI_isaac.py:655-720): `ures` = u_opt[tid] for tid < 2H
@@ -2370,7 +2359,8 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
   const int nout = f.mode == 2 ? 4 * H + 12 : 16 * H;
   const float one_m_a = 1.0f - f.oa;
   if (tid < 2 * H) {
-    f.u_nom_next[tid] = ures;
+    // written through (agent scope): the resident server's next step reads it in the same launch
+    __hip_atomic_store(f.u_nom_next + tid, ures, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ostage[tid] = ures;
     // optimal-sequence wheel filter (sampling_warp.py:120-138, k=3.0, a=0.92): the
     // inputs (u*k)*(1-a) in parallel, only the recurrences L = L*a + in on two lanes
@@ -2405,7 +2395,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
       const f4* p = reinterpret_cast<const f4*>(uo + lane * PS);
       f4* q = reinterpret_cast<f4*>(lrp + lane * PS);
       const float a = f.oa;
-      float x = lane ? FIN_STATE(f, wr) : FIN_STATE(f, wl);
+      float x = lane ? f.wr : f.wl;
       f4 A[4], B[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) A[k] = p[k];
@@ -2461,7 +2451,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
 #endif
   } else if (wave == nthreads / 64 - 1 && f.mode == 2) {
     if (lane == 0) {  // step 0 of the optimal rollout needs only the first filter step
-      const float L0 = FIN_STATE(f, wl) * f.oa + uo[0], R0 = FIN_STATE(f, wr) * f.oa + uo[PS];
+      const float L0 = f.wl * f.oa + uo[0], R0 = f.wr * f.oa + uo[PS];
       const float v0 = clampf((L0 + R0) / 2.0f, f.vmin, f.vmax);
       const float w0 = clampf(((-L0) + R0) / f.rwheel, f.wmin, f.wmax);
       float sn0, cs0;
@@ -2482,10 +2472,10 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
     csb[t] = cs;
     ostage[2 * H + t] = v;
     ostage[3 * H + t] = w;
-    if (f.mode == 2) {  // inputs of the deferred optimal rollout (mppi_tail_kernel)
-      f.tail_in[t] = v;
-      f.tail_in[H + t] = sn;
-      f.tail_in[2 * H + t] = cs;
+    if (f.mode == 2) {  // inputs of the deferred optimal rollout (mppi_tail_kernel), written through
+      __hip_atomic_store(f.tail_in + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(f.tail_in + H + t, sn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(f.tail_in + 2 * H + t, cs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   __syncthreads();
@@ -2509,7 +2499,6 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
 template <bool LDS>
 __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishArgs f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  if (fin_cancelled(f)) return;
 #if MPPI_FIN_PRIO
   __builtin_amdgcn_s_setprio(3);
 #endif
@@ -2733,7 +2722,7 @@ constexpr int COLFIN_PMAX = 4096;
 constexpr uint64_t kColfinPollTicks = 200000000ull;  // the last workgroup's u_opt wait bound (2 s)  // leaf records (K <= 1,048,576 per context)
 __device__ __forceinline__ int colfin_level_base(int P, int l) { return P - (P >> l); }
 
-// Records written by this launch's own rollout blocks (fused launch, RECS_WT) are read with
+// Records written by this launch's own rollout blocks (resident server, RECS_WT) are read with
 // agent-scope atomic loads: they bypass a stale line of the previous step's records in this XCD's
 // L2 (the rollout blocks store them write-through).
 template <bool RECS_WT, typename V>
@@ -2743,9 +2732,10 @@ __device__ __forceinline__ V rec_load(const V* p) {
 }
 
 // The column-split finish of workgroup `blk` of `nblk` (mppi_colfin_kernel, or the finish
-// workgroups of a fused launch, which also re-arm the fused launch's record counter).
+// workgroups of the resident server, which also re-arm its record counter).  false: the last
+// workgroup gave up waiting for a slice and published nothing.
 template <bool RECS_WT>
-__device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol, int blk, int nblk,
+__device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol, int blk, int nblk,
                                             unsigned* rec_cnt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
 #if MPPI_FIN_PRIO
@@ -2754,7 +2744,7 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
 #ifdef MPPI_STAMPS
   if (blk == 0) FIN_STAMP(0);
 #endif
-  const int tid = threadIdx.x;
+  const int tid = thread_id<RECS_WT, FIN_THREADS>();
   const int H = f.H;
   const int E = 2 * H + 2;
   const int n = f.n_recs;
@@ -2768,7 +2758,7 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
       Dem<false> d0;
       d0.init(f.Z, nullptr, f.rows, f.grid, 0, 0, 1, 1, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
       bool unused = false;
-      d0.template corners<false>(FIN_STATE(f, x0), FIN_STATE(f, y0), qpre, unused);
+      d0.template corners<false>(f.x0, f.y0, qpre, unused);
     }
   }
   PairScale* lps = reinterpret_cast<PairScale*>(smem_raw);
@@ -2944,12 +2934,12 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
   // root of slot c: part[c * NG]
   if (f.mode == 0) {
     for (int c = tid; c < nc; c += FIN_THREADS) f.record_out[c0 + c] = part[c * NG];
-    return;
+    return true;
   }
   const double S = extra_s ? part[nc * NG] : part[(1 - c0) * NG];
   // u_opt of this slice (columns 2 + t).  One workgroup: straight from its LDS.  Several: each
   // stores its slice as tagged words {u, seq} (agent-scope atomic stores) and only the LAST
-  // workgroup (blk nblk - 1: in a fused launch the one with the last ticket) goes on: it polls the
+  // workgroup (blk nblk - 1: in the server the one with the last ticket) goes on: it polls the
   // 2H words until each carries this step's seq.  Value and tag travel in one 64-bit word, so
   // the handoff orders nothing across locations, and no workgroup waits for its stores to
   // complete or counts itself in (round 2-3's store, vmcnt(0), barrier, counter add, barrier).
@@ -2971,7 +2961,7 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
 #ifdef MPPI_STAMPS
     FINWG_STAMP(blk, 0);
 #endif
-    if (blk != nblk - 1) return;
+    if (blk != nblk - 1) return true;
     int late = 0;
     if (tid < 2 * H) {  // bounded (2 s of the 100 MHz clock): a lost slice cannot hang the device
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -2987,11 +2977,11 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
       ures = __builtin_bit_cast(float, (unsigned)w);
     }
     // a slice that never came: publish nothing (the host's wait reports the step as failed)
-    if (__syncthreads_or(late)) return;
+    if (__syncthreads_or(late)) return false;
 #ifdef MPPI_STAMPS
     FINWG_STAMP(blk, 1);
 #endif
-    // every finish workgroup has passed its record wait (fused launch): re-arm the count
+    // every finish workgroup has passed its record wait (resident server): re-arm the count
     if (RECS_WT && tid == 0) __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #ifdef MPPI_STAMPS
@@ -3003,11 +2993,11 @@ __device__ __forceinline__ void colfin_body(const FinishArgs& f, int P, int ncol
   FIN_STAMP(1);
 #endif
   finish_phase2<false>(f, ures, smem_raw, tid, FIN_THREADS, qpre);
+  return true;
 }
 
 __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishArgs f, int P, int ncol) {
-  if (fin_cancelled(f)) return;
-  colfin_body<false>(f, P, ncol, (int)blockIdx.x, (int)gridDim.x, nullptr);
+  (void)colfin_body<false>(f, P, ncol, (int)blockIdx.x, (int)gridDim.x, nullptr);
 }
 
 // Deferred optimal rollout (MPPI_isaac.py:696-720) of the sequence a mode-2
@@ -3015,14 +3005,32 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_colfin_kernel(const FinishAr
 // next step's rollout kernel.  Bitwise identical to the mode-1 finish.
 __global__ __launch_bounds__(TAIL_THREADS) void mppi_tail_kernel(const FinishArgs f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  if (fin_cancelled(f)) return;
   const int tid = threadIdx.x;
   const int H = f.H;
   float* vb = reinterpret_cast<float*>(smem_raw);
   float* snb = vb + H;
   float* csb = snb + H;
   float* chain = csb + H;
-  for (int i = tid; i < 3 * H; i += TAIL_THREADS) vb[i] = f.tail_in[i];
+  if (f.gate) {  // resident server: launched ahead, waits (bounded, 2 s) for the finish's inputs
+    __shared__ int late;
+    if (tid == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      int lt = 0;
+      while ((int)(__hip_atomic_load(f.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - f.gate_seq) < 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 >= kColfinPollTicks) {
+          lt = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+      }
+      late = lt;
+    }
+    __syncthreads();
+    if (late) return;  // the step failed (the host released the gate or it expired): nothing to roll out
+  }
+  // (agent-scope loads: written through by the finish; an L1 line of an earlier tail could be stale)
+  for (int i = tid; i < 3 * H; i += TAIL_THREADS)
+    vb[i] = __hip_atomic_load(f.tail_in + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   Dem<false> dem;
   dem.init(f.Z, nullptr, f.rows, f.grid, 0, 0, 1, 1, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
@@ -3712,66 +3720,185 @@ __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t
   noise_rows(seed, n_base, k_offset, H, n_blocks, eps, blockIdx.x, gridDim.x, threadIdx.x);
 }
 
-// =====================================================================  fused step launch
-// One launch per MPPI step: workgroups [0, nroll) are the role-split rollout, the rest generate
-// the normals of a later step (noise_rows, four 256-trajectory rows per workgroup).  Each rollout
-// workgroup writes its record through, completes it and takes a ticket from the record counter
-// (its rank among the finished rollout workgroups).  The workgroups holding the last fin_groups
-// tickets stay on as the column-split finish: finish workgroup t - (nroll - fin_groups) waits
-// until all nroll records are counted, reduces its columns, and the last of them runs phase 2
-// and re-arms the counters.  No assumption on the dispatch order: a waiting finish workgroup has
-// finished its own rollout, at most fin_groups - 1 < (workgroup slots of the device) of them wait
-// at once, and every rollout workgroup not yet counted either runs or gets a slot as others
-// retire.  No kernel boundary between rollout and finish, no event between rollout and noise.
-template <int TB, int PROJ>
-__global__ __launch_bounds__(NROLES * TB) void mppi_step_fused_kernel(const RolloutArgs a_in, const FusedArgs z_in) {
-  const int b = (int)blockIdx.x;
-  const FusedArgs& z = z_in;
-  if (b < z.nroll) {  // (a cancelled armed step skips its rollout and finish; the noise below still runs)
-    RolloutArgs a = a_in;
-    if (!dyn_rollout(a)) return;
-    __shared__ int sh[2];
-    const int ticket = roles_body<TB, PROJ, 0, false, true>(a, z.rec_cnt, sh);
-    const int blk = ticket - (z.nroll - z.fin_groups);
-    if (blk < 0) return;
-    if (ticket == z.nroll - 1 && z.roll_done && threadIdx.x == 0)  // every rollout workgroup has counted
-      __hip_atomic_store(z.roll_done, z.roll_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __builtin_amdgcn_s_setprio(0);  // the rollout waves' priorities do not carry into the finish
-    if (threadIdx.x == 0) {  // bounded (z.wait_ticks of the 100 MHz clock): a lost count cannot hang the device
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      int late = z.wait_ticks == 0;  // 0: give up at once (the test hook of mppi_set_option)
-      while (!late && __hip_atomic_load(z.rec_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)z.nroll) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 >= z.wait_ticks) {
-          late = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      sh[1] = late;
-    }
-    __syncthreads();
-    // a finish without all records publishes nothing: the host's wait reports the step as failed
-    // ("finish kernel retired without publishing its outputs") and re-arms the counters
-    if (sh[1]) return;
-#if MPPI_COLFIN_FENCED
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+// =====================================================================  resident step server
+// One launch serves a sequence of sampled steps (mppi_capi.cpp "resident step server"): workgroup b
+// is rollout block b of every step.  Per step: wave 0 polls cmd->seq (one lane, system scope, s_sleep
+// between polls) until it reaches `expect` (or cmd->stop, or idle_ticks without a command: every
+// wave exits), reads the command words into LDS, and the workgroup runs the role-split rollout with
+// the command's state, normals slot and nominal buffer.  Its record is written through and counted
+// (rec_cnt); the workgroup with the last ticket stores seq to *roll_done (the noise gate of a later
+// step); the workgroups holding the last fin_groups tickets run the column-split finish, each after
+// rec_cnt reaches nroll (bounded by wait_ticks: a finish without every record publishes
+// done = seq | kDoneFail).  No assumption on dispatch order or co-residency: a workgroup waits only
+// for records of workgroups that run or get a slot as others reach their wait.
+// Cross-step data: the nominal sequence, the tail inputs and the records are
+// written through and read with agent-scope loads; the normals rows (another kernel's write-through
+// stores) are read with plain loads after this CU's L1 was invalidated at the end of the previous step.
+// Kernel arguments re-read every step: a pointer laundered through an empty asm, so the compiler
+// cannot hoist the (invariant) argument loads out of the step loop and keep them live across it
+// (that raised the kernel from 88 to 128 VGPRs with spills); scalar loads once per step instead.
+struct ServerLaunch {
+  RolloutArgs a;
+  ServerArgs z;
+};
+__device__ __forceinline__ const ServerLaunch* fresh_args() {
+#if __HIP_DEVICE_COMPILE__
+  uint64_t v = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+  asm volatile("" : "+s"(v));
+  // (constant address space, then generic: the loads through it stay scalar kernarg loads)
+  return (const ServerLaunch*)reinterpret_cast<const __attribute__((address_space(4))) ServerLaunch*>(v);
+#else
+  return nullptr;
 #endif
-    colfin_body<true>(z.f, z.fin_P, z.fin_ncol, blk, z.fin_groups, z.rec_cnt);
-    return;
-  }
-  const int nb = (int)gridDim.x - z.nroll;
-  const int sub = threadIdx.x >> 8;  // NROLES * TB / 256 rows in flight per workgroup
-  noise_rows(a_in.seed, z.noise_n_base, a_in.k_offset, a_in.H, z.nroll, z.noise_eps,
-             (int64_t)(b - z.nroll) * (NROLES * TB / 256) + sub, (int64_t)nb * (NROLES * TB / 256),
-             threadIdx.x & 255);
 }
 
-hipError_t launch_step_fused(const RolloutArgs& a, const FusedArgs& z, size_t lds, hipStream_t st, int proj) {
-  const dim3 g((unsigned)(z.nroll + z.noise_groups)), b(NROLES * 256);
+template <int TB, int PROJ>
+__global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const ServerLaunch args) {
+  __shared__ unsigned cmd_lds[32];
+  __shared__ int sh[2];
+  const int tid = threadIdx.x;
+  unsigned expect = args.z.first_seq;
+  for (;;) {
+    const auto* L = fresh_args();
+    const ServerArgs& z = L->z;
+    if (tid < 64) {
+      // workgroup 0 polls the pinned command (seq and stop in one 8-byte read) and relays it: the
+      // command words to relay[16..], then (after they completed) seq / stop to relay[0..1]; the
+      // others poll relay[0..1] in device memory.  An idle workgroup 0 relays a stop.
+      const bool head = blockIdx.x == 0;
+      const unsigned long long* src = head ? reinterpret_cast<const unsigned long long*>(z.cmd)
+                                           : reinterpret_cast<const unsigned long long*>(z.relay);
+      unsigned ok = 0;
+      if (tid == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        if (head && z.clk) z.clk[kClkServer + 3] = t0;
+        for (;;) {
+          const unsigned long long w = head ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                            : __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((int)((unsigned)w - expect) >= 0) {
+            ok = 1;
+            break;
+          }
+          if ((w >> 32) != 0 || __builtin_amdgcn_s_memrealtime() - t0 >= z.idle_ticks) break;
+          if (!head) __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      ok = __builtin_amdgcn_readfirstlane(ok);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler only: the words below after the poll)
+      if (ok && tid < kCmdWords) {
+        unsigned wv;
+        if (head) {
+          wv = __hip_atomic_load(reinterpret_cast<const unsigned*>(z.cmd) + tid, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(z.relay + 16 + tid, wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          wv = __hip_atomic_load(z.relay + 16 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        cmd_lds[tid] = wv;
+      }
+      if (head) {  // the words are written through and complete, then seq (or stop: every workgroup exits)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0) {
+          if (ok)
+            __hip_atomic_store(z.relay, cmd_lds[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            __hip_atomic_store(z.relay + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      if (tid == 0) cmd_lds[31] = ok;
+      if (tid == 0 && head && z.clk) z.clk[kClkServer] = __builtin_amdgcn_s_memrealtime();
+    }
+    __syncthreads();
+    if (!cmd_lds[31]) return;  // stop, or idle: the host relaunches
+    const ServerCmd& c = *reinterpret_cast<const ServerCmd*>(cmd_lds);
+    auto rd = [&](const float& x) __attribute__((always_inline)) {
+      return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
+    };
+    const unsigned seq = __builtin_amdgcn_readfirstlane(c.seq);
+    const int eps_slot = __builtin_amdgcn_readfirstlane(c.eps_slot);
+    const int cur = __builtin_amdgcn_readfirstlane(c.cur);
+    RolloutArgs a = L->a;
+    a.eps = z.eps[eps_slot];
+    a.u_nom1 = z.u_nom[cur];
+    a.u_nom2 = z.u_nom[cur] + a.H;
+    a.x0 = rd(c.x0);
+    a.y0 = rd(c.y0);
+    a.h0x = rd(c.h0x);
+    a.h0y = rd(c.h0y);
+    a.h0z = rd(c.h0z);
+    a.wl = rd(c.wl);
+    a.wr = rd(c.wr);
+    a.gx = rd(c.gx);
+    a.gy = rd(c.gy);
+    a.s1 = rd(c.s1);
+    a.s2 = rd(c.s2);
+    a.igx = rd(c.igx);
+    a.igy = rd(c.igy);
+    a.pf_scale = rd(c.pf_scale);
+    a.pf_far = __builtin_amdgcn_readfirstlane(c.pf_far);
+    a.speed_on = __builtin_amdgcn_readfirstlane(c.speed_on);
+    const int ticket = roles_body<TB, PROJ, 0, false, true>(a, z.rec_cnt, sh);
+    if (ticket == z.nroll - 1 && tid == 0) {  // every rollout workgroup has counted: the noise gate
+      __hip_atomic_store(z.roll_done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (z.clk) z.clk[kClkServer + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    const int blk = ticket - (z.nroll - z.fin_groups);
+    if (blk >= 0) {
+      __builtin_amdgcn_s_setprio(0);  // the rollout waves' priorities do not carry into the finish
+      if (tid == 0) {  // bounded (z.wait_ticks of the 100 MHz clock): a lost count cannot hang the device
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        int late = z.wait_ticks == 0;  // 0: give up at once (the test hook of mppi_set_option)
+        while (!late && __hip_atomic_load(z.rec_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)z.nroll) {
+          if (__builtin_amdgcn_s_memrealtime() - t0 >= z.wait_ticks) {
+            late = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        sh[1] = late;
+      }
+      __syncthreads();
+      bool ok = !sh[1];
+      if (ok) {
+#if MPPI_COLFIN_FENCED
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+        FinishArgs f = z.f;
+        const int mode = __builtin_amdgcn_readfirstlane(c.mode);
+        const int slot = __builtin_amdgcn_readfirstlane(c.tail_slot);
+        f.mode = mode;
+        f.seq = seq;
+        f.u_nom_next = z.u_nom[cur ^ 1];
+        f.tail_in = z.tail_in[slot];
+        f.tail_out = z.tail_out[slot];
+        f.x0 = a.x0;
+        f.y0 = a.y0;
+        f.h0x = a.h0x;
+        f.h0y = a.h0y;
+        f.h0z = a.h0z;
+        f.wl = a.wl;
+        f.wr = a.wr;
+        ok = colfin_body<true>(f, z.fin_P, z.fin_ncol, blk, z.fin_groups, z.rec_cnt);
+        if (ok && blk == z.fin_groups - 1 && tid == 0 && z.clk) z.clk[kClkServer + 2] = __builtin_amdgcn_s_memrealtime();
+      }
+      // a finish that gave up publishes the failure (the host stops the server and re-arms the count)
+      if (!ok && tid == 0)
+        __hip_atomic_store(z.f.done, seq | kDoneFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // this CU's L1 forgets the step's normals rows before a later step reads rewritten ones
+    // (asynchronous: the next poll's wait covers it)
+    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    expect = seq + 1;
+    __syncthreads();  // every wave is done with this step's LDS and command words
+  }
+}
+
+hipError_t launch_step_server(const RolloutArgs& a, const ServerArgs& z, size_t lds, hipStream_t st, int proj) {
+  const dim3 g((unsigned)z.nroll), b(NROLES * 256);
   if (proj == 3)
-    hipLaunchKernelGGL((mppi_step_fused_kernel<256, 3>), g, b, lds, st, a, z);
+    hipLaunchKernelGGL((mppi_step_server_kernel<256, 3>), g, b, lds, st, ServerLaunch{a, z});
   else
-    hipLaunchKernelGGL((mppi_step_fused_kernel<256, 2>), g, b, lds, st, a, z);
+    hipLaunchKernelGGL((mppi_step_server_kernel<256, 2>), g, b, lds, st, ServerLaunch{a, z});
   return hipGetLastError();
 }
 
@@ -3785,39 +3912,6 @@ __global__ __launch_bounds__(64) void mppi_gate_kernel(const unsigned* sig, unsi
 
 hipError_t launch_gate(const unsigned* sig, unsigned seq, uint64_t ticks, hipStream_t st) {
   hipLaunchKernelGGL(mppi_gate_kernel, dim3(1), dim3(64), 0, st, sig, seq, ticks);
-  return hipGetLastError();
-}
-
-__global__ __launch_bounds__(64) void mppi_arm_gate_kernel(const StepDyn* host, StepDyn* dev, unsigned* host_out,
-                                                            unsigned id, uint64_t ticks) {
-  __shared__ unsigned decision;
-  if (threadIdx.x == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    unsigned v = __hip_atomic_load(&host->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    while ((v & kArmIdMask) != id) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 >= ticks) {
-        v = id | kArmCancel | kArmExpired;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      v = __hip_atomic_load(&host->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    decision = v;
-  }
-  __syncthreads();
-  // the host stores the state words, then go (release): read them after go (acquire, system scope)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  const unsigned v = decision;
-  const unsigned* hw = reinterpret_cast<const unsigned*>(host);
-  unsigned* dw = reinterpret_cast<unsigned*>(dev);
-  if (threadIdx.x < kDynWords) dw[threadIdx.x] = __hip_atomic_load(hw + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (threadIdx.x == kDynWords) dw[kDynWords] = v;
-  if (threadIdx.x == 0) __hip_atomic_store(host_out, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-hipError_t launch_arm_gate(const StepDyn* host, StepDyn* dev, unsigned* host_out, unsigned id, uint64_t ticks,
-                           hipStream_t st) {
-  hipLaunchKernelGGL(mppi_arm_gate_kernel, dim3(1), dim3(64), 0, st, host, dev, host_out, id, ticks);
   return hipGetLastError();
 }
 

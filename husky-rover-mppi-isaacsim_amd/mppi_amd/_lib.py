@@ -469,8 +469,8 @@ class Engine:
         info = (C.c_int64 * 15)()
         self._c(self.lib.mppi_get_launch_info(self.ctx, info, 15), "mppi_get_launch_info")
         keys = ("reserved", "block", "blocks", "window_cols", "window_rows", "lds_bytes", "finish_kind",
-                "finish_records", "finish_ncol", "finish_groups", "ucache_steps", "fused",
-                "armed_taken", "armed_cancelled", "armed_expired")
+                "finish_records", "finish_ncol", "finish_groups", "ucache_steps", "resident",
+                "server_launches", "server_steps", "server_failed_steps")
         return dict(zip(keys, [int(v) for v in info]))
 
     def chain_clock(self):

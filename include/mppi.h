@@ -265,33 +265,32 @@ int mppi_dump_rollouts(mppi_ctx* ctx, float* traj, float* heading, float* left_w
  * kernel, measured on the context stream around each launch.  enable: 0 off,
  * 1 rollout, finish and deferred-tail events (the host waits for the stream and
  * for each tail to collect them), 2 rollout events only (no host wait: the
- * pipelined schedule undisturbed; the finish time reads 0).  A synchronous
- * step that ran as ONE fused launch (rollout + finish + optimal rollout,
- * mppi_get_launch_info info[11] = 1) is counted whole as rollout time and
- * adds nothing to the finish time. */
+ * pipelined schedule undisturbed; the finish time reads 0).  While timing is on,
+ * steps run as separate launches (rollout, finish, tail), not on the resident
+ * server, whose per-step kernel time no launch event brackets. */
 int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
 
-/* Per-context tuning and test hooks, by name (MPPI_EINVAL for an unknown name):
- *   "fused_wait_ticks"  bound, in ticks of the 100 MHz s_memrealtime clock, on how long a
- *                       finish workgroup of the fused step launch waits for the rollout
- *                       records (default 2e8 = 2 s).  A finish that gives up publishes
- *                       nothing: the step returns MPPI_EHIP and the counters are re-armed,
- *                       so the next step is correct (0: give up at once, the test hook).
- *   "arm"               0 (default; env MPPI_ARM=1 turns it on) / 1: the armed next step.
- *                       After a sampled mppi_step has enqueued its launches, the launches of
- *                       step + 1 (same projection) are enqueued too, behind a one-wave gate
- *                       kernel that waits for the next mppi_step call to store the robot state
- *                       (mppi_set_state's, read at that call) and a go word in pinned memory;
- *                       that step then starts on the GPU without a host launch on its path.
- *                       Results are bitwise those of the ordinary path.  A call with another
- *                       step number or projection, any other call on the context (except
- *                       mppi_set_state and mppi_get_outputs), or a gate that waited longer than
- *                       "arm_wait_us" cancels it: its kernels return at once and the call runs
- *                       the ordinary way.  A device-wide synchronize right after a step waits
- *                       for the gate to expire (mppi_sync cancels it first).  Off by default:
- *                       on MI355X the gate's extra dependent launch costs more (16.8 us from
- *                       the finish's end to the next rollout) than the host's launch (8.7 us).
- *   "arm_wait_us"       the gate's bound, microseconds (default 500). */
+/* Per-context options and test hooks, by name (MPPI_EINVAL for an unknown name):
+ *   "resident"           1 (default; env MPPI_RESIDENT=0 turns it off) / 0: sampled steps of
+ *                        the role-split plan (K <= 256 x CUs, records that fit the in-kernel
+ *                        finish: C1-C3) run on the resident step server, one launch that stays
+ *                        on the GPU across steps and polls a command block in pinned memory
+ *                        (mppi_step_server_kernel): no launch and no kernel boundary on a
+ *                        step's path.  It leaves after "resident_idle_us" without a step, and
+ *                        every call on the context other than mppi_step / mppi_set_state /
+ *                        mppi_get_outputs / mppi_get_timing stops it first.  While it is
+ *                        resident it holds one workgroup slot and ~154 KB of LDS on every CU:
+ *                        other kernels on the device get the rest of each CU.  Results are
+ *                        bitwise those of the separate launches (0).
+ *   "resident_idle_us"   the server's idle limit, microseconds (default 2000, [100, 1e6]).
+ *   "finish_wait_ticks"  bound, in ticks of the 100 MHz s_memrealtime clock, on how long a
+ *                        finish workgroup of the server waits for the step's rollout records
+ *                        (default 2e8 = 2 s).  A finish that gives up publishes the failure:
+ *                        the step returns MPPI_EHIP, the server is stopped and the counters
+ *                        re-armed, so the next step is correct (0: give up at once, the test
+ *                        hook).
+ *   "record_tree_finish" 1: the record-tree finish (mppi_finish_kernel) at every record count
+ *                        (default 0: the column-split finish wherever its shape fits). */
 int mppi_set_option(mppi_ctx* ctx, const char* name, int64_t value);
 int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_t* launches);
 /* HIP-event time of the deferred optimal-rollout kernels (side stream). */
@@ -302,9 +301,9 @@ int mppi_get_tail_timing(mppi_ctx* ctx, double* tail_ms, int64_t* launches);
  * the DEM window the step's lanes can touch, [5]=rollout LDS bytes, [6]=finish kind (1 =
  * column-split mppi_colfin_kernel, 0 = record tree mppi_finish_kernel), [7]=records padded
  * (column-split) or records (tree), [8]=columns per finish workgroup, [9]=finish workgroups,
- * [10]=steps whose sampled controls the rollout keeps in LDS, [11]=1 if the step ran as one
- * fused launch (mppi_step_fused_kernel), else 0; [12]/[13]/[14] = armed steps taken /
- * cancelled / expired so far (mppi_set_option "arm"). */
+ * [10]=steps whose sampled controls the rollout keeps in LDS, [11]=1 if the step ran on the
+ * resident step server (mppi_step_server_kernel), else 0; [12]/[13]/[14] = server launches /
+ * steps served / failed steps so far (mppi_set_option "resident"). */
 int mppi_get_launch_info(mppi_ctx* ctx, int64_t* info, int32_t n);
 
 /* Shader clock of the last sampled 3D rollout, from the chain wave of trajectories 0..63

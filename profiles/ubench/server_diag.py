@@ -1,0 +1,44 @@
+"""Diagnostic (not part of the product): host-side timing of the resident step server's calls.
+Per step: mppi_step wall time, mppi_get_outputs wall time (waits for the deferred tail), and the
+server launch count, for the deferred-tail and the synchronous modes, C3 (K 65536, H 100)."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "husky-rover-mppi-isaacsim_amd"))
+from mppi_amd import _lib, scene  # noqa: E402
+
+Z, hw, cm = scene.scene_c3()
+H = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+for async_tail in (True, False):
+    eng = _lib.Engine(_lib.make_params(65536, H), 0)
+    eng.set_dem(Z, hw)
+    eng.set_costmap(cm, hw)
+    eng.set_state(_lib.make_state(-60.0, -5.0, (1.0, 0.0, 0.0), goal_x=65.0, goal_y=10.0))
+    eng.set_async_tail(async_tail)
+    rows = []
+    for i in range(12):
+        t0 = time.perf_counter()
+        eng.step("3d", i, copy=False)
+        t1 = time.perf_counter()
+        if i % 3 == 2:
+            eng.outputs()
+        t2 = time.perf_counter()
+        rows.append((i, (t1 - t0) * 1e6, (t2 - t1) * 1e6, eng.launch_info()["server_launches"]))
+    t0 = time.perf_counter()
+    n = 200
+    for i in range(12, 12 + n):
+        eng.step("3d", i, copy=False)
+    eng.outputs()
+    dt = (time.perf_counter() - t0) / n * 1e6
+    info = eng.launch_info()
+    import ctypes as C
+    v = (C.c_double * 269)()
+    eng._c(eng.lib.mppi_get_chain_clock(eng.ctx, v, 269), "mppi_get_chain_clock")
+    print(f"  last step: chain {v[1]:.0f} cyc/step {v[2]:.1f} us, wg0 leaf {v[6]:.1f} us, wg start spread {v[7]:.1f}, "
+          f"end spread {v[8]:.1f}, span {v[9]:.1f} us; server: poll->cmd {v[266]:.1f}, ->last ticket {v[267]:.1f}, "
+          f"->done {v[268]:.1f} us")
+    eng.close()
+    print(f"async_tail={async_tail}: " + "  ".join(f"[{i} step {a:.0f} out {b:.0f} L{l}]" for i, a, b, l in rows))
+    print(f"  {n} back-to-back steps: {dt:.1f} us/step, launches {info['server_launches']}, steps {info['server_steps']}")

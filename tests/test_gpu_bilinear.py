@@ -92,3 +92,18 @@ def test_bin_queries_empty():
     eng.bin_queries(e.data_ptr(), e.data_ptr(), 0, e.data_ptr(), e.data_ptr(), perm.data_ptr(), off.data_ptr())
     assert off.cpu().tolist() == [0, 0]
     eng.close()
+
+
+def test_bin_queries_refuses_skinny_dem():
+    """A skinny DEM (2 x 2^23 cells: 65 536 tiles of 128 x 128) has more tiles than the binning's LDS
+    histogram holds: mppi_bin_queries refuses it with a clear error instead of a failed launch."""
+    import torch
+    Z = np.zeros((2, 1 << 23), np.float32)
+    eng = _engine(Z, 3.2)
+    assert eng.bilinear_tiles() == 65536
+    e = torch.empty(4, device="cuda")
+    perm = torch.empty(4, dtype=torch.int32, device="cuda")
+    off = torch.empty(65537, dtype=torch.int32, device="cuda")
+    with pytest.raises(RuntimeError, match="exceed the LDS histogram"):
+        eng.bin_queries(e.data_ptr(), e.data_ptr(), 4, e.data_ptr(), e.data_ptr(), perm.data_ptr(), off.data_ptr())
+    eng.close()

@@ -1,23 +1,17 @@
-"""GPU: the engine's scheduling variants are bitwise identical to the default path.
+"""GPU: the engine's schedules are bitwise identical to each other.
 
-Each toggle below changes only WHERE or WHEN work runs, never the arithmetic:
-  MPPI_COLFIN=0     finish by the record tree (mppi_finish_kernel) instead of the
-                    column-split kernel
-  MPPI_UCACHE=0     leaf reduction re-reads every normals row instead of the LDS-cached controls
-  MPPI_NOISE_AT=1/2 noise of the steps ahead launched after the finish / beside the rollout
-  MPPI_NOISE_AHEAD=1  normals generated one step ahead instead of two
-  MPPI_ROLES=0/1    the pair rollout kernel / the role-split one at any K
-  MPPI_NOISE_GPC=1  noise grid of one workgroup per CU
-  MPPI_FUSED=0      rollout, finish and noise as three launches instead of the fused step launch
-  MPPI_FUSED=2      the fused launch also with the deferred tail (default: synchronous steps only)
-  MPPI_FUSED_NOISE_GROUPS=0/7/-2  the fused launch's noise before it on the context stream / inside it
-                    on 7 workgroups / after it on the noise stream behind a gate kernel (default:
-                    inside it on one workgroup per CU the finish leaves)
-  MPPI_WAVE_PRIO=0  rollout waves at the default issue priority (no s_setprio)
-The toggles are read when a context is created, so each variant gets its own engine.
+Each variant below changes only WHERE or WHEN work runs, never the arithmetic:
+  resident server (default)  sampled steps of the role-split plan on one resident launch
+                             (mppi_step_server_kernel)
+  "resident" = 0             one launch per kernel: rollout, column-split finish, deferred tail
+  MPPI_ROLES=0 / 1           the pair rollout kernel / the role-split one at any K
+  "record_tree_finish" = 1   the record-tree finish (mppi_finish_kernel) instead of the column split
+and the server's own protocol: idle exit and relaunch, stop by another call, a finish that gives
+up, two contexts taking turns on one device, step counters that jump.
 Sizes: n = 256 leaf records (C3 K) and n = 1024 (C5 K) at a short horizon.
 """
 import os
+import time
 
 import numpy as np
 import pytest
@@ -25,13 +19,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 KEYS = ("u1_opt", "u2_opt", "lin_vel", "ang_vel")
+ALL = KEYS + ("traj_sim", "heading_sim", "left_wheel_sim", "right_wheel_sim")
 
 
-def _run(env, K, H, steps=3, info=None, step_ids=None):
+def _engine(K, H, env=None, opts=None, async_tail=False):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     from mppi_amd import _lib, scene
+    env = env or {}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -42,39 +38,129 @@ def _run(env, K, H, steps=3, info=None, step_ids=None):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+    for k, v in (opts or {}).items():
+        eng.set_option(k, v)
     Z, hw, cm = scene.scene_c3()
     eng.set_dem(Z, hw)
     eng.set_costmap(cm, hw)
     eng.set_state(_lib.make_state(-60.0, -5.0, (1.0, 0.0, 0.0), goal_x=65.0, goal_y=10.0))
+    eng.set_async_tail(async_tail)
+    return eng
+
+
+def _state(i):
+    """A different robot state per step (the closed loop's: pose, heading, wheel speeds, sigmas)."""
+    from mppi_amd import _lib
+    return _lib.make_state(-60.0 + 0.7 * i, -5.0 + 0.3 * i, (1.0, 0.1 * i, 0.0), left_wheel_speed=0.1 * i,
+                           right_wheel_speed=0.15 * i, goal_x=65.0, goal_y=10.0, std_dev_u1=0.25 + 0.05 * i,
+                           std_dev_u2=0.4)
+
+
+def _run(K, H, env=None, opts=None, steps=3, info=None, step_ids=None, async_tail=False, states=False):
+    eng = _engine(K, H, env, opts, async_tail)
     outs = []
-    for i in (step_ids if step_ids is not None else range(steps)):
-        o = eng.step("3d", i)
-        outs.append({k: o[k].copy() for k in KEYS})
-    costs = eng.costs()
-    if info is not None:
-        info.update(eng.launch_info())
-    eng.close()
+    try:
+        for n, i in enumerate(step_ids if step_ids is not None else range(steps)):
+            if states:
+                eng.set_state(_state(n))
+            eng.step("3d", i, copy=False)
+            o = eng.outputs()
+            outs.append({k: o[k].copy() for k in ALL})
+        costs = eng.costs()
+        if info is not None:
+            info.update(eng.launch_info())
+    finally:
+        eng.close()
     return outs, costs
 
 
+def _same(got, ref, tag):
+    (g, gc), (r, rc) = got, ref
+    np.testing.assert_array_equal(gc, rc, err_msg=f"costs {tag}")
+    for i, (a, b) in enumerate(zip(g, r)):
+        for k in ALL:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=f"step {i} {k} {tag}")
+
+
 @pytest.mark.parametrize("K,H", [(65536, 24), (262144, 16)])
-@pytest.mark.parametrize("env", [{"MPPI_COLFIN": "0"}, {"MPPI_UCACHE": "0"}, {"MPPI_NOISE_AT": "1"},
-                                 {"MPPI_NOISE_AT": "2"}, {"MPPI_NOISE_AHEAD": "1"}, {"MPPI_ROLES": "0"},
-                                 {"MPPI_ROLES": "1"}, {"MPPI_NOISE_GPC": "1"}, {"MPPI_FUSED": "0"},
-                                 {"MPPI_FUSED": "2"}, {"MPPI_FUSED_NOISE_GROUPS": "0"},
-                                 {"MPPI_FUSED_NOISE_GROUPS": "7"}, {"MPPI_FUSED_NOISE_GROUPS": "-2"},
-                                 {"MPPI_WAVE_PRIO": "0"}],
-                         ids=["record-tree", "no-ucache", "noise-after-finish", "noise-beside-rollout",
-                              "noise-one-ahead", "pair-kernel", "role-split-kernel", "noise-1-per-cu",
-                              "unfused", "fused-pipelined-too", "fused-noise-separate", "fused-7-noise-groups",
-                              "fused-noise-gated", "no-wave-priority"])
-def test_variant_bitwise_equal(K, H, env):
-    ref, ref_costs = _run({}, K, H)
-    got, got_costs = _run(env, K, H)
-    np.testing.assert_array_equal(got_costs, ref_costs)
-    for i, (a, b) in enumerate(zip(got, ref)):
-        for k in KEYS:
-            np.testing.assert_array_equal(a[k], b[k], err_msg=f"step {i} {k} {env}")
+@pytest.mark.parametrize("variant", ["separate-launches", "pair-kernel", "role-split-kernel", "record-tree"])
+def test_variant_bitwise_equal(K, H, variant):
+    env, opts = {}, {}
+    if variant == "separate-launches":
+        opts = {"resident": 0}
+    elif variant == "pair-kernel":
+        env = {"MPPI_ROLES": "0"}
+    elif variant == "role-split-kernel":
+        env = {"MPPI_ROLES": "1"}
+    else:
+        opts = {"record_tree_finish": 1}
+    i_ref, i_got = {}, {}
+    ref = _run(K, H, info=i_ref)
+    got = _run(K, H, env, opts, info=i_got)
+    _same(got, ref, variant)
+    if K == 65536:  # the default at C3 is the server; at 1024 records the pair kernel, separate launches
+        assert i_ref["resident"] == 1 and i_ref["server_steps"] == 3, i_ref
+    else:
+        assert i_ref["resident"] == 0, i_ref
+    if variant in ("separate-launches", "pair-kernel", "record-tree"):
+        assert i_got["resident"] == 0, i_got
+
+
+@pytest.mark.parametrize("async_tail", [False, True], ids=["sync", "deferred-tail"])
+def test_server_closed_loop_states(async_tail):
+    """A new robot state every step (the command block carries it), with and without the deferred
+    optimal rollout: the server equals the separate launches in every output, incl. the *_sim rows."""
+    i_got = {}
+    ref = _run(65536, 24, opts={"resident": 0}, steps=5, async_tail=async_tail, states=True)
+    got = _run(65536, 24, steps=5, async_tail=async_tail, states=True, info=i_got)
+    _same(got, ref, f"closed loop async={async_tail}")
+    assert i_got["resident"] == 1 and i_got["server_launches"] == 1 and i_got["server_steps"] == 5, i_got
+
+
+def test_server_idle_exit_and_stop():
+    """The server leaves after its idle limit and is relaunched by the next step; a call that stops it
+    (mppi_get_costs) between steps, too.  Every step equals the separate launches."""
+    ref = _run(65536, 24, opts={"resident": 0}, steps=4, async_tail=True)
+    eng = _engine(65536, 24, opts={"resident_idle_us": 200}, async_tail=True)
+    outs = []
+    try:
+        for i in range(4):
+            eng.step("3d", i, copy=False)
+            o = eng.outputs()
+            outs.append({k: o[k].copy() for k in ALL})
+            if i == 1:
+                time.sleep(0.01)      # past the idle limit: the server has exited
+            if i == 2:
+                eng.costs()           # stops the server
+        info = eng.launch_info()
+        costs = eng.costs()
+    finally:
+        eng.close()
+    _same((outs, costs), ref, "idle / stop")
+    assert info["server_launches"] == 3 and info["server_steps"] == 4, info
+
+
+def test_two_contexts_take_turns():
+    """Two contexts on one device stepping alternately, each with its own server: a server waits for
+    the CUs the other's holds until that one's idle exit (at most resident_idle_us).  Both equal
+    their separate-launch runs."""
+    ref_a = _run(65536, 24, opts={"resident": 0}, steps=3)
+    ref_b = _run(32768, 20, opts={"resident": 0}, steps=3)
+    a = _engine(65536, 24, opts={"resident_idle_us": 500})
+    b = _engine(32768, 20, opts={"resident_idle_us": 500})
+    oa, ob = [], []
+    try:
+        for i in range(3):
+            for eng, outs in ((a, oa), (b, ob)):
+                eng.step("3d", i, copy=False)
+                o = eng.outputs()
+                outs.append({k: o[k].copy() for k in ALL})
+        ca, cb = a.costs(), b.costs()
+    finally:
+        a.close()
+        b.close()
+    _same((oa, ca), ref_a, "context a")
+    _same((ob, cb), ref_b, "context b")
 
 
 @pytest.mark.parametrize("K,H", [(1048576, 40), (1048576, 100)])
@@ -83,57 +169,43 @@ def test_column_split_finish_at_4096_records(K, H):
     record-tree fallback where (columns + 1) x (records / 16) exceeds the workgroup (H=100).
     launch_info names the finish that ran; the oracle pins H=100 in test_gpu_headline.py."""
     i_ref, i_got = {}, {}
-    ref, ref_costs = _run({"MPPI_COLFIN": "0"}, K, H, steps=2, info=i_ref)
-    got, got_costs = _run({}, K, H, steps=2, info=i_got)
+    ref = _run(K, H, opts={"record_tree_finish": 1}, steps=2, info=i_ref)
+    got = _run(K, H, steps=2, info=i_got)
     assert i_ref["finish_kind"] == 0 and i_ref["finish_records"] == 4096
     assert i_got["finish_kind"] == (1 if H == 40 else 0), i_got
     if H == 40:
         assert i_got["finish_records"] == 4096 and i_got["finish_ncol"] >= 2
-    np.testing.assert_array_equal(got_costs, ref_costs)
-    for i, (a, b) in enumerate(zip(got, ref)):
-        for k in KEYS:
-            np.testing.assert_array_equal(a[k], b[k], err_msg=f"step {i} {k}")
+    _same(got, ref, "4096 records")
 
 
-@pytest.mark.parametrize("env", [{"MPPI_FUSED": "0"}, {"MPPI_FUSED": "1"}], ids=["unfused", "fused"])
-def test_step_counter_jumps(env):
+@pytest.mark.parametrize("resident", [0, 1], ids=["separate", "server"])
+def test_step_counter_jumps(resident):
     """Step counters that skip and repeat (normals generated out of order, slots reused) give the
-    same results with and without the fused launch."""
+    same results on the server and on separate launches of either rollout kernel."""
     ids = [0, 1, 5, 6, 6, 2]
-    ref, ref_costs = _run({"MPPI_FUSED": "0", "MPPI_ROLES": "0"}, 65536, 24, step_ids=ids)
-    got, got_costs = _run(env, 65536, 24, step_ids=ids)
-    np.testing.assert_array_equal(got_costs, ref_costs)
-    for i, (a, b) in enumerate(zip(got, ref)):
-        for k in KEYS:
-            np.testing.assert_array_equal(a[k], b[k], err_msg=f"call {i} {k} {env}")
+    ref = _run(65536, 24, env={"MPPI_ROLES": "0"}, step_ids=ids, async_tail=True)
+    got = _run(65536, 24, opts={"resident": resident}, step_ids=ids, async_tail=True)
+    _same(got, ref, f"jumps resident={resident}")
 
 
 def test_timing_modes():
     """mppi_set_timing: mode 2 times the rollout only (no host wait), mode 1 also the finish and
-    the deferred tail; other modes are refused."""
-    import torch
-    if not torch.cuda.is_available():
-        pytest.skip("needs a GPU")
-    from mppi_amd import _lib, scene
-    eng = _lib.Engine(_lib.make_params(65536, 24), 0)
-    Z, hw, cm = scene.scene_c3()
-    eng.set_dem(Z, hw)
-    eng.set_costmap(cm, hw)
-    eng.set_state(_lib.make_state(-60.0, -5.0, (1.0, 0.0, 0.0), goal_x=65.0, goal_y=10.0))
+    the deferred tail (both as separate launches: timing is off the server); other modes are
+    refused."""
+    eng = _engine(65536, 24, async_tail=True)
     try:
-        eng.set_async_tail(True)
         eng.set_timing(2)
         for i in range(4):
             eng.step("3d", i, copy=False)
         roll, fin, n = eng.timing()
         assert n == 4 and roll > 0.0 and fin == 0.0
         assert eng.tail_timing()[1] == 0
+        assert eng.launch_info()["resident"] == 0
         eng.set_timing(True)
         for i in range(4, 8):
             eng.step("3d", i, copy=False)
         roll, fin, n = eng.timing()
-        fused = eng.launch_info()["fused"] == 1   # a fused launch times rollout + finish as one kernel
-        assert n == 4 and roll > 0.0 and (fin == 0.0 if fused else fin > 0.0)
+        assert n == 4 and roll > 0.0 and fin > 0.0
         assert eng.tail_timing()[1] >= 3
         with pytest.raises(Exception):
             eng.set_timing(3)
@@ -141,34 +213,24 @@ def test_timing_modes():
         eng.close()
 
 
-def test_fused_finish_gives_up_then_recovers():
-    """A fused finish that stops waiting for the records (mppi_set_option("fused_wait_ticks", 0):
-    give up at once) publishes nothing: the step raises, the host re-arms the record and handoff
-    counters, and the next step is bitwise equal to a fresh context's (the nominal controls were
-    not touched by the failed step)."""
-    import torch
-    if not torch.cuda.is_available():
-        pytest.skip("needs a GPU")
-    from mppi_amd import _lib, scene
-    Z, hw, cm = scene.scene_c3()
-
-    def make():
-        e = _lib.Engine(_lib.make_params(65536, 24), 0)
-        e.set_dem(Z, hw)
-        e.set_costmap(cm, hw)
-        e.set_state(_lib.make_state(-60.0, -5.0, (1.0, 0.0, 0.0), goal_x=65.0, goal_y=10.0))
-        return e
-
-    eng, ref = make(), make()
+def test_server_finish_gives_up_then_recovers():
+    """A server finish that stops waiting for the records (mppi_set_option("finish_wait_ticks", 0):
+    give up at once) publishes the failure: the step raises, the host stops the server and re-arms
+    the record and handoff counters, and the next steps are bitwise equal to a fresh context's (the
+    nominal controls were not touched by the failed step)."""
+    eng, ref = _engine(65536, 24, async_tail=True), _engine(65536, 24, async_tail=True)
     try:
-        eng.set_option("fused_wait_ticks", 0)
-        with pytest.raises(RuntimeError, match="without publishing"):
+        eng.set_option("finish_wait_ticks", 0)
+        with pytest.raises(RuntimeError, match="gave up"):
             eng.step("3d", 0)
-        assert eng.launch_info()["fused"] == 1
-        eng.set_option("fused_wait_ticks", 200000000)
+        info = eng.launch_info()
+        assert info["resident"] == 1 and info["server_failed_steps"] == 1, info
+        eng.set_option("finish_wait_ticks", 200000000)
         for i in (1, 2):
-            a, b = eng.step("3d", i), ref.step("3d", i)
-            for k in KEYS:
+            eng.step("3d", i, copy=False)
+            ref.step("3d", i, copy=False)
+            a, b = eng.outputs(), ref.outputs()
+            for k in ALL:
                 np.testing.assert_array_equal(a[k], b[k], err_msg=f"step {i} {k}")
         np.testing.assert_array_equal(eng.costs(), ref.costs())
         with pytest.raises(RuntimeError, match="unknown option"):
