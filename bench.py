@@ -79,6 +79,7 @@ def parse():
     ap.add_argument("--timed-events", action="store_true",
                     help="record the rollout kernel's HIP events inside the timed region (not a separate pass)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 full-step leg (N=1)")
+    ap.add_argument("--no-shard", action="store_true", help="skip the C4 per-GPU shard leg (N=1)")
     ap.add_argument("--no-costmap", action="store_true", help="skip the obstacle-costmap builder leg")
     ap.add_argument("--no-sync-pass", action="store_true",
                     help="skip the synchronous-mode pass (profiling runs: only the headline schedule's launches)")
@@ -422,6 +423,54 @@ def timed_run(torch, dist, run, proj, warmup, steps, step0, async_tail, kernel_t
     return el
 
 
+def shard_bench(torch, device, proj, steps=200, warmup=20):
+    """One GPU's share of the 8-GPU C4 step: K = 131 072 of the 1 048 576, H = 100,
+    as a K-sharded member runs it: partial step (rollout + the member's record), the record
+    all-gather through RCCL (a one-member C-ABI group with the exchange forced, MPPI_GROUP_RCCL=1:
+    comm init, ncclAllGather on the member's stream), then the finish over the gathered record; the
+    plain one-context step at the same K beside it.  With 8 real ranks the all-gather moves 8
+    records instead of 1 (1.6 KB each)."""
+    from mppi_amd import _lib
+    K, H, scene_fn, start, goal, _ = CONFIGS["c4s8"]
+    Z, hw, cm = get_scene(scene_fn)
+    state = _lib.make_state(start[0], start[1], (1.0, 0.0, 0.0), goal_x=goal[0], goal_y=goal[1])
+    old = os.environ.get("MPPI_GROUP_RCCL")
+    os.environ["MPPI_GROUP_RCCL"] = "1"
+    try:
+        g = _lib.Group(_lib.make_params(K, H), [device])
+    finally:
+        if old is None:
+            os.environ.pop("MPPI_GROUP_RCCL", None)
+        else:
+            os.environ["MPPI_GROUP_RCCL"] = old
+    one = _lib.Engine(_lib.make_params(K, H), device)
+    rec = {"workload": CONFIGS["c4s8"][5] + ": partial step -> 1-rank RCCL all-gather -> finish",
+           "rccl": bool(g.info().get("rccl"))}
+    try:
+        for e in g.members + [one]:
+            e.set_dem(Z, hw)
+            e.set_costmap(cm, hw)
+            e.set_state(state)
+            e.set_async_tail(True)
+        for name, fn in (("sharded", lambda i: g.step(proj, i, copy=False)),
+                         ("plain", lambda i: one.step(proj, i, copy=False))):
+            for i in range(warmup):
+                fn(i)
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            for i in range(steps):
+                fn(warmup + i)
+            g.outputs() if name == "sharded" else one.outputs()
+            torch.cuda.synchronize(device)
+            dt = (time.perf_counter() - t0) / steps
+            rec[f"{name}_ms_per_step"] = round(dt * 1e3, 4)
+            rec[f"{name}_steps_per_s"] = round(1.0 / dt, 2)
+    finally:
+        g.close()
+        one.close()
+    return rec
+
+
 def chain_static(path=os.path.join(ROOT, "profiles", "isa", "chain_count.json")):
     """The chain step's static instruction count (profiles/isa/chain_count.py) if it was taken
     from the current kernel sources, else None."""
@@ -658,6 +707,8 @@ def main():
             r2.close()
             rec["c2"] = {"workload": CONFIGS["c2"][5], "steps_per_s": round(200 / t2, 3),
                          "ms_per_step": round(t2 / 200 * 1e3, 4)}
+        if world == 1 and devices is None and not args.no_shard:
+            rec["c4_shard"] = shard_bench(torch, local_rank, args.proj)
         if world == 1 and devices is None and not args.no_c5 and args.config != "c5":
             r5 = Runner("c5", local_rank, 1, solo=True)
             t5 = timed_run(torch, None, r5, args.proj, 10, 50, 0, not args.sync)

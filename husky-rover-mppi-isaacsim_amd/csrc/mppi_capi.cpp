@@ -46,9 +46,8 @@ int fail(int code, const std::string& msg) {
 
 constexpr size_t kLdsBytes = 160 * 1024;
 constexpr int kEpsSlots = 3;
-// deferred optimal rollouts in flight: the tail of step i may run until the finish of step i + 3
-// is enqueued (beside the next rollout it gets only the issue slots the rollout waves leave)
-constexpr int kTailSlots = 3;
+// (mppi::kTailSlots deferred optimal rollouts in flight: the tail of step i may run until step
+// i + kTailSlots is issued; beside the next rollouts it gets only the issue slots their waves leave)
 
 struct Plan {
   int traj_per_block = 256;
@@ -134,7 +133,6 @@ struct mppi_ctx {
   // step; the host relaunches it when the last command is older than half the idle limit.
   int resident = 1;
   ServerCmd* cmd = nullptr;   // pinned
-  unsigned* sigs = nullptr;   // pinned: [0] roll_done (noise gate), [16] fin_done (tail gate)
   unsigned* relay = nullptr;  // device [64]: workgroup 0's relay of the command (ServerArgs::relay)
   bool srv_running = false;
   int srv_proj = 0;
@@ -142,6 +140,12 @@ struct mppi_ctx {
   uint64_t srv_idle_us = 2000;
   int64_t srv_launches = 0, srv_steps = 0, srv_failed = 0;
   uint64_t fin_wait_ticks = 200000000ull;  // a finish's record wait bound (2 s at 100 MHz; mppi_set_option)
+  int tail_streams = 2;  // server: deferred tails alternating over 2 streams, or on 1 (mppi_set_option "tail_streams")
+  // the server's tail of the last step, launched once its completion word was seen (at the next
+  // step's command, or when its outputs are wanted): no kernel waits on the GPU for its inputs
+  bool tail_deferred = false;
+  FinishArgs tail_def{};
+  int tail_def_par = 0;
   hipEvent_t ev_prev_roll = nullptr;  // recorded after the last rollout that read an eps slot
   // finish: column-split u_opt slice records / first tree level, arrival counter
   double* level1 = nullptr;       // finish kernel first-level records
@@ -494,9 +498,20 @@ void collect_tail_timing(mppi_ctx* c) {
   c->ev_tail_pending = false;
 }
 
+int enqueue_tail(mppi_ctx* c, const FinishArgs& f, int par);
+
+// Launch the server's deferred tail of the last step (its completion word has been seen).
+int flush_tail(mppi_ctx* c) {
+  if (!c->tail_deferred) return MPPI_OK;
+  c->tail_deferred = false;
+  return enqueue_tail(c, c->tail_def, c->tail_def_par);
+}
+
 // Wait until no deferred optimal rollout can still read tail_in or the DEM, and
 // merge the latest one's outputs into out_host[4H, 16H).
 int sync_tail(mppi_ctx* c) {
+  const int rc = flush_tail(c);
+  if (rc) return rc;
   bool any = c->tail_pending;
   for (int i = 0; i < kTailSlots; ++i) any |= c->tail_inflight[i];
   if (!any) return MPPI_OK;
@@ -512,13 +527,7 @@ int sync_tail(mppi_ctx* c) {
   return MPPI_OK;
 }
 
-// The gates of the noise / tail launches waiting on a step that will not publish (failed step,
-// stopped server): open them at the latest sequence number.
-void release_gates(mppi_ctx* c) {
-  if (!c->sigs) return;
-  __atomic_store_n(c->sigs, c->seq, __ATOMIC_RELEASE);
-  __atomic_store_n(c->sigs + 16, c->seq, __ATOMIC_RELEASE);
-}
+
 
 // Stop the resident server (it finishes the step it runs, sees cmd->stop and exits): every call on
 // the context but mppi_step / set_state / get_outputs / get_timing starts with this.
@@ -535,7 +544,6 @@ void quiesce(mppi_ctx* c) {
 // step that did not complete them; no launch of the context may be running.
 void rearm_counters(mppi_ctx* c) {
   if (hipMemsetAsync(c->level1_cnt, 0, 128, c->stream) == hipSuccess) hipStreamSynchronize(c->stream);
-  release_gates(c);
 }
 
 // Spin until the finish has published c->wait_seq (all outputs in pinned host memory).  A finish
@@ -632,19 +640,14 @@ int eps_victim(const mppi_ctx* c, int used, uint64_t step) {
   return -1;
 }
 
-// After the rollout of `step` (which reads slot `used`) is enqueued or commanded: make sure the
-// normals of steps step + 1 and step + 2 are generated or in flight, on noise_stream.  In steady
-// state that is one launch, of step + 2's normals, which then has the finish, the host round trip
-// and the whole next step to complete, so no rollout waits for it.  It is ordered after the current
-// rollout (gate: a wait on the stream's event `after`, or a gate kernel polling *gate_sig for
-// gate_seq, the server's rollout-done word), so its workgroups run beside the finish and the next
-// rollout rather than this one.  A missing step + 1 (first steps, a step counter that jumped) is
-// generated at once.  Every earlier reader of a reused slot has completed (server) or precedes the
-// gate on the context stream.
-int speculate_eps(mppi_ctx* c, const Plan& pl, uint64_t step, int used, hipEvent_t after, const unsigned* gate_sig,
-                  unsigned gate_seq) {
+// After the rollout of `step` (which reads slot `used`) is enqueued: make sure the normals of steps
+// step + 1 and step + 2 are generated or in flight, on noise_stream after the event `after` (recorded
+// after this rollout, the last reader of a reused slot).  In steady state that is one launch, of step
+// + 2's normals, which then has the finish, the host round trip and the whole next step to complete,
+// so no rollout waits for it, and which runs beside the finish and the next rollout, not this one.
+int speculate_eps(mppi_ctx* c, const Plan& pl, uint64_t step, int used, hipEvent_t after) {
   const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
-  bool gated = false;
+  bool waited = false;
   for (int d = 1; d <= 2; ++d) {
     const uint64_t target = step + (uint64_t)d;
     bool have = false;
@@ -652,10 +655,9 @@ int speculate_eps(mppi_ctx* c, const Plan& pl, uint64_t step, int used, hipEvent
     if (have) continue;
     const int slot = eps_victim(c, used, step);
     if (slot < 0) return fail(MPPI_ESTATE, "no free noise slot");
-    if (!gated && (d == 2 || after)) {
-      if (after) HIP_TRY(hipStreamWaitEvent(c->noise_stream, after, 0));
-      else HIP_TRY(launch_gate(gate_sig, gate_seq, c->fin_wait_ticks, c->noise_stream));
-      gated = true;
+    if (!waited) {
+      HIP_TRY(hipStreamWaitEvent(c->noise_stream, after, 0));
+      waited = true;
     }
     HIP_TRY(launch_noise(c->p.seed, target * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[slot], c->noise_stream,
                          noise_groups(c)));
@@ -706,7 +708,7 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   }
   if (eps_slot >= 0 && !dump_args) {  // the next steps' normals on the noise stream after this rollout
     HIP_TRY(hipEventRecord(c->ev_prev_roll, c->stream));
-    return speculate_eps(c, pl, step, eps_slot, c->ev_prev_roll, nullptr, 0);
+    return speculate_eps(c, pl, step, eps_slot, c->ev_prev_roll);
   }
   return MPPI_OK;
 }
@@ -741,23 +743,27 @@ int prepare_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, int mode, 
   return MPPI_OK;
 }
 
-// The deferred optimal rollout on the side stream: after the context stream's finish (event), or,
-// for the resident server, behind the in-kernel gate on fin_done (f.gate).
+// The deferred optimal rollout on a side stream: after the context stream's finish (event), or, for
+// the resident server (its finish has published: f.clk set), at once.  The server's tails alternate
+// over the tail and the noise stream (tail_streams = 2): beside a server workgroup a tail takes
+// about a step period, so two may run at once (each beside its own workgroup).
 int enqueue_tail(mppi_ctx* c, const FinishArgs& f, int par) {
-  if (!f.gate) {
+  const bool server = f.clk != nullptr;
+  hipStream_t ts = (server && c->tail_streams == 2 && (par & 1)) ? c->noise_stream : c->tail_stream;
+  if (!server) {
     HIP_TRY(hipEventRecord(c->ev_fin_done, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->tail_stream, c->ev_fin_done, 0));
   }
   if (c->timing == 1) {  // (collecting waits for the previous tail: mode 2 leaves the tail untimed)
     collect_tail_timing(c);
-    HIP_TRY(hipEventRecord(c->ev[4], c->tail_stream));
+    HIP_TRY(hipEventRecord(c->ev[4], ts));
   }
-  HIP_TRY(launch_tail(f, c->tail_stream));
+  HIP_TRY(launch_tail(f, ts));
   if (c->timing == 1) {
-    HIP_TRY(hipEventRecord(c->ev[5], c->tail_stream));
+    HIP_TRY(hipEventRecord(c->ev[5], ts));
     c->ev_tail_pending = true;
   }
-  HIP_TRY(hipEventRecord(c->ev_tail[par], c->tail_stream));
+  HIP_TRY(hipEventRecord(c->ev_tail[par], ts));
   c->tail_inflight[par] = true;
   c->tail_par = par;
   c->tail_pending = true;
@@ -842,7 +848,8 @@ int copy_outputs(mppi_ctx* c, mppi_outputs* out) {
   const int H = H_of(c);
   int rc = wait_done(c);
   if (rc) {
-    c->tail_pending = false;  // a failed step's tail (if any) has nothing to merge
+    c->tail_pending = false;  // a failed step's tail (if any) has nothing to merge or to launch
+    c->tail_deferred = false;
     return rc;
   }
   if (c->async_tail) {
@@ -884,11 +891,11 @@ void remember(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
 // ---- resident step server (mppi_step_server_kernel) ----
 // Sampled steps of the role-split plan whose records fit the column-split finish in the rollout
 // workgroups (C1-C3).  Per step the host waits (normally not at all) for the step's normals and the
-// tail slot it reuses, writes the command (state, slots, nominal buffer, then seq), launches the
-// server if it is not running, enqueues the noise of step + 2 (gate kernel on roll_done) and the
-// deferred optimal rollout (in-kernel gate on fin_done), and spins on the completion word.  No
-// launch and no kernel boundary on the step's path: the gap between two steps is the host's round
-// trip (completion word seen -> next command) plus one poll of pinned memory.
+// tail slot it reuses, writes the command (state, slots, nominal buffer, the slot for the normals of
+// step + 2 that the server's noise phase generates, then seq), launches the server if it is not
+// running, enqueues the deferred optimal rollout (in-kernel gate on fin_done), and spins on the
+// completion word.  No launch and no kernel boundary on the step's path: the gap between two steps
+// is the host's round trip (completion word seen -> next command) plus one poll of pinned memory.
 bool server_shape(const mppi_ctx* c, const Plan& pl, int mode, int* P, int* ncol, int* groups, size_t* lds) {
   if (!c->resident || mode != 0 || !pl.roles || !c->colfin || c->timing != 0 || pl.blocks < 1) return false;
   size_t cf_lds = 0;
@@ -909,13 +916,43 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
     quiesce(c);
   int rc = ensure_nodes(c, pl.blocks);
   if (rc) return rc;
+  // a step whose normals no slot holds (first step, a jump of the step counter): the server may still
+  // be writing normals of a later step in its last noise phase, so it is stopped before any slot is
+  // regenerated
+  bool have = false;
+  for (int i = 0; i < kEpsSlots; ++i) have |= c->eps_step[i] == (int64_t)step;
+  if (!have) quiesce(c);
   int slot = -1;
   const double te = c->trace ? now_us() : 0.0;
   rc = eps_for_step(c, pl, step, c->noise_stream, true, &slot);
   if (rc) return rc;
+  // normals of step + 1 (normally generated by the previous step's noise phase; else now, on the
+  // noise stream beside this step) and of step + 2 (by this step's noise phase, in the server)
+  const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
+  int noise_slot = -1;
+  for (int d = 1; d <= 2; ++d) {
+    const uint64_t target = step + (uint64_t)d;
+    bool got = false;
+    for (int i = 0; i < kEpsSlots; ++i) got |= c->eps_step[i] == (int64_t)target;
+    if (got) continue;
+    const int v = eps_victim(c, slot, step);
+    if (v < 0) return fail(MPPI_ESTATE, "no free noise slot");
+    if (d == 1) {
+      HIP_TRY(launch_noise(c->p.seed, target * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[v], c->noise_stream,
+                           noise_groups(c)));
+      HIP_TRY(hipEventRecord(c->eps_ev[v], c->noise_stream));
+      c->eps_pending[v] = true;
+    } else {
+      // complete before step + 2 can be commanded: every workgroup ends its noise phase before its
+      // rollout of step + 1, whose records the completion of step + 1 needs
+      noise_slot = v;
+      c->eps_pending[v] = false;
+    }
+    c->eps_step[v] = (int64_t)target;
+  }
   const double tt = c->trace ? now_us() : 0.0;
-  const int par = (c->tail_par + 1) % kTailSlots;
-  if (c->async_tail && c->tail_inflight[par]) {  // the tail of three steps ago: long done
+  const int par = ((c->tail_deferred ? c->tail_def_par : c->tail_par) + 1) % kTailSlots;
+  if (c->async_tail && c->tail_inflight[par]) {  // the tail of kTailSlots steps ago: long done
     HIP_TRY(hipEventSynchronize(c->ev_tail[par]));
     c->tail_inflight[par] = false;
   }
@@ -931,6 +968,9 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   d.cur = c->cur;
   d.tail_slot = par;
   d.mode = c->async_tail ? 2 : 1;
+  d.noise_slot = noise_slot;
+  d.noise_n_base_lo = (unsigned)((step + 2) * nb);
+  d.noise_n_base_hi = (unsigned)(((step + 2) * nb) >> 32);
   unsigned* cw = reinterpret_cast<unsigned*>(cmd);
   const unsigned* dw = reinterpret_cast<const unsigned*>(&d);
   for (int i = 2; i < kCmdWords; ++i) __atomic_store_n(cw + i, dw[i], __ATOMIC_RELAXED);
@@ -949,7 +989,6 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
     z.f.level1 = c->level1;
     z.f.level1_cnt = c->level1_cnt;
     z.f.done = c->done;
-    z.f.fin_done = c->sigs + 16;
     z.nroll = pl.blocks;
     z.fin_P = P;
     z.fin_ncol = ncol;
@@ -958,7 +997,6 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
     z.cmd = c->cmd;
     z.relay = c->relay;
     z.clk = c->clk;
-    z.roll_done = c->sigs;
     for (int i = 0; i < kEpsSlots; ++i) z.eps[i] = c->eps[i];
     z.u_nom[0] = c->u_nom[0];
     z.u_nom[1] = c->u_nom[1];
@@ -986,21 +1024,19 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   c->fin_P = P;
   c->fin_ncol = ncol;
   c->fin_groups = groups;
-  // the normals of step + 2 beside this step's finish and the next rollout (gated on roll_done)
   const double tl = c->trace ? now_us() : 0.0;
-  rc = speculate_eps(c, pl, step, slot, nullptr, c->sigs, seq);
+  rc = flush_tail(c);  // the previous step's tail (its outputs were published before this call)
   if (rc) return rc;
-  if (c->async_tail) {  // rows 1.. of the optimal rollout beside the next step (gated on fin_done)
-    FinishArgs f;
+  if (c->async_tail) {  // rows 1.. of the optimal rollout: launched once this step has published
+    FinishArgs& f = c->tail_def;
     fill_finish(c, pl, c->st, f);
     f.mode = 2;
     f.seq = seq;
     f.tail_in = c->tail_in[par];
     f.tail_out = c->tail_host[par];
-    f.gate = c->sigs + 16;
-    f.gate_seq = seq;
-    rc = enqueue_tail(c, f, par);
-    if (rc) return rc;
+    f.clk = c->clk;
+    c->tail_deferred = true;
+    c->tail_def_par = par;
   }
   if (c->trace) c->tr_srv[3] += now_us() - tl;
   return MPPI_OK;
@@ -1022,7 +1058,11 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   int sP = 0, scol = 0, sgroups = 0;
   size_t slds = 0;
   const bool resident = server_shape(c, pl, mode, &sP, &scol, &sgroups, &slds);
-  if (!resident) quiesce(c);
+  if (!resident) {
+    quiesce(c);
+    rc = flush_tail(c);
+    if (rc) return rc;
+  }
   rc = resident ? server_step(c, proj, step, pl, sP, scol, sgroups, slds) : enqueue_step(c, proj, step, mode, pl);
   if (rc) return rc;
   c->last_resident = resident;
@@ -1195,17 +1235,15 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipMalloc(&c->level1_cnt, 128) != hipSuccess ||  // [0]: finish handoff, [16]: the server's record count
       hipMalloc(&c->uopt, (size_t)2 * H * sizeof(unsigned long long)) != hipSuccess ||
       hipHostMalloc(&c->cmd, sizeof(ServerCmd), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&c->sigs, 128, hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->relay, 64 * sizeof(unsigned)) != hipSuccess ||
       hipMalloc(&c->clk, kClkWords * sizeof(uint64_t)) != hipSuccess ||
-      hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess ||
-      hipMalloc(&c->tail_in[0], 3 * H * sizeof(float)) != hipSuccess ||
-      hipMalloc(&c->tail_in[1], 3 * H * sizeof(float)) != hipSuccess ||
-      hipMalloc(&c->tail_in[2], 3 * H * sizeof(float)) != hipSuccess ||
-      hipHostMalloc(&c->tail_host[0], 12 * H * sizeof(float), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&c->tail_host[1], 12 * H * sizeof(float), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&c->tail_host[2], 12 * H * sizeof(float), hipHostMallocDefault) != hipSuccess)
+      hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "device allocation failed"));
+  for (int i = 0; i < kTailSlots; ++i)
+    if (hipMalloc(&c->tail_in[i], 3 * H * sizeof(float)) != hipSuccess ||
+        hipHostMalloc(&c->tail_host[i], 12 * H * sizeof(float), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_tail[i], hipEventDisableTiming) != hipSuccess)
+      return cleanup(fail(MPPI_EHIP, "tail slot allocation failed"));
   if (hipMemset(c->u_nom[0], 0, 2 * H * sizeof(float)) != hipSuccess ||
       hipMemset(c->u_nom[1], 0, 2 * H * sizeof(float)) != hipSuccess ||
       hipMemset(c->cost, 0, std::max<int64_t>(p.num_trajectories, 1) * sizeof(float)) != hipSuccess)
@@ -1213,9 +1251,6 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(MPPI_EHIP, "hipEventCreate failed"));
   if (hipEventCreateWithFlags(&c->ev_fin_done, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_tail[0], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_tail[1], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_tail[2], hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->tail_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithPriority(&c->noise_stream, hipStreamNonBlocking, c->prio_least) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_prev_roll, hipEventDisableTiming) != hipSuccess ||
@@ -1227,7 +1262,6 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   std::memset(c->stage, 0, 16 * H * sizeof(float));
   *c->done = 0;
   std::memset(c->cmd, 0, sizeof(ServerCmd));
-  std::memset(c->sigs, 0, 128);
   if (hipMemset(c->level1_cnt, 0, 128) != hipSuccess ||
       hipMemset(c->uopt, 0, (size_t)2 * H * sizeof(unsigned long long)) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
@@ -1252,7 +1286,6 @@ void mppi_destroy(mppi_ctx* c) {
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->tail_stream) hipStreamSynchronize(c->tail_stream);
-  release_gates(c);
   if (c->noise_stream) hipStreamSynchronize(c->noise_stream);
   if (c->Z_owned && c->Z) hipFree(c->Z);
   if (c->ntab) hipFree(c->ntab);
@@ -1287,7 +1320,6 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->level1_cnt) hipFree(c->level1_cnt);
   if (c->uopt) hipFree(c->uopt);
   if (c->cmd) hipHostFree(c->cmd);
-  if (c->sigs) hipHostFree(c->sigs);
   if (c->relay) hipFree(c->relay);
   if (c->clk) hipFree(c->clk);
   if (c->bin_counts) hipFree(c->bin_counts);
@@ -1581,6 +1613,11 @@ int mppi_set_option(mppi_ctx* c, const char* name, int64_t value) {
     c->srv_idle_us = (uint64_t)value;
     return MPPI_OK;
   }
+  if (n == "tail_streams") {  // the server's deferred tails on 1 stream or alternating over 2
+    if (value != 1 && value != 2) return fail(MPPI_EINVAL, "tail_streams must be 1 or 2");
+    c->tail_streams = (int)value;
+    return MPPI_OK;
+  }
   if (n == "record_tree_finish") {  // 1: the record-tree finish (mppi_finish_kernel) at any record count
     c->colfin = value == 0;
     return MPPI_OK;
@@ -1676,12 +1713,18 @@ int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
   // then, per workgroup b, the time from the first workgroup start to b's record (microseconds)
   for (int b = 0; b < nb && 10 + b < n; ++b)
     out[10 + b] = wg_ok ? (double)(v[kClkBase + 2 * b + 1] - s_lo) / 100.0 : 0.0;
-  // then (resident server) microseconds from workgroup 0's poll start to: the command seen, the last
-  // rollout ticket, the completion word
-  for (int k = 0; k < 3 && 10 + nb + k < n; ++k) {
-    const uint64_t p0 = v[kClkServer + 3], pk = v[kClkServer + k];
-    out[10 + nb + k] = p0 && pk >= p0 ? (double)(pk - p0) / 100.0 : 0.0;
-  }
+  // then (resident server) the stamps of the last 8 steps (kClkServer ring), microseconds from the
+  // oldest stamp of the ring (0 = not stamped): out[10 + nb + 8 r + k], r = 0..7 in step order
+  uint64_t lo = UINT64_MAX;
+  for (int k = 0; k < 64; ++k)
+    if (v[kClkServer + k]) lo = std::min(lo, v[kClkServer + k]);
+  const int last = (int)(c->seq & 7);
+  for (int r = 0; r < 8; ++r)
+    for (int k = 0; k < 8; ++k) {
+      const int idx = 10 + nb + 8 * r + k;
+      const uint64_t x = v[kClkServer + 8 * ((last + 1 + r) & 7) + k];
+      if (idx < n) out[idx] = x && lo != UINT64_MAX ? (double)(x - lo) / 100.0 : 0.0;
+    }
   return MPPI_OK;
 }
 

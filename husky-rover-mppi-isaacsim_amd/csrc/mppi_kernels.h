@@ -16,12 +16,17 @@ struct ServerCmd {
   int cur;         // nominal buffer the step reads (the finish writes the other one)
   int tail_slot;   // deferred optimal rollout slot (mode 2)
   int mode;        // 1: finish with the whole optimal rollout, 2: step 0 only (the rest deferred)
-  int pad0[2];
+  int noise_slot;  // >= 0: the rollout workgroups outside the finish generate the normals of Philox block
+                   // base noise_n_base into this slot after their records (-1: none)
+  unsigned noise_n_base_lo;
   float x0, y0, h0x, h0y, h0z, wl, wr, gx, gy, s1, s2, igx, igy, pf_scale;  // robot / goal state
   int pf_far, speed_on;
-  unsigned pad1[8];
+  unsigned noise_n_base_hi;
+  unsigned pad1[7];
 };
-constexpr int kCmdWords = 24;                 // the words a step reads (seq .. speed_on)
+constexpr int kTailSlots = 4;                 // deferred optimal rollouts in flight (mppi_capi.cpp)
+constexpr int kCmdWords = 25;                 // the words a step reads (seq .. noise_n_base_hi)
+constexpr int kNoiseChunk = 16;               // noise units a server workgroup claims at a time
 constexpr unsigned kDoneFail = 0x80000000u;   // done | kDoneFail: the step's finish gave up
 struct FinishArgs {
   int H;
@@ -55,11 +60,7 @@ struct FinishArgs {
   // memory, system scope, release) so the host can spin on it instead of a stream sync
   unsigned* done;
   unsigned seq;
-  // resident server: after `done`, the finish stores seq to *fin_done (its tail inputs are
-  // complete); mppi_tail_kernel with gate != null waits for *gate >= gate_seq before reading them
-  unsigned* fin_done;
-  const unsigned* gate;
-  unsigned gate_seq;
+  uint64_t* clk;  // optional: the deferred tail's stamps (kClkServer ring)
   // multi-workgroup first tree level (launch_finish with groups > 1)
   double* level1;         // [groups][2H+2]
   unsigned* level1_cnt;   // zero-initialised, re-armed in-kernel
@@ -120,9 +121,11 @@ struct RolloutArgs {
 // clk layout: [0..8) the stamps above, then (role-split kernel) [kClkBase + 2 b], [.. + 1] =
 // s_memrealtime when workgroup b (< kClkBlocks) starts and when its record is written
 constexpr int kClkBase = 8, kClkBlocks = 4096;
-// then (resident server, last step) s_memrealtime at [kClkServer + k]: 0 workgroup 0 saw the command,
-// 1 the last rollout ticket, 2 the completion word stored, 3 workgroup 0 started polling for it
-constexpr int kClkServer = kClkBase + 2 * kClkBlocks, kClkWords = kClkServer + 8;
+// then (resident server) s_memrealtime per step, ring of 8 steps: [kClkServer + 8 (seq % 8) + k], k =
+// 0 workgroup 0 saw the command, 1 the last rollout ticket, 2 the completion word stored, 3 the
+// latest end of a noise phase (atomic max), 4 the deferred tail started, 5 the tail ended,
+// 6 workgroup 0 started polling for the command
+constexpr int kClkServer = kClkBase + 2 * kClkBlocks, kClkWords = kClkServer + 64;
 // The finish's phase-2 LDS (finish_phase2): uo[2][PS] v w sin cos[H] chain[12H] out[16H]
 // lr[2][PS] floats, PS = the filter rows' stride (a multiple of 4 floats, >= H + 32 for the
 // filter's read-ahead); the DEM window (LDS finish) starts at fin_phase2_floats(H) floats.
@@ -157,31 +160,28 @@ constexpr int ROLES_WAVES_PER_TRAJ_WAVE = 4;
 // the next sequence number (or cmd->stop, or idle_ticks of the 100 MHz clock without a command:
 // then it exits), runs its rollout and writes its record through, and takes a ticket from rec_cnt;
 // the workgroups holding the last fin_groups tickets run the column-split finish (each after rec_cnt
-// reaches nroll, or wait_ticks: then the step publishes done | kDoneFail).  The workgroup taking the
-// last ticket stores seq to *roll_done (pinned: the gate of the noise of a later step).  Only workgroup
+// reaches nroll, or wait_ticks: then the step publishes done | kDoneFail); the other workgroups
+// generate the normals of step + 2 meanwhile (ServerCmd::noise_slot).  Only workgroup
 // 0 polls the pinned command (256 workgroups polling host memory cost ~30 us per step, one ~4 us:
 // profiles/ubench/server.hip); it relays the command words and seq / stop through device memory.
 struct ServerArgs {
   FinishArgs f;
   int nroll, fin_P, fin_ncol, fin_groups;
-  unsigned* rec_cnt;          // zeroed, re-armed by the finish
+  unsigned* rec_cnt;          // [0] records counted, [1 + seq % 2] noise units claimed; zeroed, re-armed by
+                              // the finish (the noise counter of the step before)
   const ServerCmd* cmd;       // pinned host memory (polled by workgroup 0 only)
   unsigned* relay;            // device: [0] seq, [1] stop as relayed by workgroup 0, [16, 16 + kCmdWords) the
                               // command words (zeroed before the launch)
-  unsigned* roll_done;        // pinned host memory
   float* eps[3];              // the normals slots
   float* u_nom[2];            // the nominal double buffer, [2H] each
-  float* tail_in[3];          // deferred optimal rollout inputs per slot (device)
-  float* tail_out[3];         // its outputs per slot (pinned)
+  float* tail_in[kTailSlots];   // deferred optimal rollout inputs per slot (device)
+  float* tail_out[kTailSlots];  // its outputs per slot (pinned)
   unsigned first_seq;
   uint64_t wait_ticks;        // a finish's record wait bound
   uint64_t idle_ticks;        // exit after this long without a command
   uint64_t* clk;              // optional: the server stamps [kClkServer, kClkServer + 4) of RolloutArgs::clk
 };
 hipError_t launch_step_server(const RolloutArgs& a, const ServerArgs& z, size_t lds, hipStream_t st, int proj);
-// one wave on `st` that returns once *sig >= seq (wrap-safe compare) or after `ticks` of the 100 MHz
-// clock: whatever `st` holds next runs after the server's rollout part of step seq
-hipError_t launch_gate(const unsigned* sig, unsigned seq, uint64_t ticks, hipStream_t st);
 // record tree finish (mppi_finish_kernel): the fallback where the column-split shape does not fit
 hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, int groups = 1);
 // column-split finish: every workgroup builds the pair-scale table and reduces ncol columns

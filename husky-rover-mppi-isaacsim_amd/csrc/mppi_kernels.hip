@@ -2325,12 +2325,11 @@ __device__ __forceinline__ void store_out(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // Every wave's stores (outputs, nominal sequence, tail inputs; all write-through) complete, then the
-// completion word and, for a resident server's gated tail, fin_done.
+// completion word (the host launches a resident server's deferred tail after seeing it).
 __device__ __forceinline__ void signal_done(const FinishArgs& f) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0 && f.done) __hip_atomic_store(f.done, f.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (threadIdx.x == 0 && f.fin_done) __hip_atomic_store(f.fin_done, f.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Phase 2 of the finish (MPPI_isaac.py:655-720): `ures` = u_opt[tid] for tid < 2H
@@ -2947,7 +2946,10 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
   if (nblk == 1) {
     if (tid < 2 * H) ures = (S > 0.0) ? (float)(part[(tid + 2) * NG] / S) : 0.0f;
     __syncthreads();
-    if (RECS_WT && tid == 0) __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (RECS_WT && tid == 0) {  // (and the noise counter of the step before: every claim on it is done)
+      __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(rec_cnt + 1 + ((f.seq - 1) & 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   } else {
     const unsigned long long tag = (unsigned long long)f.seq << 32;
     for (int c = tid; c < nc; c += FIN_THREADS) {
@@ -2982,7 +2984,10 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
     FINWG_STAMP(blk, 1);
 #endif
     // every finish workgroup has passed its record wait (resident server): re-arm the count
-    if (RECS_WT && tid == 0) __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (RECS_WT && tid == 0) {  // (and the noise counter of the step before: every claim on it is done)
+      __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(rec_cnt + 1 + ((f.seq - 1) & 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 #ifdef MPPI_STAMPS
   FIN_STAMP(13);
@@ -3011,23 +3016,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void mppi_tail_kernel(const FinishArg
   float* snb = vb + H;
   float* csb = snb + H;
   float* chain = csb + H;
-  if (f.gate) {  // resident server: launched ahead, waits (bounded, 2 s) for the finish's inputs
-    __shared__ int late;
-    if (tid == 0) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      int lt = 0;
-      while ((int)(__hip_atomic_load(f.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - f.gate_seq) < 0) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 >= kColfinPollTicks) {
-          lt = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(8);
-      }
-      late = lt;
-    }
-    __syncthreads();
-    if (late) return;  // the step failed (the host released the gate or it expired): nothing to roll out
-  }
+  if (tid == 0 && f.clk) f.clk[kClkServer + 8 * (f.seq & 7) + 4] = __builtin_amdgcn_s_memrealtime();
   // (agent-scope loads: written through by the finish; an L1 line of an earlier tail could be stale)
   for (int i = tid; i < 3 * H; i += TAIL_THREADS)
     vb[i] = __hip_atomic_load(f.tail_in + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3036,6 +3025,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void mppi_tail_kernel(const FinishArg
   dem.init(f.Z, nullptr, f.rows, f.grid, 0, 0, 1, 1, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
   dem.N = f.ntab;
   optimal_rollout<false>(f, dem, vb, snb, csb, chain, H, f.tail_out, tid, TAIL_THREADS);
+  if (tid == 0 && f.clk) f.clk[kClkServer + 8 * (f.seq & 7) + 5] = __builtin_amdgcn_s_memrealtime();
 }
 
 // =====================================================================  standalone bilinear
@@ -3677,43 +3667,34 @@ hipError_t launch_normal_table(const float* Z, int rows, int grid, float res, fl
   return hipGetLastError();
 }
 
-#ifndef MPPI_NOISE_WT
-#define MPPI_NOISE_WT 1
-#endif
-// The step's sampling normals (sampling_warp.py:54-92 with the Philox noise of
-// DEFINED D1), precomputed so the rollout's side waves only load them: thread =
-// (block, Philox block n = t/2, trajectory); writes eps1/eps2 of steps t, t+1.
-// Rows g = g0, g0 + gstride, ... of (block, Philox block n) for trajectory tj of each block.
+// The step's sampling normals (sampling_warp.py:54-92 with the Philox noise of DEFINED D1),
+// precomputed so the rollout's producer waves only load them.  Unit g = (block g / NB, Philox block
+// n = g % NB) for the trajectory tj of that block: eps1 / eps2 of steps t = 2n, 2n + 1, stored
+// write-through (agent scope, sc1): the rows do not sit dirty in the XCD's L2 (a later kernel
+// boundary would write them back) and other CUs read them after an L1 invalidate only.
+__device__ __forceinline__ void noise_unit(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int64_t g,
+                                           float* __restrict__ eps, int tj) {
+  const int NB = (H + 1) >> 1;
+  const int n = (int)(g % NB);
+  const int64_t blk = g / NB;
+  const uint64_t kg = (uint64_t)(k_offset + blk * 256 + tj);
+  float a1, a2, b1, b2;
+  noise_block(seed, n_base + (uint64_t)n, kg, &a1, &a2, &b1, &b2);
+  const int t = 2 * n;
+  float* e1 = eps + ((size_t)blk * 2 * H + t) * 256 + tj;
+  float* e2 = e1 + (size_t)H * 256;
+  __hip_atomic_store(e1, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(e2, a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t + 1 < H) {
+    __hip_atomic_store(e1 + 256, b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(e2 + 256, b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// units g0, g0 + gstride, ... of n_blocks blocks
 __device__ __forceinline__ void noise_rows(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int n_blocks,
                                            float* __restrict__ eps, int64_t g0, int64_t gstride, int tj) {
   const int NB = (H + 1) >> 1;
-  for (int64_t g = g0; g < (int64_t)n_blocks * NB; g += gstride) {
-    const int n = (int)(g % NB);
-    const int64_t blk = g / NB;
-    const uint64_t kg = (uint64_t)(k_offset + blk * 256 + tj);
-    float a1, a2, b1, b2;
-    noise_block(seed, n_base + (uint64_t)n, kg, &a1, &a2, &b1, &b2);
-    const int t = 2 * n;
-    float* e1 = eps + ((size_t)blk * 2 * H + t) * 256 + tj;
-    float* e2 = e1 + (size_t)H * 256;
-#if MPPI_NOISE_WT
-    // write-through (agent-scope, sc1) stores: the rows do not sit dirty in the XCD's L2, where the
-    // next kernel boundary on any stream would have to write them back
-    __hip_atomic_store(e1, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(e2, a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t + 1 < H) {
-      __hip_atomic_store(e1 + 256, b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(e2 + 256, b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#else
-    e1[0] = a1;
-    e2[0] = a2;
-    if (t + 1 < H) {
-      e1[256] = b1;
-      e2[256] = b2;
-    }
-#endif
-  }
+  for (int64_t g = g0; g < (int64_t)n_blocks * NB; g += gstride) noise_unit(seed, n_base, k_offset, H, g, eps, tj);
 }
 __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t n_base, int64_t k_offset,
                                                          int H, int n_blocks, float* __restrict__ eps) {
@@ -3726,10 +3707,10 @@ __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t
 // between polls) until it reaches `expect` (or cmd->stop, or idle_ticks without a command: every
 // wave exits), reads the command words into LDS, and the workgroup runs the role-split rollout with
 // the command's state, normals slot and nominal buffer.  Its record is written through and counted
-// (rec_cnt); the workgroup with the last ticket stores seq to *roll_done (the noise gate of a later
-// step); the workgroups holding the last fin_groups tickets run the column-split finish, each after
-// rec_cnt reaches nroll (bounded by wait_ticks: a finish without every record publishes
-// done = seq | kDoneFail).  No assumption on dispatch order or co-residency: a workgroup waits only
+// (rec_cnt); the workgroups holding the last fin_groups tickets run the column-split finish, each
+// after rec_cnt reaches nroll (bounded by wait_ticks: a finish without every record publishes
+// done = seq | kDoneFail); the others generate the normals of step + 2 meanwhile (noise phase:
+// the chip is otherwise idle while the finish reduces and the host turns the step around).  No assumption on dispatch order or co-residency: a workgroup waits only
 // for records of workgroups that run or get a slot as others reach their wait.
 // Cross-step data: the nominal sequence, the tail inputs and the records are
 // written through and read with agent-scope loads; the normals rows (another kernel's write-through
@@ -3771,7 +3752,7 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
       unsigned ok = 0;
       if (tid == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        if (head && z.clk) z.clk[kClkServer + 3] = t0;
+        if (head && z.clk) z.clk[kClkServer + 8 * (expect & 7) + 6] = t0;
         for (;;) {
           const unsigned long long w = head ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                             : __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3780,7 +3761,7 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
             break;
           }
           if ((w >> 32) != 0 || __builtin_amdgcn_s_memrealtime() - t0 >= z.idle_ticks) break;
-          if (!head) __builtin_amdgcn_s_sleep(1);
+          if (!head) __builtin_amdgcn_s_sleep(8);  // (~0.2 us: 255 pollers of one word stay off the rollout's way)
         }
       }
       ok = __builtin_amdgcn_readfirstlane(ok);
@@ -3806,7 +3787,7 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
         }
       }
       if (tid == 0) cmd_lds[31] = ok;
-      if (tid == 0 && head && z.clk) z.clk[kClkServer] = __builtin_amdgcn_s_memrealtime();
+      if (tid == 0 && head && z.clk && ok) z.clk[kClkServer + 8 * (cmd_lds[0] & 7)] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     if (!cmd_lds[31]) return;  // stop, or idle: the host relaunches
@@ -3838,11 +3819,35 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
     a.pf_far = __builtin_amdgcn_readfirstlane(c.pf_far);
     a.speed_on = __builtin_amdgcn_readfirstlane(c.speed_on);
     const int ticket = roles_body<TB, PROJ, 0, false, true>(a, z.rec_cnt, sh);
-    if (ticket == z.nroll - 1 && tid == 0) {  // every rollout workgroup has counted: the noise gate
-      __hip_atomic_store(z.roll_done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (z.clk) z.clk[kClkServer + 1] = __builtin_amdgcn_s_memrealtime();
-    }
+    if (ticket == z.nroll - 1 && tid == 0 && z.clk) z.clk[kClkServer + 8 * (seq & 7) + 1] = __builtin_amdgcn_s_memrealtime();
     const int blk = ticket - (z.nroll - z.fin_groups);
+    if (blk < 0 && c.noise_slot >= 0) {
+      // the normals of a later step (c.noise_n_base, into slot c.noise_slot) while the finish
+      // workgroups reduce the records and the host turns the step around: chunks of kNoiseChunk
+      // units claimed from this step's counter (rec_cnt[1 + seq % 2], zeroed by the finish of the
+      // step after), four 256-trajectory units per pass
+      __builtin_amdgcn_s_setprio(0);
+      const int nslot = __builtin_amdgcn_readfirstlane(c.noise_slot);
+      const uint64_t nbase = ((uint64_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_hi) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_lo);
+      const int64_t U = (int64_t)z.nroll * ((a.H + 1) >> 1);
+      float* eps_out = z.eps[nslot];
+      unsigned* ctr = z.rec_cnt + 1 + (seq & 1);
+      for (;;) {
+        if (tid == 0) sh[1] = (int)__hip_atomic_fetch_add(ctr, (unsigned)kNoiseChunk, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int64_t u0 = sh[1];
+        __syncthreads();
+        if (u0 >= U) break;
+        const int64_t u1 = min(u0 + kNoiseChunk, U);
+        for (int64_t g = u0 + (tid >> 8); g < u1; g += NROLES * TB / 256)
+          noise_unit(a.seed, nbase, a.k_offset, a.H, g, eps_out, tid & 255);
+      }
+      if (tid == 0 && z.clk)
+        __hip_atomic_fetch_max(z.clk + kClkServer + 8 * (seq & 7) + 3, (uint64_t)__builtin_amdgcn_s_memrealtime(),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (blk >= 0) {
       __builtin_amdgcn_s_setprio(0);  // the rollout waves' priorities do not carry into the finish
       if (tid == 0) {  // bounded (z.wait_ticks of the 100 MHz clock): a lost count cannot hang the device
@@ -3879,7 +3884,7 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
         f.wl = a.wl;
         f.wr = a.wr;
         ok = colfin_body<true>(f, z.fin_P, z.fin_ncol, blk, z.fin_groups, z.rec_cnt);
-        if (ok && blk == z.fin_groups - 1 && tid == 0 && z.clk) z.clk[kClkServer + 2] = __builtin_amdgcn_s_memrealtime();
+        if (ok && blk == z.fin_groups - 1 && tid == 0 && z.clk) z.clk[kClkServer + 8 * (seq & 7) + 2] = __builtin_amdgcn_s_memrealtime();
       }
       // a finish that gave up publishes the failure (the host stops the server and re-arms the count)
       if (!ok && tid == 0)
@@ -3899,19 +3904,6 @@ hipError_t launch_step_server(const RolloutArgs& a, const ServerArgs& z, size_t 
     hipLaunchKernelGGL((mppi_step_server_kernel<256, 3>), g, b, lds, st, ServerLaunch{a, z});
   else
     hipLaunchKernelGGL((mppi_step_server_kernel<256, 2>), g, b, lds, st, ServerLaunch{a, z});
-  return hipGetLastError();
-}
-
-__global__ __launch_bounds__(64) void mppi_gate_kernel(const unsigned* sig, unsigned seq, uint64_t ticks) {
-  if (threadIdx.x != 0) return;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while ((int)(__hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0 &&
-         __builtin_amdgcn_s_memrealtime() - t0 < ticks)
-    __builtin_amdgcn_s_sleep(8);
-}
-
-hipError_t launch_gate(const unsigned* sig, unsigned seq, uint64_t ticks, hipStream_t st) {
-  hipLaunchKernelGGL(mppi_gate_kernel, dim3(1), dim3(64), 0, st, sig, seq, ticks);
   return hipGetLastError();
 }
 

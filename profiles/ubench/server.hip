@@ -89,6 +89,13 @@ __global__ __launch_bounds__(1024) void k_server(const Box* box, unsigned* cnt, 
   }
 }
 
+// a noise-like side kernel (4-wave workgroups, few VGPRs, no LDS) on another stream
+__global__ __launch_bounds__(256) void k_side(float* out, int iters) {
+  float x = (float)threadIdx.x;
+  for (int i = 0; i < iters; ++i) x = x * 1.0001f + 0.5f;
+  out[(blockIdx.x * 256 + threadIdx.x) & 4095] = x;
+}
+
 static double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -162,6 +169,39 @@ int main(int argc, char** argv) {
       printf("resident grid=%d poll=%d W=%u us: %.2f us/step (overhead %.2f)\n", grid, poll, w_us, (t1 - t0) / steps,
              (t1 - t0) / steps - w_us);
     }
+  }
+  // co-residency: a side kernel (1024 x 256 threads) on a low-priority stream per step while the
+  // resident kernel (relay polling) serves the steps; time the host waits for the side kernel
+  {
+    hipStream_t s2;
+    int lo = 0, hi = 0;
+    hipDeviceGetStreamPriorityRange(&lo, &hi);
+    hipStreamCreateWithPriority(&s2, hipStreamNonBlocking, lo);
+    hipEvent_t e2;
+    hipEventCreateWithFlags(&e2, hipEventDisableTiming);
+    float* side;
+    hipMalloc(&side, 4096 * sizeof(float));
+    box->stop = 0;
+    hipMemset(relay, 0, 64);
+    hipDeviceSynchronize();
+    hipLaunchKernelGGL(k_server, dim3(256), dim3(1024), lds, s, (const Box*)box, cnt, done, w_us, sink, 3, seq + 1, relay);
+    double side_wait = 0, t0 = now_us();
+    const int n = 200;
+    for (int i = 0; i < n; ++i) {
+      ++seq;
+      __atomic_store_n(&box->go, seq, __ATOMIC_RELEASE);
+      hipLaunchKernelGGL(k_side, dim3(1024), dim3(256), 0, s2, side, 2000);
+      hipEventRecord(e2, s2);
+      wait(seq);
+      const double a = now_us();
+      hipEventSynchronize(e2);
+      side_wait += now_us() - a;
+    }
+    const double t1 = now_us();
+    __atomic_store_n(&box->stop, 1u, __ATOMIC_RELEASE);
+    hipStreamSynchronize(s);
+    printf("resident + side kernel per step: %.2f us/step, host wait for the side kernel %.2f us/step\n",
+           (t1 - t0) / n, side_wait / n);
   }
   return 0;
 }

@@ -11,8 +11,12 @@ from mppi_amd import _lib, scene  # noqa: E402
 
 Z, hw, cm = scene.scene_c3()
 H = int(sys.argv[1]) if len(sys.argv) > 1 else 100
-for async_tail in (True, False):
+for async_tail, ts in ((True, 1), (True, 2), (False, 1)):
     eng = _lib.Engine(_lib.make_params(65536, H), 0)
+    if os.environ.get("MPPI_RESIDENT", "1") != "0":
+        eng.set_option("tail_streams", ts)
+    elif ts == 2:
+        continue
     eng.set_dem(Z, hw)
     eng.set_costmap(cm, hw)
     eng.set_state(_lib.make_state(-60.0, -5.0, (1.0, 0.0, 0.0), goal_x=65.0, goal_y=10.0))
@@ -34,11 +38,23 @@ for async_tail in (True, False):
     dt = (time.perf_counter() - t0) / n * 1e6
     info = eng.launch_info()
     import ctypes as C
-    v = (C.c_double * 269)()
-    eng._c(eng.lib.mppi_get_chain_clock(eng.ctx, v, 269), "mppi_get_chain_clock")
+    import numpy as np
+    v = (C.c_double * 330)()
+    eng._c(eng.lib.mppi_get_chain_clock(eng.ctx, v, 330), "mppi_get_chain_clock")
     print(f"  last step: chain {v[1]:.0f} cyc/step {v[2]:.1f} us, wg0 leaf {v[6]:.1f} us, wg start spread {v[7]:.1f}, "
-          f"end spread {v[8]:.1f}, span {v[9]:.1f} us; server: poll->cmd {v[266]:.1f}, ->last ticket {v[267]:.1f}, "
-          f"->done {v[268]:.1f} us")
+          f"end spread {v[8]:.1f}, span {v[9]:.1f} us")
+    rec = np.array([v[10 + b] for b in range(256)])
+    print("  per-workgroup record time from the first start (us): min %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f" %
+          (rec.min(), *np.percentile(rec, [10, 50, 90]), rec.max()))
+    st = np.array([[v[266 + 8 * r + k] for k in range(8)] for r in range(8)])
+    print("  server timeline, last 8 steps (us): [cmd seen, rollout = last ticket - cmd, finish = done - last ticket, "
+          "noise end - done, next cmd - done, tail: gate - done, run]")
+    for r in range(8):
+        cmd, tick, done, nz, tg, te = st[r, :6]
+        nxt = st[r + 1, 0] if r < 7 else 0.0
+        print("    %8.1f  roll %6.1f  fin %6.1f  noise %+6.1f  turn %6.1f  tail %6.1f %6.1f" % (
+            cmd, tick - cmd, done - tick, (nz - done) if nz else float("nan"), (nxt - done) if nxt else float("nan"),
+            (tg - done) if tg else float("nan"), (te - tg) if te else float("nan")))
     eng.close()
-    print(f"async_tail={async_tail}: " + "  ".join(f"[{i} step {a:.0f} out {b:.0f} L{l}]" for i, a, b, l in rows))
+    print(f"async_tail={async_tail} tail_streams={ts}: " + "  ".join(f"[{i} step {a:.0f} out {b:.0f} L{l}]" for i, a, b, l in rows))
     print(f"  {n} back-to-back steps: {dt:.1f} us/step, launches {info['server_launches']}, steps {info['server_steps']}")

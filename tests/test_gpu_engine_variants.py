@@ -121,7 +121,7 @@ def test_server_idle_exit_and_stop():
     """The server leaves after its idle limit and is relaunched by the next step; a call that stops it
     (mppi_get_costs) between steps, too.  Every step equals the separate launches."""
     ref = _run(65536, 24, opts={"resident": 0}, steps=4, async_tail=True)
-    eng = _engine(65536, 24, opts={"resident_idle_us": 200}, async_tail=True)
+    eng = _engine(65536, 24, opts={"resident_idle_us": 5000}, async_tail=True)
     outs = []
     try:
         for i in range(4):
@@ -129,7 +129,7 @@ def test_server_idle_exit_and_stop():
             o = eng.outputs()
             outs.append({k: o[k].copy() for k in ALL})
             if i == 1:
-                time.sleep(0.01)      # past the idle limit: the server has exited
+                time.sleep(0.02)      # past the idle limit: the server has exited
             if i == 2:
                 eng.costs()           # stops the server
         info = eng.launch_info()
