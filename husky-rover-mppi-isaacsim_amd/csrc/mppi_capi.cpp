@@ -430,6 +430,8 @@ void fill_rollout(const mppi_ctx* c, const Plan& pl, const mppi_state& st, uint6
   a.inj_u1 = c->inj1;
   a.inj_u2 = c->inj2;
   a.wave_prio = 1;
+  // |w dt| < pi/4 for every clamped w: sin / cos without the range reduction (same bits)
+  a.small_angle = std::max(std::fabs(p.v_min_angular), std::fabs(p.v_max_angular)) * p.dt < 0.78f;
 }
 
 void fill_finish(const mppi_ctx* c, const Plan& pl, const mppi_state& st, FinishArgs& f) {

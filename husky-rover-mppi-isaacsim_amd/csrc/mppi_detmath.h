@@ -118,6 +118,31 @@ MPPI_HD void dm_sincosf(float x, float* s_out, float* c_out) {
   *c_out = cneg ? -c0 : c0;
 }
 
+// dm_sincosf for |x| * 4/pi < 1 (quadrant 0), the same bits: there j = 0, the reduction subtracts
+// exact zeros (r = |x|), no swap and no sign flips but sin's, and (poly * z) * x + x = -((poly * z)
+// * |x| + |x|) for x < 0 (IEEE negation is exact): the Rodrigues angle w * dt of the rollout, with
+// |w| <= max(|w_min|, |w_max|) and that bound times dt under pi/4 (RolloutArgs::small_angle).
+MPPI_HD void dm_sincosf_small(float x, float* s_out, float* c_out) {
+  const float z = x * x;
+  float ps = -1.9515295891e-4f * z;
+  ps = ps + 8.3321608736e-3f;
+  ps = ps * z;
+  ps = ps + -1.6666654611e-1f;
+  ps = ps * z;
+  ps = ps * x;
+  ps = ps + x;
+  float pc = 2.443315711809948e-5f * z;
+  pc = pc + -1.388731625493765e-3f;
+  pc = pc * z;
+  pc = pc + 4.166664568298827e-2f;
+  pc = pc * z;
+  pc = pc * z;
+  pc = pc - 0.5f * z;
+  pc = pc + 1.0f;
+  *s_out = ps;
+  *c_out = pc;
+}
+
 // ------------------------------------------------------------------ Philox4x32-10
 struct U4 {
   uint32_t x, y, z, w;

@@ -110,6 +110,8 @@ struct RolloutArgs {
   // dump (DUMP)
   float *d_traj, *d_hv, *d_lw, *d_rw, *d_v, *d_w, *d_u1, *d_u2;
   int wave_prio;        // pair kernel: raise the waves' issue priority (s_setprio 2)
+  int small_angle;      // max(|wmin|, |wmax|) * dt < 0.78: the Rodrigues angle's sin / cos by
+                        // dm_sincosf_small (the same bits, no range reduction)
   int ucache_steps;     // pair kernel, MODE 0: steps [0, n) keep their sampled controls in LDS
                         // ([2][n][TB] floats after the scratch) for leaf_records
   // optional [8]: the chain wave of group 0 in workgroup 0 stores s_memtime / s_memrealtime at

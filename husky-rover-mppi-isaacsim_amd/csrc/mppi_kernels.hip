@@ -1518,7 +1518,8 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 #if MPPI_SC_SIDE
         {
           float sn, cs;
-          dm_sincosf(wp * a.dt, &sn, &cs);
+          if (a.small_angle) dm_sincosf_small(wp * a.dt, &sn, &cs);
+          else dm_sincosf(wp * a.dt, &sn, &cs);
           ri[TB] = sn;
           ri[2 * TB] = cs;
           ri[3 * TB] = 1.0f - cs;
@@ -1871,7 +1872,8 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
       const float vp = clampf((L + R) / 2.0f, a.vmin, a.vmax);
       const float wp = clampf(((-L) + R) / a.rwheel, a.wmin, a.wmax);
       float sn, cs;
-      dm_sincosf(wp * a.dt, &sn, &cs);
+      if (a.small_angle) dm_sincosf_small(wp * a.dt, &sn, &cs);
+      else dm_sincosf(wp * a.dt, &sn, &cs);
       wait_ge(f_cost, p - D + 1, seen_cost);
       float* ri = ring_in + (p % D) * RI * TB + tj;
       ri[0] = vp;

@@ -152,6 +152,29 @@ def dm_sincosf(x):
     return s, c
 
 
+def dm_sincosf_small(x):
+    """dm_sincosf for |x| * 4/pi < 1 without the reduction (csrc/mppi_detmath.h dm_sincosf_small):
+    the same float32 op sequence on r = x; equal bits there (tests/test_oracle_golden.py)."""
+    x = f32(x)
+    z = x * x
+    ps = SIN_P[0] * z
+    ps = ps + SIN_P[1]
+    ps = ps * z
+    ps = ps + SIN_P[2]
+    ps = ps * z
+    ps = ps * x
+    ps = ps + x
+    pc = COS_P[0] * z
+    pc = pc + COS_P[1]
+    pc = pc * z
+    pc = pc + COS_P[2]
+    pc = pc * z
+    pc = pc * z
+    pc = pc - F32(0.5) * z
+    pc = pc + F32(1.0)
+    return ps.astype(F32), pc.astype(F32)
+
+
 # ---------------------------------------------------------------- Philox
 def _mulhilo(m, a):
     p = m * a.astype(U64)

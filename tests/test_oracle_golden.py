@@ -140,3 +140,20 @@ def test_oracle_step_regression(steps, name):
     out = mg.run_step_case(name, steps["Z"], float(steps["hw"]), steps["cm"])
     for key, val in out.items():
         np.testing.assert_array_equal(val, steps[f"{name}/{key}"], err_msg=f"{name}/{key}")
+
+
+def test_sincos_small_angle_path_equals_general():
+    """dm_sincosf_small (the rollout's sin / cos of w dt when max|w| dt < 0.78, no range reduction)
+    gives dm_sincosf's bits on every float32 in [-0.78, 0.78] sampled densely (all floats in
+    [2^-12, 2^-11) and [0.75, 0.78], 4 M random ones, zeros, the bound) — both signs."""
+    rng = np.random.default_rng(5)
+    lo = np.arange(np.float32(2.0 ** -12).view(np.uint32), np.float32(2.0 ** -11).view(np.uint32), dtype=np.uint32)
+    hi = np.arange(np.float32(0.75).view(np.uint32), np.float32(0.78).view(np.uint32), dtype=np.uint32)
+    x = np.concatenate([lo.view(F32), hi.view(F32), rng.uniform(0, 0.78, 4_000_000).astype(F32),
+                        np.array([0.0, 1e-30, 0.78, 0.045], F32)])
+    x = np.concatenate([x, -x])
+    assert np.all(np.abs(x) * dmath.FOPI < F32(1.0))
+    s0, c0 = dmath.dm_sincosf(x)
+    s1, c1 = dmath.dm_sincosf_small(x)
+    assert np.array_equal(s0.view(np.uint32), s1.view(np.uint32))
+    assert np.array_equal(c0.view(np.uint32), c1.view(np.uint32))
