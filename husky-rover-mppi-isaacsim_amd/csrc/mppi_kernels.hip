@@ -1694,6 +1694,9 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 // ~98 and ~120 us (profiles/r02_notes.md); 0: ~9900 against ~9200 steps/s
 #define MPPI_SIDE_PRIO 0
 #endif
+#ifndef MPPI_DIAG_SIDE
+#define MPPI_DIAG_SIDE 0  // diagnostic builds: 1 wheel / cost roles idle, 2 also a constant producer
+#endif
 #ifndef MPPI_PROD_PRIO
 #define MPPI_PROD_PRIO MPPI_SIDE_PRIO  // the producer's (the chain waits on it each step)
 #endif
@@ -1835,7 +1838,36 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
       }
       lds_store_release(f_chain, sc + 1);
     }
-  } else if (role == ROLE_PROD) {
+  }
+#if MPPI_DIAG_SIDE  // diagnostic builds only: the side roles keep the protocol and skip their work
+  else if (role == ROLE_PROD && MPPI_DIAG_SIDE >= 2) {
+    int seen_cost = 0;
+    for (int p = 0; p < H; ++p) {
+      wait_ge(f_cost, p - D + 1, seen_cost);
+      float* ri = ring_in + (p % D) * RI * TB + tj;
+      const float sn = 0.0123f * (float)(tj & 7) - 0.04f, cs = 0.99f;
+      ri[0] = 0.9f;
+      ri[TB] = sn;
+      ri[2 * TB] = cs;
+      ri[3 * TB] = 1.0f - cs;
+      lds_store_release(f_prod, p + 1);
+    }
+  } else if (role == ROLE_WHEEL) {
+    int seen_chain = 0;
+    for (int sc = 0; sc < H; sc += 2) {
+      wait_ge(f_chain, sc + 1, seen_chain);
+      lds_store_release(f_wheel, min(sc + 2, H));
+    }
+    sw_lds[tj] = 0.f;
+  } else if (role == ROLE_COST) {
+    int seen_chain = 0;
+    for (int sc = 0; sc < H; ++sc) {
+      wait_ge(f_chain, sc + 1, seen_chain);
+      lds_store_release(f_cost, sc + 1);
+    }
+  }
+#endif
+  else if (role == ROLE_PROD) {
     // ---------------- sampling + wheel filter + sin/cos, normals prefetched two steps ahead
     // (even / odd steps in their own registers: no loop-carried copy of a load in flight)
     const float* eps_row = (MODE == 0) ? a.eps + (size_t)blockIdx.x * (2 * H) * TB + tj : nullptr;

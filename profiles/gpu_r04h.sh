@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 4: resident server with deferred tails (diag timeline, variant tests, 20/200-step benches
+# against separate launches), then the chain-alone diagnostic builds (ab/side1.so: wheel and cost
+# roles idle; ab/side2.so: also a constant producer)
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+TAG=${1:-r04h}
+O=$R/gpurun_out
+cd $R
+bash profiles/gpu_r04g.sh $TAG || exit 1
+for lib in ab/side1.so ab/side2.so; do
+  MPPI_LIB_PATH=$R/$lib MPPI_RESIDENT=0 timeout -k 10 200 python bench.py --steps 50 --warmup 5 --cpu-baseline-seconds 0 --no-bilinear --no-costmap --no-c5 --no-c4 --no-shard --no-sync-pass > $O/side.json 2>$O/side.err || { tail -5 $O/side.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/side.json')); print('[$lib] chain', d['config'].get('chain'), 'roll', d['roofline']['kernel_avg_ms'])"
+done
+MPPI_RESIDENT=0 timeout -k 10 200 python bench.py --steps 50 --warmup 5 --cpu-baseline-seconds 0 --no-bilinear --no-costmap --no-c5 --no-c4 --no-shard --no-sync-pass > $O/side.json 2>$O/side.err || { tail -5 $O/side.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/side.json')); print('[product] chain', d['config'].get('chain'), 'roll', d['roofline']['kernel_avg_ms'])"
