@@ -931,6 +931,10 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   // normals of step + 1 (normally generated by the previous step's noise phase; else now, on the
   // noise stream beside this step) and of step + 2 (by this step's noise phase, in the server)
   const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
+  // the noise phase runs in the workgroups outside the finish but workgroup 0: with fewer than a
+  // quarter of them, or fewer than two (few records: every rollout workgroup may hold a finish
+  // column) the noise kernel does it
+  const bool srv_noise = pl.blocks - groups >= 2 && (int64_t)(pl.blocks - groups) * 4 >= (int64_t)pl.blocks;
   int noise_slot = -1;
   for (int d = 1; d <= 2; ++d) {
     const uint64_t target = step + (uint64_t)d;
@@ -939,7 +943,7 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
     if (got) continue;
     const int v = eps_victim(c, slot, step);
     if (v < 0) return fail(MPPI_ESTATE, "no free noise slot");
-    if (d == 1) {
+    if (d == 1 || !srv_noise) {
       HIP_TRY(launch_noise(c->p.seed, target * nb, c->p.k_offset, pl.blocks, H_of(c), c->eps[v], c->noise_stream,
                            noise_groups(c)));
       HIP_TRY(hipEventRecord(c->eps_ev[v], c->noise_stream));
@@ -978,8 +982,8 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   for (int i = 2; i < kCmdWords; ++i) __atomic_store_n(cw + i, dw[i], __ATOMIC_RELAXED);
   __atomic_store_n(&cmd->seq, seq, __ATOMIC_RELEASE);
   if (!c->srv_running) {
-    HIP_TRY(hipMemsetAsync(c->relay, 0, 64 * sizeof(unsigned), c->stream));
-    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->relay), seq - 1, 1, c->stream));
+    // (no reset of the relay: its seq word is older than this command, and its stop word holds
+    // the first seq of the launch that wrote it, never this one's)
     RolloutArgs a;
     fill_rollout(c, pl, c->st, step, c->u_nom[c->cur], a);
     ServerArgs z;
@@ -1248,7 +1252,8 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       return cleanup(fail(MPPI_EHIP, "tail slot allocation failed"));
   if (hipMemset(c->u_nom[0], 0, 2 * H * sizeof(float)) != hipSuccess ||
       hipMemset(c->u_nom[1], 0, 2 * H * sizeof(float)) != hipSuccess ||
-      hipMemset(c->cost, 0, std::max<int64_t>(p.num_trajectories, 1) * sizeof(float)) != hipSuccess)
+      hipMemset(c->cost, 0, std::max<int64_t>(p.num_trajectories, 1) * sizeof(float)) != hipSuccess ||
+      hipMemset(c->relay, 0, 64 * sizeof(unsigned)) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(MPPI_EHIP, "hipEventCreate failed"));

@@ -173,6 +173,105 @@ MPPI_HD void dm_box_muller(uint32_t ra, uint32_t rb, float* z0, float* z1) {
   *z1 = rad * s;
 }
 
+// ------------------------------------------------------------------ the two Box-Mullers of a block, packed
+// The same op sequences as dm_logf / dm_sincosf / dm_box_muller on (ra, rb) and (rc, rd) side by side:
+// every float product and sum of the pair is one packed FP32 instruction (v_pk_mul_f32 / v_pk_add_f32,
+// IEEE per half, so each half's bits are the scalar sequence's); integer parts, square roots and the
+// quadrant selects stay per half.  sincos: the argument 2 pi v is >= +0, where dm_sincosf's |x| and
+// final sign flip are identities.  Bit-identical to noise_block (tests/test_noise_pack.py, host).
+typedef float mf2 __attribute__((ext_vector_type(2)));
+
+MPPI_HD mf2 dm_logf2(mf2 x) {
+  const uint32_t b0 = f_bits(x.x), b1 = f_bits(x.y);
+  int e0 = (int)((b0 >> 23) & 0xFFu) - 126, e1 = (int)((b1 >> 23) & 0xFFu) - 126;
+  const mf2 m0 = mf2{bits_f((b0 & 0x807FFFFFu) | 0x3F000000u), bits_f((b1 & 0x807FFFFFu) | 0x3F000000u)};
+  const mf2 lo = (m0 + m0) - 1.0f;
+  const mf2 hi = m0 - 1.0f;
+  const bool s0 = m0.x < 0.707106781186547524f, s1 = m0.y < 0.707106781186547524f;
+  e0 -= s0 ? 1 : 0;
+  e1 -= s1 ? 1 : 0;
+  const mf2 m = mf2{s0 ? lo.x : hi.x, s1 ? lo.y : hi.y};
+  const mf2 z = m * m;
+  mf2 y = mf2{7.0376836292e-2f, 7.0376836292e-2f};
+  y = y * m + -1.1514610310e-1f;
+  y = y * m + 1.1676998740e-1f;
+  y = y * m + -1.2420140846e-1f;
+  y = y * m + 1.4249322787e-1f;
+  y = y * m + -1.6668057665e-1f;
+  y = y * m + 2.0000714765e-1f;
+  y = y * m + -2.4999993993e-1f;
+  y = y * m + 3.3333331174e-1f;
+  y = y * m;
+  y = y * z;
+  const mf2 fe = mf2{(float)e0, (float)e1};
+  y = y + -2.12194440e-4f * fe;
+  y = y + -0.5f * z;
+  mf2 r = m + y;
+  r = r + 0.693359375f * fe;
+  return r;
+}
+
+// dm_sincosf of x >= +0 in both halves
+MPPI_HD void dm_sincosf2_pos(mf2 x, mf2* s_out, mf2* c_out) {
+  const mf2 t = x * 1.27323954473516f;
+  int j0 = (int)t.x, j1 = (int)t.y;
+  const mf2 y0 = mf2{(float)j0, (float)j1};
+  const mf2 y1 = y0 + 1.0f;
+  const bool o0 = (j0 & 1) != 0, o1 = (j1 & 1) != 0;
+  j0 = (o0 ? j0 + 1 : j0) & 7;
+  j1 = (o1 ? j1 + 1 : j1) & 7;
+  const mf2 y = mf2{o0 ? y1.x : y0.x, o1 ? y1.y : y0.y};
+  mf2 r = x - y * 0.78515625f;
+  r = r - y * 2.4187564849853515625e-4f;
+  r = r - y * 3.77489497744594108e-8f;
+  const mf2 z = r * r;
+  mf2 ps = -1.9515295891e-4f * z;
+  ps = ps + 8.3321608736e-3f;
+  ps = ps * z;
+  ps = ps + -1.6666654611e-1f;
+  ps = ps * z;
+  ps = ps * r;
+  ps = ps + r;
+  mf2 pc = 2.443315711809948e-5f * z;
+  pc = pc + -1.388731625493765e-3f;
+  pc = pc * z;
+  pc = pc + 4.166664568298827e-2f;
+  pc = pc * z;
+  pc = pc * z;
+  pc = pc - 0.5f * z;
+  pc = pc + 1.0f;
+  auto quad = [](int j, float ps_, float pc_, float* so, float* co) {
+    const bool swap = (j & 2) != 0;
+    const float s0 = swap ? pc_ : ps_;
+    const float c0 = swap ? ps_ : pc_;
+    const bool sneg = (j & 4) != 0;
+    const bool cneg = ((j >> 1) ^ (j >> 2)) & 1;
+    *so = sneg ? -s0 : s0;
+    *co = cneg ? -c0 : c0;
+  };
+  float sa, ca, sb, cb;
+  quad(j0, ps.x, pc.x, &sa, &ca);
+  quad(j1, ps.y, pc.y, &sb, &cb);
+  *s_out = mf2{sa, sb};
+  *c_out = mf2{ca, cb};
+}
+
+MPPI_HD void noise_block_pk(uint64_t seed, uint64_t n, uint64_t k, float* a1, float* a2, float* b1, float* b2) {
+  const U4 r = philox4x32_10(U4{(uint32_t)n, (uint32_t)(n >> 32), (uint32_t)k, (uint32_t)(k >> 32)},
+                             (uint32_t)seed, (uint32_t)(seed >> 32));
+  const mf2 u = (mf2{(float)(r.x >> 8), (float)(r.z >> 8)} + 1.0f) * 5.9604644775390625e-8f;
+  const mf2 v = mf2{(float)(r.y >> 8), (float)(r.w >> 8)} * 5.9604644775390625e-8f;
+  const mf2 l = -2.0f * dm_logf2(u);
+  const mf2 rad = mf2{sqrtf(l.x), sqrtf(l.y)};
+  mf2 s, c;
+  dm_sincosf2_pos(6.2831853071795864769f * v, &s, &c);
+  const mf2 zc = rad * c, zs = rad * s;
+  *a1 = zc.x;
+  *a2 = zs.x;
+  *b1 = zc.y;
+  *b2 = zs.y;
+}
+
 // Noise block n of trajectory k: e1[t], e2[t], e1[t+1], e2[t+1] (t = 2(n mod ceil(H/2))).
 MPPI_HD void noise_block(uint64_t seed, uint64_t n, uint64_t k, float* a1, float* a2, float* b1,
                          float* b2) {

@@ -3706,14 +3706,11 @@ hipError_t launch_normal_table(const float* Z, int rows, int grid, float res, fl
 // n = g % NB) for the trajectory tj of that block: eps1 / eps2 of steps t = 2n, 2n + 1, stored
 // write-through (agent scope, sc1): the rows do not sit dirty in the XCD's L2 (a later kernel
 // boundary would write them back) and other CUs read them after an L1 invalidate only.
-__device__ __forceinline__ void noise_unit(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int64_t g,
+__device__ __forceinline__ void noise_unit(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int blk, int n,
                                            float* __restrict__ eps, int tj) {
-  const int NB = (H + 1) >> 1;
-  const int n = (int)(g % NB);
-  const int64_t blk = g / NB;
-  const uint64_t kg = (uint64_t)(k_offset + blk * 256 + tj);
+  const uint64_t kg = (uint64_t)(k_offset + (int64_t)blk * 256 + tj);
   float a1, a2, b1, b2;
-  noise_block(seed, n_base + (uint64_t)n, kg, &a1, &a2, &b1, &b2);
+  noise_block_pk(seed, n_base + (uint64_t)n, kg, &a1, &a2, &b1, &b2);
   const int t = 2 * n;
   float* e1 = eps + ((size_t)blk * 2 * H + t) * 256 + tj;
   float* e2 = e1 + (size_t)H * 256;
@@ -3724,15 +3721,28 @@ __device__ __forceinline__ void noise_unit(uint64_t seed, uint64_t n_base, int64
     __hip_atomic_store(e2 + 256, b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
-// units g0, g0 + gstride, ... of n_blocks blocks
-__device__ __forceinline__ void noise_rows(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int n_blocks,
-                                           float* __restrict__ eps, int64_t g0, int64_t gstride, int tj) {
+// units g0, g0 + gstride, ... below `end` (unit g = block g / NB, Philox block g % NB), the block and
+// Philox index carried from unit to unit (wave-uniform: no 64-bit division per unit; g < 2^31,
+// mppi_create bounds K)
+__device__ __forceinline__ void noise_rows(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int end,
+                                           float* __restrict__ eps, int g0, int gstride, int tj) {
   const int NB = (H + 1) >> 1;
-  for (int64_t g = g0; g < (int64_t)n_blocks * NB; g += gstride) noise_unit(seed, n_base, k_offset, H, g, eps, tj);
+  if (g0 >= end) return;
+  int blk = g0 / NB, n = g0 - blk * NB;
+  const int sq = gstride / NB, sr = gstride - sq * NB;
+  for (int g = g0; g < end; g += gstride) {
+    noise_unit(seed, n_base, k_offset, H, blk, n, eps, tj);
+    blk += sq;
+    n += sr;
+    if (n >= NB) {
+      n -= NB;
+      ++blk;
+    }
+  }
 }
 __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t n_base, int64_t k_offset,
                                                          int H, int n_blocks, float* __restrict__ eps) {
-  noise_rows(seed, n_base, k_offset, H, n_blocks, eps, blockIdx.x, gridDim.x, threadIdx.x);
+  noise_rows(seed, n_base, k_offset, H, n_blocks * ((H + 1) >> 1), eps, blockIdx.x, gridDim.x, threadIdx.x);
 }
 
 // =====================================================================  resident step server
@@ -3779,7 +3789,9 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
     if (tid < 64) {
       // workgroup 0 polls the pinned command (seq and stop in one 8-byte read) and relays it: the
       // command words to relay[16..], then (after they completed) seq / stop to relay[0..1]; the
-      // others poll relay[0..1] in device memory.  An idle workgroup 0 relays a stop.
+      // others poll relay[0..1] in device memory.  An idle workgroup 0 relays a stop.  The relay's
+      // stop word is this launch's first seq (a stale one from an earlier launch never matches), so
+      // the host launches without resetting the relay.
       const bool head = blockIdx.x == 0;
       const unsigned long long* src = head ? reinterpret_cast<const unsigned long long*>(z.cmd)
                                            : reinterpret_cast<const unsigned long long*>(z.relay);
@@ -3794,7 +3806,8 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
             ok = 1;
             break;
           }
-          if ((w >> 32) != 0 || __builtin_amdgcn_s_memrealtime() - t0 >= z.idle_ticks) break;
+          const bool stop = head ? (w >> 32) != 0 : (unsigned)(w >> 32) == z.first_seq;
+          if (stop || __builtin_amdgcn_s_memrealtime() - t0 >= z.idle_ticks) break;
           if (!head) __builtin_amdgcn_s_sleep(8);  // (~0.2 us: 255 pollers of one word stay off the rollout's way)
         }
       }
@@ -3817,7 +3830,7 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
           if (ok)
             __hip_atomic_store(z.relay, cmd_lds[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           else
-            __hip_atomic_store(z.relay + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(z.relay + 1, z.first_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       if (tid == 0) cmd_lds[31] = ok;
@@ -3855,9 +3868,10 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
     const int ticket = roles_body<TB, PROJ, 0, false, true>(a, z.rec_cnt, sh);
     if (ticket == z.nroll - 1 && tid == 0 && z.clk) z.clk[kClkServer + 8 * (seq & 7) + 1] = __builtin_amdgcn_s_memrealtime();
     const int blk = ticket - (z.nroll - z.fin_groups);
-    if (blk < 0 && c.noise_slot >= 0) {
+    if (blk < 0 && c.noise_slot >= 0 && blockIdx.x != 0) {
       // the normals of a later step (c.noise_n_base, into slot c.noise_slot) while the finish
-      // workgroups reduce the records and the host turns the step around: chunks of kNoiseChunk
+      // workgroups reduce the records and the host turns the step around (not workgroup 0, which
+      // goes back to polling for the next command at once): chunks of kNoiseChunk
       // units claimed from this step's counter (rec_cnt[1 + seq % 2], zeroed by the finish of the
       // step after), four 256-trajectory units per pass
       __builtin_amdgcn_s_setprio(0);
@@ -3874,9 +3888,9 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
         const int64_t u0 = sh[1];
         __syncthreads();
         if (u0 >= U) break;
-        const int64_t u1 = min(u0 + kNoiseChunk, U);
-        for (int64_t g = u0 + (tid >> 8); g < u1; g += NROLES * TB / 256)
-          noise_unit(a.seed, nbase, a.k_offset, a.H, g, eps_out, tid & 255);
+        const int u1 = (int)min(u0 + kNoiseChunk, U);
+        noise_rows(a.seed, nbase, a.k_offset, a.H, u1, eps_out, (int)u0 + __builtin_amdgcn_readfirstlane(tid >> 8),
+                   NROLES * TB / 256, tid & 255);
       }
       if (tid == 0 && z.clk)
         __hip_atomic_fetch_max(z.clk + kClkServer + 8 * (seq & 7) + 3, (uint64_t)__builtin_amdgcn_s_memrealtime(),

@@ -117,6 +117,20 @@ def test_server_closed_loop_states(async_tail):
     assert i_got["resident"] == 1 and i_got["server_launches"] == 1 and i_got["server_steps"] == 5, i_got
 
 
+@pytest.mark.parametrize("K", [2048, 8192, 16384])
+@pytest.mark.parametrize("async_tail", [False, True], ids=["sync", "deferred-tail"])
+def test_server_few_records(K, async_tail):
+    """Few leaf records (8 / 32 / 64): every rollout workgroup may hold a finish column, so the
+    normals of step + 2 come from the noise kernel instead of the server's noise phase (8 and 32
+    records) or from the few workgroups outside the finish (64).  Five steps with the nominal
+    sequence carried across them equal the separate launches."""
+    i_got = {}
+    ref = _run(K, 40, opts={"resident": 0}, steps=5, async_tail=async_tail, states=True)
+    got = _run(K, 40, steps=5, async_tail=async_tail, states=True, info=i_got)
+    _same(got, ref, f"K={K} async={async_tail}")
+    assert i_got["resident"] == 1 and i_got["server_steps"] == 5, i_got
+
+
 def test_server_idle_exit_and_stop():
     """The server leaves after its idle limit and is relaunched by the next step; a call that stops it
     (mppi_get_costs) between steps, too.  Every step equals the separate launches."""
