@@ -26,7 +26,6 @@ struct ServerCmd {
 };
 constexpr int kTailSlots = 4;                 // deferred optimal rollouts in flight (mppi_capi.cpp)
 constexpr int kCmdWords = 25;                 // the words a step reads (seq .. noise_n_base_hi)
-constexpr int kNoiseChunk = 16;               // noise units a server workgroup claims at a time
 constexpr unsigned kDoneFail = 0x80000000u;   // done | kDoneFail: the step's finish gave up
 struct FinishArgs {
   int H;
@@ -163,17 +162,17 @@ constexpr int ROLES_WAVES_PER_TRAJ_WAVE = 4;
 // then it exits), runs its rollout and writes its record through, and takes a ticket from rec_cnt;
 // the workgroups holding the last fin_groups tickets run the column-split finish (each after rec_cnt
 // reaches nroll, or wait_ticks: then the step publishes done | kDoneFail); the other workgroups
-// generate the normals of step + 2 meanwhile (ServerCmd::noise_slot).  Only workgroup
+// generate the normals of step + 2 meanwhile (ServerCmd::noise_slot, a static share per ticket;
+// workgroup 0's first wave keeps out of it).  Only workgroup
 // 0 polls the pinned command (256 workgroups polling host memory cost ~30 us per step, one ~4 us:
 // profiles/ubench/server.hip); it relays the command words and seq / stop through device memory.
 struct ServerArgs {
   FinishArgs f;
   int nroll, fin_P, fin_ncol, fin_groups;
-  unsigned* rec_cnt;          // [0] records counted, [1 + seq % 2] noise units claimed; zeroed, re-armed by
-                              // the finish (the noise counter of the step before)
+  unsigned* rec_cnt;          // [0] records counted; zeroed, re-armed by the finish
   const ServerCmd* cmd;       // pinned host memory (polled by workgroup 0 only)
-  unsigned* relay;            // device: [0] seq, [1] stop as relayed by workgroup 0, [16, 16 + kCmdWords) the
-                              // command words (zeroed before the launch)
+  unsigned* relay;            // device: [0] seq, [1] stop (the first_seq of the launch that stopped) as relayed
+                              // by workgroup 0, [16, 16 + kCmdWords) the command words
   float* eps[3];              // the normals slots
   float* u_nom[2];            // the nominal double buffer, [2H] each
   float* tail_in[kTailSlots];   // deferred optimal rollout inputs per slot (device)

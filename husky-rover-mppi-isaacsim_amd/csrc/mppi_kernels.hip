@@ -2168,6 +2168,12 @@ __device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>
 // chain3d_lean's.  Writes x, y (0, 1), n (6..8) and the new heading (9..11) of each step into
 // chain[12 t ..] (lane 0).
 constexpr int TAIL_WIN = 8, TAIL_WIN_LO = 3;  // neighbourhood cells [c - 3, c + 4] per axis
+// Every lane computes the same values, so the cell of a position is taken wave-uniform (readfirstlane):
+// the neighbourhood test, the source lane and the table offset are scalar, the test is a scalar
+// branch (no exec-mask divergence), and the rest of the step is the rollout chain's (orient_step,
+// then advance_step<true, false> of the next position, both redone with IEEE operators if the guards
+// fail).  Each step's v / sin / cos are read one step ahead.  Every lane stores the step's record
+// (same values, same LDS words).
 __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem<false>& dem, const float* vb,
                                               const float* snb, const float* csb, float* chain, int H, int lane,
                                               const float* qpre) {
@@ -2176,7 +2182,7 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem<fal
   const float4* ntab0 = dem.N + (f.grid + 2);  // entry (jj, ii) = (1 - tjj, ti + 1): offset ti - tjj * (grid + 1)
   const int nrow = f.grid + 1;
   const int ldx = (lane % TAIL_WIN) - TAIL_WIN_LO, ldy = (lane / TAIL_WIN) - TAIL_WIN_LO;
-  // (ti, tjj) of the cell holding pos: min(i, grid - 1), -min(j, rows - 1) (Dem::cell)
+  // (ti, tjj) of the cell holding pos: min(i, grid - 1), -min(j, rows - 1) (Dem::cell), wave-uniform
   auto cell_of = [&](f2 pos, int& ti, int& tjj) __attribute__((always_inline)) {
     f2 q;
     if (dem.cdiv) {
@@ -2187,29 +2193,32 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem<fal
     } else {
       q = f2{(pos.x - f.x_min) / f.res, (pos.y + f.y_min) / f.res};
     }
-    ti = (int)__builtin_amdgcn_fmed3f(q.x, -1.0f, fi_hi);
-    tjj = (int)__builtin_amdgcn_fmed3f(q.y, fj_lo, 1.0f);
+    ti = __builtin_amdgcn_readfirstlane((int)__builtin_amdgcn_fmed3f(q.x, -1.0f, fi_hi));
+    tjj = __builtin_amdgcn_readfirstlane((int)__builtin_amdgcn_fmed3f(q.y, fj_lo, 1.0f));
   };
   // this lane's cell of the neighbourhood centred on (ti, tjj): its table offset, load issued
+  // (|tjj|, nrow < 2^23 and the table < 4 GiB: 24-bit multiplies, as the rollout chain)
   auto issue = [&](int ti, int tjj, int& lo, float4& w) __attribute__((always_inline)) {
     const int ci = min(max(ti + ldx, -1), f.grid - 1);
     const int cj = min(max(tjj + ldy, 1 - f.rows), 1);
-    lo = ci - cj * nrow;
+    lo = ci - __mul24(cj, nrow);
     w = ntab0[lo];
   };
-  // the normal of (ti, tjj) from the neighbourhood centred on (cti, ctjj)
+  // the normal of (ti, tjj) from the neighbourhood centred on (cti, ctjj) (all scalar but the loads)
   auto pick = [&](int ti, int tjj, int cti, int ctjj, int lo, const float4& w) __attribute__((always_inline)) {
-    const int to = ti - tjj * nrow;
+    const int to = ti - __mul24(tjj, nrow);
     const int dx = ti - cti + TAIL_WIN_LO, dy = tjj - ctjj + TAIL_WIN_LO;
-    const int src = __builtin_amdgcn_readfirstlane(dy * TAIL_WIN + dx);
-    const bool in = ((unsigned)dx < (unsigned)TAIL_WIN) & ((unsigned)dy < (unsigned)TAIL_WIN);
+    const int src = (dy * TAIL_WIN + dx) & 63;
     float3 n;
-    if (in && __builtin_amdgcn_readlane(lo, src & 63) == to) {
-      n.x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w.x), src & 63));
-      n.y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w.y), src & 63));
-      n.z = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w.z), src & 63));
-    } else {
-      const float4 d = ntab0[to];
+    if (((unsigned)dx < (unsigned)TAIL_WIN) & ((unsigned)dy < (unsigned)TAIL_WIN) &&
+        __builtin_amdgcn_readlane(lo, src) == to) {
+      n.x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w.x), src));
+      n.y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w.y), src));
+      n.z = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w.z), src));
+    } else {  // outside the neighbourhood: a vector load of the entry (the offset through a VGPR)
+      int tv = to;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(to));
+      const float4 d = ntab0[tv];
       n = make_float3(d.x, d.y, d.z);
     }
     return n;
@@ -2217,25 +2226,32 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem<fal
   const Traj s0 = initial_pose(f, dem, qpre);
   Head hd{f2{s0.hx, s0.hy}, s0.hz};
   f2 pos = f2{s0.x, s0.y};
-  int tiA, tjjA, tiB, tjjB, loA, loB;
+  {  // step 0's position (guarded: the heading comes from the IEEE initial pose)
+    Lean la;
+    lean_init(la);
+    f2 p = advance_step<true>(hd, vb[0], f.dt, pos, la);
+    if (__builtin_expect(lean_bad(la), 0)) p = advance_step<false>(hd, vb[0], f.dt, pos, la);
+    pos = p;
+  }
+  int ti, tjj;
+  cell_of(pos, ti, tjj);
+  int tiA = ti, tjjA = tjj, tiB = ti, tjjB = tjj, loA, loB;  // neighbourhoods of steps 0 and 1: around step 0
   float4 wA, wB;
-  cell_of(pos, tiA, tjjA);  // the neighbourhoods of steps 0 and 1: around the start
-  tiB = tiA;
-  tjjB = tjjA;
   issue(tiA, tjjA, loA, wA);
   loB = loA;
   wB = wA;
-  // step t: position, normal from neighbourhood X (centred two steps back), refill X around
-  // this step's cell for step t + 2, orientation, record
-  auto step = [&](int t, int& ctiX, int& ctjjX, int& loX, float4& wX) __attribute__((always_inline)) {
-    const float v = vb[t], sn = snb[t], cs = csb[t];
-    Lean la;
-    lean_init(la);
-    f2 p = advance_step<true>(hd, v, f.dt, pos, la);
-    if (__builtin_expect(lean_bad(la), 0)) p = advance_step<false>(hd, v, f.dt, pos, la);
-    pos = p;
-    int ti, tjj;
-    cell_of(pos, ti, tjj);
+  float vn = H > 1 ? vb[1] : 0.f, snn = snb[0], csn = csb[0];
+  // step t (position known, its cell (ti, tjj)): normal from neighbourhood X (centred two steps
+  // back), refill X around this cell for step t + 2, orientation, record, next position and cell
+  auto step = [&](auto more_tag, int t, int& ctiX, int& ctjjX, int& loX, float4& wX) __attribute__((always_inline)) {
+    constexpr bool more = decltype(more_tag)::value;
+    const float v1 = vn, sn = snn, cs = csn;
+    if constexpr (more) {  // the next step's inputs, one step ahead
+      const int t2 = min(t + 2, H - 1);
+      vn = vb[t2];
+      snn = snb[t + 1];
+      csn = csb[t + 1];
+    }
     const float3 n = pick(ti, tjj, ctiX, ctjjX, loX, wX);
     ctiX = ti;
     ctjjX = tjj;
@@ -2245,21 +2261,35 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem<fal
     Lean l;
     lean_init(l);
     Head ho = orient_step<true>(nxy, n.z, hd, sn, cs, omc, l);
-    if (__builtin_expect(lean_bad(l), 0)) ho = orient_step<false>(nxy, n.z, hd, sn, cs, omc, l);
+    f2 p1 = pos;
+    if constexpr (more) p1 = advance_step<true, false>(ho, v1, f.dt, pos, l);
+    if (__builtin_expect(lean_bad(l), 0)) {
+      ho = orient_step<false>(nxy, n.z, hd, sn, cs, omc, l);
+      if constexpr (more) p1 = advance_step<false>(ho, v1, f.dt, pos, l);
+    }
+    float* ch = chain + 12 * t;
+    ch[0] = pos.x; ch[1] = pos.y;
+    ch[6] = n.x; ch[7] = n.y; ch[8] = n.z;
+    ch[9] = ho.xy.x; ch[10] = ho.xy.y; ch[11] = ho.z;
     hd = ho;
-    if (lane == 0) {
-      float* ch = chain + 12 * t;
-      ch[0] = pos.x; ch[1] = pos.y;
-      ch[6] = n.x; ch[7] = n.y; ch[8] = n.z;
-      ch[9] = ho.xy.x; ch[10] = ho.xy.y; ch[11] = ho.z;
+    if constexpr (more) {
+      pos = p1;
+      cell_of(pos, ti, tjj);
     }
   };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
   int t = 0;
-  for (; t + 1 < H; t += 2) {
-    step(t, tiA, tjjA, loA, wA);
-    step(t + 1, tiB, tjjB, loB, wB);
+  for (; t + 2 < H; t += 2) {
+    step(T_{}, t, tiA, tjjA, loA, wA);
+    step(T_{}, t + 1, tiB, tjjB, loB, wB);
   }
-  if (t < H) step(t, tiA, tjjA, loA, wA);
+  if (t + 1 < H) {
+    step(T_{}, t, tiA, tjjA, loA, wA);
+    step(F_{}, t + 1, tiB, tjjB, loB, wB);
+  } else {
+    step(F_{}, t, tiA, tjjA, loA, wA);
+  }
 }
 
 // Step 0 of the optimal rollout on one lane (no barrier): traj | hv | lw | rw of the
@@ -2980,10 +3010,7 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
   if (nblk == 1) {
     if (tid < 2 * H) ures = (S > 0.0) ? (float)(part[(tid + 2) * NG] / S) : 0.0f;
     __syncthreads();
-    if (RECS_WT && tid == 0) {  // (and the noise counter of the step before: every claim on it is done)
-      __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(rec_cnt + 1 + ((f.seq - 1) & 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (RECS_WT && tid == 0) __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     const unsigned long long tag = (unsigned long long)f.seq << 32;
     for (int c = tid; c < nc; c += FIN_THREADS) {
@@ -3018,10 +3045,7 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
     FINWG_STAMP(blk, 1);
 #endif
     // every finish workgroup has passed its record wait (resident server): re-arm the count
-    if (RECS_WT && tid == 0) {  // (and the noise counter of the step before: every claim on it is done)
-      __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(rec_cnt + 1 + ((f.seq - 1) & 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (RECS_WT && tid == 0) __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #ifdef MPPI_STAMPS
   FIN_STAMP(13);
@@ -3740,6 +3764,27 @@ __device__ __forceinline__ void noise_rows(uint64_t seed, uint64_t n_base, int64
     }
   }
 }
+// wave-units q0, q0 + stride, ... below q1 (wave-unit q = trajectories 64 (q % 4) .. + 63 of unit
+// q / 4), the unit's block and Philox index carried (all wave-uniform)
+__device__ __forceinline__ void noise_waves(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int q, int q1,
+                                            int stride, float* __restrict__ eps, int lane) {
+  const int NB = (H + 1) >> 1;
+  if (q >= q1) return;
+  int g = q >> 2;
+  int blk = g / NB, n = g - blk * NB;
+  for (;;) {
+    noise_unit(seed, n_base, k_offset, H, blk, n, eps, ((q & 3) << 6) + lane);
+    const int q2 = q + stride;
+    if (q2 >= q1) break;
+    n += (q2 >> 2) - g;
+    g = q2 >> 2;
+    q = q2;
+    while (n >= NB) {
+      n -= NB;
+      ++blk;
+    }
+  }
+}
 __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t n_base, int64_t k_offset,
                                                          int H, int n_blocks, float* __restrict__ eps) {
   noise_rows(seed, n_base, k_offset, H, n_blocks * ((H + 1) >> 1), eps, blockIdx.x, gridDim.x, threadIdx.x);
@@ -3868,29 +3913,24 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
     const int ticket = roles_body<TB, PROJ, 0, false, true>(a, z.rec_cnt, sh);
     if (ticket == z.nroll - 1 && tid == 0 && z.clk) z.clk[kClkServer + 8 * (seq & 7) + 1] = __builtin_amdgcn_s_memrealtime();
     const int blk = ticket - (z.nroll - z.fin_groups);
-    if (blk < 0 && c.noise_slot >= 0 && blockIdx.x != 0) {
+    if (blk < 0 && c.noise_slot >= 0) {
       // the normals of a later step (c.noise_n_base, into slot c.noise_slot) while the finish
-      // workgroups reduce the records and the host turns the step around (not workgroup 0, which
-      // goes back to polling for the next command at once): chunks of kNoiseChunk
-      // units claimed from this step's counter (rec_cnt[1 + seq % 2], zeroed by the finish of the
-      // step after), four 256-trajectory units per pass
+      // workgroups reduce the records and the host turns the step around.  A static share per
+      // noise workgroup (its ticket t < nn = nroll - fin_groups: wave-units [t 4U / nn, (t + 1) 4U
+      // / nn), a wave-unit = one Philox block of 64 trajectories), no claims: workgroup 0's wave 0
+      // skips it and goes back to polling for the next command, its other 15 waves take its share
       __builtin_amdgcn_s_setprio(0);
-      const int nslot = __builtin_amdgcn_readfirstlane(c.noise_slot);
-      const uint64_t nbase = ((uint64_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_hi) << 32) |
-                             (uint32_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_lo);
-      const int64_t U = (int64_t)z.nroll * ((a.H + 1) >> 1);
-      float* eps_out = z.eps[nslot];
-      unsigned* ctr = z.rec_cnt + 1 + (seq & 1);
-      for (;;) {
-        if (tid == 0) sh[1] = (int)__hip_atomic_fetch_add(ctr, (unsigned)kNoiseChunk, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const int64_t u0 = sh[1];
-        __syncthreads();
-        if (u0 >= U) break;
-        const int u1 = (int)min(u0 + kNoiseChunk, U);
-        noise_rows(a.seed, nbase, a.k_offset, a.H, u1, eps_out, (int)u0 + __builtin_amdgcn_readfirstlane(tid >> 8),
-                   NROLES * TB / 256, tid & 255);
+      const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+      const bool w0 = blockIdx.x == 0;
+      if (!(w0 && wave == 0)) {
+        const int nslot = __builtin_amdgcn_readfirstlane(c.noise_slot);
+        const uint64_t nbase = ((uint64_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_hi) << 32) |
+                               (uint32_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_lo);
+        const int64_t W = 4 * (int64_t)z.nroll * ((a.H + 1) >> 1);
+        const int nn = z.nroll - z.fin_groups;
+        const int q0 = (int)(W * ticket / nn), q1 = (int)(W * (ticket + 1) / nn);
+        noise_waves(a.seed, nbase, a.k_offset, a.H, q0 + (w0 ? wave - 1 : wave), q1, w0 ? NROLES * TB / 64 - 1 : NROLES * TB / 64,
+                    z.eps[nslot], tid & 63);
       }
       if (tid == 0 && z.clk)
         __hip_atomic_fetch_max(z.clk + kClkServer + 8 * (seq & 7) + 3, (uint64_t)__builtin_amdgcn_s_memrealtime(),

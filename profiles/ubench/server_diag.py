@@ -48,12 +48,14 @@ for async_tail, ts in ((True, 1), (True, 2), (False, 1)):
           (rec.min(), *np.percentile(rec, [10, 50, 90]), rec.max()))
     st = np.array([[v[266 + 8 * r + k] for k in range(8)] for r in range(8)])
     print("  server timeline, last 8 steps (us): [cmd seen, rollout = last ticket - cmd, finish = done - last ticket, "
-          "noise end - done, next cmd - done, tail: gate - done, run]")
+          "noise end - done, next cmd - done, wg0 poll start - done, tail: gate - done, run]")
     for r in range(8):
         cmd, tick, done, nz, tg, te = st[r, :6]
         nxt = st[r + 1, 0] if r < 7 else 0.0
-        print("    %8.1f  roll %6.1f  fin %6.1f  noise %+6.1f  turn %6.1f  tail %6.1f %6.1f" % (
+        pol = st[r + 1, 6] if r < 7 else 0.0
+        print("    %8.1f  roll %6.1f  fin %6.1f  noise %+6.1f  turn %6.1f  poll %+6.1f  tail %6.1f %6.1f" % (
             cmd, tick - cmd, done - tick, (nz - done) if nz else float("nan"), (nxt - done) if nxt else float("nan"),
+            (pol - done) if pol else float("nan"),
             (tg - done) if tg else float("nan"), (te - tg) if te else float("nan")))
     eng.close()
     print(f"async_tail={async_tail} tail_streams={ts}: " + "  ".join(f"[{i} step {a:.0f} out {b:.0f} L{l}]" for i, a, b, l in rows))
