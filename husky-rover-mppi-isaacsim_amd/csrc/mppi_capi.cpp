@@ -124,6 +124,8 @@ struct mppi_ctx {
   bool trace = false;
   double tr_prev_done = 0, tr_sum[4] = {0, 0, 0, 0}, tr_t0 = 0, tr_t1 = 0;
   double tr_srv[4] = {0, 0, 0, 0};  // server steps: stop / relaunch, normals wait, tail-slot wait, side launches
+  double tr_log[8][5] = {};  // last 8 steps: call, command written, side launches done, completion seen, return
+  int tr_slot = 0;
   long tr_n = 0;
   int roles = -1;     // rollout kernel: -1 auto (role split at <= 1 workgroup per CU), 0 pair, 1 roles (MPPI_ROLES)
   // Resident step server (mppi_step_server_kernel): sampled steps of the role-split plan run on one
@@ -140,7 +142,8 @@ struct mppi_ctx {
   uint64_t srv_idle_us = 2000;
   int64_t srv_launches = 0, srv_steps = 0, srv_failed = 0;
   uint64_t fin_wait_ticks = 200000000ull;  // a finish's record wait bound (2 s at 100 MHz; mppi_set_option)
-  int tail_streams = 2;  // server: deferred tails alternating over 2 streams, or on 1 (mppi_set_option "tail_streams")
+  int tail_streams = kTailSlots;  // server: deferred tails round-robin over this many streams (one per slot by
+                                  // default; mppi_set_option "tail_streams": 1, 2 or 4)
   // the server's tail of the last step, launched once its completion word was seen (at the next
   // step's command, or when its outputs are wanted): no kernel waits on the GPU for its inputs
   bool tail_deferred = false;
@@ -177,6 +180,7 @@ struct mppi_ctx {
   // deferred optimal rollout (mppi_set_async_tail): side stream + buffers
   bool async_tail = false;
   hipStream_t tail_stream = nullptr;
+  hipStream_t tail_more[kTailSlots - 1] = {};  // the server's other tail streams
   hipEvent_t ev_fin_done = nullptr;
   hipEvent_t ev_tail[kTailSlots] = {};  // per slot: tail done
   bool tail_pending = false;       // the latest tail's outputs are not merged into out_host yet
@@ -746,12 +750,14 @@ int prepare_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, int mode, 
 }
 
 // The deferred optimal rollout on a side stream: after the context stream's finish (event), or, for
-// the resident server (its finish has published: f.clk set), at once.  The server's tails alternate
-// over the tail and the noise stream (tail_streams = 2): beside a server workgroup a tail takes
-// about a step period, so two may run at once (each beside its own workgroup).
+// the resident server (its finish has published: f.clk set), at once.  The server's tails go to the
+// stream of their slot (tail_streams = 4): beside a server workgroup a tail takes about two step
+// periods (~175 us against ~52 us alone at C3), so on one or two streams each waited for the one
+// before it and the host for the slot (measured: every other command ~15 us late with two).
 int enqueue_tail(mppi_ctx* c, const FinishArgs& f, int par) {
   const bool server = f.clk != nullptr;
-  hipStream_t ts = (server && c->tail_streams == 2 && (par & 1)) ? c->noise_stream : c->tail_stream;
+  const int si = server ? par % c->tail_streams : 0;
+  hipStream_t ts = si == 0 ? c->tail_stream : c->tail_more[si - 1];
   if (!server) {
     HIP_TRY(hipEventRecord(c->ev_fin_done, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->tail_stream, c->ev_fin_done, 0));
@@ -931,7 +937,7 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   // normals of step + 1 (normally generated by the previous step's noise phase; else now, on the
   // noise stream beside this step) and of step + 2 (by this step's noise phase, in the server)
   const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
-  // the noise phase runs in the workgroups outside the finish but workgroup 0: with fewer than a
+  // the server's noise phase runs mostly in the workgroups outside the finish: with fewer than a
   // quarter of them, or fewer than two (few records: every rollout workgroup may hold a finish
   // column) the noise kernel does it
   const bool srv_noise = pl.blocks - groups >= 2 && (int64_t)(pl.blocks - groups) * 4 >= (int64_t)pl.blocks;
@@ -1044,7 +1050,15 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
     c->tail_deferred = true;
     c->tail_def_par = par;
   }
-  if (c->trace) c->tr_srv[3] += now_us() - tl;
+  if (c->trace) {
+    const double tn = now_us();
+    c->tr_srv[3] += tn - tl;
+    c->tr_slot = (int)(c->srv_steps & 7);
+    double* lg = c->tr_log[c->tr_slot];
+    lg[0] = c->tr_t0;
+    lg[1] = c->srv_last_us;
+    lg[2] = tn;
+  }
   return MPPI_OK;
 }
 
@@ -1085,6 +1099,10 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
     ++c->tr_n;
   }
   c->tr_prev_done = t3;
+  if (c->last_resident) {
+    c->tr_log[c->tr_slot][3] = t3;  // (copy_outputs returns right after the completion word)
+    c->tr_log[c->tr_slot][4] = now_us();
+  }
   return rc;
 }
 
@@ -1259,6 +1277,9 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
     if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(MPPI_EHIP, "hipEventCreate failed"));
   if (hipEventCreateWithFlags(&c->ev_fin_done, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->tail_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->tail_more[0], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->tail_more[1], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->tail_more[2], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithPriority(&c->noise_stream, hipStreamNonBlocking, c->prio_least) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_prev_roll, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->eps_ev[0], hipEventDisableTiming) != hipSuccess ||
@@ -1289,10 +1310,20 @@ void mppi_destroy(mppi_ctx* c) {
                    "tail slot wait %.1f  noise+tail launches %.1f  (server launches %ld)\n", (long)c->srv_steps,
                    c->tr_srv[0] / c->srv_steps, c->tr_srv[1] / c->srv_steps, c->tr_srv[2] / c->srv_steps,
                    c->tr_srv[3] / c->srv_steps, (long)c->srv_launches);
+    if (c->srv_steps > 0) {  // the last 8 steps, us from the first: call, command, launches, completion, return
+      const double o = c->tr_log[(c->tr_slot + 1) & 7][0];
+      for (int r = 0; r < 8; ++r) {
+        const double* lg = c->tr_log[(c->tr_slot + 1 + r) & 7];
+        std::fprintf(stderr, "  host step: call %8.1f  cmd %+6.1f  launches %+6.1f  done seen %+6.1f  return %+6.1f\n",
+                     lg[0] - o, lg[1] - lg[0], lg[2] - lg[0], lg[3] - lg[0], lg[4] - lg[0]);
+      }
+    }
   }
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->tail_stream) hipStreamSynchronize(c->tail_stream);
+  for (hipStream_t t : c->tail_more)
+    if (t) hipStreamSynchronize(t);
   if (c->noise_stream) hipStreamSynchronize(c->noise_stream);
   if (c->Z_owned && c->Z) hipFree(c->Z);
   if (c->ntab) hipFree(c->ntab);
@@ -1336,6 +1367,8 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->bin_ci) hipFree(c->bin_ci);
   if (c->noise_stream) hipStreamDestroy(c->noise_stream);
   if (c->tail_stream) hipStreamDestroy(c->tail_stream);
+  for (hipStream_t t : c->tail_more)
+    if (t) hipStreamDestroy(t);
   if (c->inj1) hipFree(c->inj1);
   if (c->inj2) hipFree(c->inj2);
   for (auto& e : c->ev)
@@ -1620,8 +1653,8 @@ int mppi_set_option(mppi_ctx* c, const char* name, int64_t value) {
     c->srv_idle_us = (uint64_t)value;
     return MPPI_OK;
   }
-  if (n == "tail_streams") {  // the server's deferred tails on 1 stream or alternating over 2
-    if (value != 1 && value != 2) return fail(MPPI_EINVAL, "tail_streams must be 1 or 2");
+  if (n == "tail_streams") {  // the server's deferred tails round-robin over 1, 2 or 4 streams
+    if (value != 1 && value != 2 && value != 4) return fail(MPPI_EINVAL, "tail_streams must be 1, 2 or 4");
     c->tail_streams = (int)value;
     return MPPI_OK;
   }
@@ -1732,6 +1765,13 @@ int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
       const uint64_t x = v[kClkServer + 8 * ((last + 1 + r) & 7) + k];
       if (idx < n) out[idx] = x && lo != UINT64_MAX ? (double)(x - lo) / 100.0 : 0.0;
     }
+  // then (diagnostic builds with MPPI_DIAG_W0) workgroup 0's per-wave stamps of its last step: 16
+  // noise ends, 16 end-of-step arrivals (same origin), then that step's seq
+  for (int k = 0; k < 33; ++k) {
+    const int idx = 10 + nb + 64 + k;
+    const uint64_t x = v[kClkBase + 2 * 4000 + k];
+    if (idx < n) out[idx] = k == 32 ? (double)x : (x && lo != UINT64_MAX ? ((double)x - (double)lo) / 100.0 : 0.0);
+  }
   return MPPI_OK;
 }
 

@@ -123,9 +123,9 @@ struct RolloutArgs {
 // s_memrealtime when workgroup b (< kClkBlocks) starts and when its record is written
 constexpr int kClkBase = 8, kClkBlocks = 4096;
 // then (resident server) s_memrealtime per step, ring of 8 steps: [kClkServer + 8 (seq % 8) + k], k =
-// 0 workgroup 0 saw the command, 1 the last rollout ticket, 2 the completion word stored, 3 the
-// latest end of a noise phase (atomic max), 4 the deferred tail started, 5 the tail ended,
-// 6 workgroup 0 started polling for the command
+// 0 the head saw the command, 1 the last rollout ticket, 2 the completion word stored, 3 the
+// latest end of a noise share (atomic max), 4 the deferred tail started, 5 the tail ended,
+// 6 the head started polling for the command, 7 the latest end of any workgroup's step
 constexpr int kClkServer = kClkBase + 2 * kClkBlocks, kClkWords = kClkServer + 64;
 // The finish's phase-2 LDS (finish_phase2): uo[2][PS] v w sin cos[H] chain[12H] out[16H]
 // lr[2][PS] floats, PS = the filter rows' stride (a multiple of 4 floats, >= H + 32 for the

@@ -890,6 +890,95 @@ __device__ __forceinline__ int thread_id() {
   return t;
 }
 
+// =====================================================================  sampling normals
+// The step's sampling normals (sampling_warp.py:54-92 with the Philox noise of DEFINED D1),
+// precomputed so the rollout's producer waves only load them.  Unit g = (block g / NB, Philox block
+// n = g % NB) for the trajectory tj of that block: eps1 / eps2 of steps t = 2n, 2n + 1, stored
+// write-through (agent scope, sc1): the rows do not sit dirty in the XCD's L2 (a later kernel
+// boundary would write them back) and other CUs read them after an L1 invalidate only.
+struct NoiseVals {
+  float a1, a2, b1, b2;
+};
+__device__ __forceinline__ NoiseVals noise_gen(uint64_t seed, uint64_t n_base, int64_t k_offset, int blk, int n, int tj) {
+  const uint64_t kg = (uint64_t)(k_offset + (int64_t)blk * 256 + tj);
+  NoiseVals v;
+  noise_block_pk(seed, n_base + (uint64_t)n, kg, &v.a1, &v.a2, &v.b1, &v.b2);
+  return v;
+}
+__device__ __forceinline__ void noise_store(float* __restrict__ eps, int H, int blk, int n, int tj, const NoiseVals& v) {
+  const int t = 2 * n;
+  float* e1 = eps + ((size_t)blk * 2 * H + t) * 256 + tj;
+  float* e2 = e1 + (size_t)H * 256;
+  __hip_atomic_store(e1, v.a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(e2, v.a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t + 1 < H) {
+    __hip_atomic_store(e1 + 256, v.b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(e2 + 256, v.b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__device__ __forceinline__ void noise_unit(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int blk, int n,
+                                           float* __restrict__ eps, int tj) {
+  noise_store(eps, H, blk, n, tj, noise_gen(seed, n_base, k_offset, blk, n, tj));
+}
+// units g0, g0 + gstride, ... below `end` (unit g = block g / NB, Philox block g % NB), the block and
+// Philox index carried from unit to unit (wave-uniform: no 64-bit division per unit; g < 2^31,
+// mppi_create bounds K)
+__device__ __forceinline__ void noise_rows(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int end,
+                                           float* __restrict__ eps, int g0, int gstride, int tj) {
+  const int NB = (H + 1) >> 1;
+  if (g0 >= end) return;
+  int blk = g0 / NB, n = g0 - blk * NB;
+  const int sq = gstride / NB, sr = gstride - sq * NB;
+  for (int g = g0; g < end; g += gstride) {
+    noise_unit(seed, n_base, k_offset, H, blk, n, eps, tj);
+    blk += sq;
+    n += sr;
+    if (n >= NB) {
+      n -= NB;
+      ++blk;
+    }
+  }
+}
+// wave-units q0, q0 + stride, ... below q1 (wave-unit q = trajectories 64 (q % 4) .. + 63 of unit
+// q / 4), two per iteration (independent Philox blocks: each one's dependent packed steps fill the
+// other's wait states), the units' block and Philox index carried (all wave-uniform)
+struct NoisePos {
+  int q, g, blk, n;
+};
+__device__ __forceinline__ void noise_pos_step(NoisePos& p, int stride, int NB) {
+  p.q += stride;
+  p.n += (p.q >> 2) - p.g;
+  p.g = p.q >> 2;
+  while (p.n >= NB) {
+    p.n -= NB;
+    ++p.blk;
+  }
+}
+__device__ __forceinline__ void noise_waves(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int q, int q1,
+                                            int stride, float* __restrict__ eps, int lane) {
+  const int NB = (H + 1) >> 1;
+  if (q >= q1) return;
+  NoisePos a;
+  a.q = q;
+  a.g = q >> 2;
+  a.blk = a.g / NB;
+  a.n = a.g - a.blk * NB;
+  for (;;) {
+    NoisePos b = a;
+    noise_pos_step(b, stride, NB);
+    const bool has_b = b.q < q1;
+    if (!has_b) b = a;  // (computed, not stored)
+    const NoiseVals va = noise_gen(seed, n_base, k_offset, a.blk, a.n, ((a.q & 3) << 6) + lane);
+    const NoiseVals vb = noise_gen(seed, n_base, k_offset, b.blk, b.n, ((b.q & 3) << 6) + lane);
+    noise_store(eps, H, a.blk, a.n, ((a.q & 3) << 6) + lane, va);
+    if (!has_b) break;
+    noise_store(eps, H, b.blk, b.n, ((b.q & 3) << 6) + lane, vb);
+    a = b;
+    noise_pos_step(a, stride, NB);
+    if (a.q >= q1) break;
+  }
+}
+
 // LDS row stride (floats) of the pair kernel's control cache: 256 trajectories + one float4 of
 // skew, so the leaf's lanes (one row each) hit different banks
 constexpr int UCACHE_ROW = 256 + 4;
@@ -3725,66 +3814,6 @@ hipError_t launch_normal_table(const float* Z, int rows, int grid, float res, fl
   return hipGetLastError();
 }
 
-// The step's sampling normals (sampling_warp.py:54-92 with the Philox noise of DEFINED D1),
-// precomputed so the rollout's producer waves only load them.  Unit g = (block g / NB, Philox block
-// n = g % NB) for the trajectory tj of that block: eps1 / eps2 of steps t = 2n, 2n + 1, stored
-// write-through (agent scope, sc1): the rows do not sit dirty in the XCD's L2 (a later kernel
-// boundary would write them back) and other CUs read them after an L1 invalidate only.
-__device__ __forceinline__ void noise_unit(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int blk, int n,
-                                           float* __restrict__ eps, int tj) {
-  const uint64_t kg = (uint64_t)(k_offset + (int64_t)blk * 256 + tj);
-  float a1, a2, b1, b2;
-  noise_block_pk(seed, n_base + (uint64_t)n, kg, &a1, &a2, &b1, &b2);
-  const int t = 2 * n;
-  float* e1 = eps + ((size_t)blk * 2 * H + t) * 256 + tj;
-  float* e2 = e1 + (size_t)H * 256;
-  __hip_atomic_store(e1, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(e2, a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t + 1 < H) {
-    __hip_atomic_store(e1 + 256, b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(e2 + 256, b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-// units g0, g0 + gstride, ... below `end` (unit g = block g / NB, Philox block g % NB), the block and
-// Philox index carried from unit to unit (wave-uniform: no 64-bit division per unit; g < 2^31,
-// mppi_create bounds K)
-__device__ __forceinline__ void noise_rows(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int end,
-                                           float* __restrict__ eps, int g0, int gstride, int tj) {
-  const int NB = (H + 1) >> 1;
-  if (g0 >= end) return;
-  int blk = g0 / NB, n = g0 - blk * NB;
-  const int sq = gstride / NB, sr = gstride - sq * NB;
-  for (int g = g0; g < end; g += gstride) {
-    noise_unit(seed, n_base, k_offset, H, blk, n, eps, tj);
-    blk += sq;
-    n += sr;
-    if (n >= NB) {
-      n -= NB;
-      ++blk;
-    }
-  }
-}
-// wave-units q0, q0 + stride, ... below q1 (wave-unit q = trajectories 64 (q % 4) .. + 63 of unit
-// q / 4), the unit's block and Philox index carried (all wave-uniform)
-__device__ __forceinline__ void noise_waves(uint64_t seed, uint64_t n_base, int64_t k_offset, int H, int q, int q1,
-                                            int stride, float* __restrict__ eps, int lane) {
-  const int NB = (H + 1) >> 1;
-  if (q >= q1) return;
-  int g = q >> 2;
-  int blk = g / NB, n = g - blk * NB;
-  for (;;) {
-    noise_unit(seed, n_base, k_offset, H, blk, n, eps, ((q & 3) << 6) + lane);
-    const int q2 = q + stride;
-    if (q2 >= q1) break;
-    n += (q2 >> 2) - g;
-    g = q2 >> 2;
-    q = q2;
-    while (n >= NB) {
-      n -= NB;
-      ++blk;
-    }
-  }
-}
 __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t n_base, int64_t k_offset,
                                                          int H, int n_blocks, float* __restrict__ eps) {
   noise_rows(seed, n_base, k_offset, H, n_blocks * ((H + 1) >> 1), eps, blockIdx.x, gridDim.x, threadIdx.x);
@@ -3828,16 +3857,19 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
   __shared__ int sh[2];
   const int tid = threadIdx.x;
   unsigned expect = args.z.first_seq;
+  // the head polls the pinned command and relays it: workgroup 0 for the first step of the launch,
+  // then the workgroup that took the previous step's last ticket (it ran the finish's phase 2 and
+  // published the completion word, so it is the first to be free)
+  bool head = blockIdx.x == 0;
   for (;;) {
     const auto* L = fresh_args();
     const ServerArgs& z = L->z;
     if (tid < 64) {
-      // workgroup 0 polls the pinned command (seq and stop in one 8-byte read) and relays it: the
+      // the head polls the pinned command (seq and stop in one 8-byte read) and relays it: the
       // command words to relay[16..], then (after they completed) seq / stop to relay[0..1]; the
-      // others poll relay[0..1] in device memory.  An idle workgroup 0 relays a stop.  The relay's
-      // stop word is this launch's first seq (a stale one from an earlier launch never matches), so
-      // the host launches without resetting the relay.
-      const bool head = blockIdx.x == 0;
+      // others poll relay[0..1] in device memory.  An idle head relays a stop.  The relay's stop
+      // word is this launch's first seq (a stale one from an earlier launch never matches), so the
+      // host launches without resetting the relay.
       const unsigned long long* src = head ? reinterpret_cast<const unsigned long long*>(z.cmd)
                                            : reinterpret_cast<const unsigned long long*>(z.relay);
       unsigned ok = 0;
@@ -3910,31 +3942,29 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
     a.pf_scale = rd(c.pf_scale);
     a.pf_far = __builtin_amdgcn_readfirstlane(c.pf_far);
     a.speed_on = __builtin_amdgcn_readfirstlane(c.speed_on);
+    const int nslot = __builtin_amdgcn_readfirstlane(c.noise_slot);
+    const uint64_t nbase = ((uint64_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_hi) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_lo);
+    // the normals of step + 2 (when commanded): W wave-units (one Philox block of 64 trajectories
+    // each) in S static shares, two per workgroup outside the finish (ticket t: shares 2t, 2t + 1,
+    // from its record on) and one per finish workgroup but the last (blk: share 2 nn + blk, after
+    // its columns, ~10 us later); the last finish workgroup runs phase 2 and heads the next poll
+    const int64_t W = 4 * (int64_t)z.nroll * ((a.H + 1) >> 1);
+    const int nn = z.nroll - z.fin_groups;
+    const int64_t S = 2 * (int64_t)nn + z.fin_groups - 1;
     const int ticket = roles_body<TB, PROJ, 0, false, true>(a, z.rec_cnt, sh);
     if (ticket == z.nroll - 1 && tid == 0 && z.clk) z.clk[kClkServer + 8 * (seq & 7) + 1] = __builtin_amdgcn_s_memrealtime();
     const int blk = ticket - (z.nroll - z.fin_groups);
-    if (blk < 0 && c.noise_slot >= 0) {
-      // the normals of a later step (c.noise_n_base, into slot c.noise_slot) while the finish
-      // workgroups reduce the records and the host turns the step around.  A static share per
-      // noise workgroup (its ticket t < nn = nroll - fin_groups: wave-units [t 4U / nn, (t + 1) 4U
-      // / nn), a wave-unit = one Philox block of 64 trajectories), no claims: workgroup 0's wave 0
-      // skips it and goes back to polling for the next command, its other 15 waves take its share
+    if (blk < 0 && nslot >= 0) {
+      // shares 2t, 2t + 1 of the normals of step + 2 while the finish workgroups reduce the records
+      // and the host turns the step around (static: no claims)
       __builtin_amdgcn_s_setprio(0);
       const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-      const bool w0 = blockIdx.x == 0;
-      if (!(w0 && wave == 0)) {
-        const int nslot = __builtin_amdgcn_readfirstlane(c.noise_slot);
-        const uint64_t nbase = ((uint64_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_hi) << 32) |
-                               (uint32_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_lo);
-        const int64_t W = 4 * (int64_t)z.nroll * ((a.H + 1) >> 1);
-        const int nn = z.nroll - z.fin_groups;
-        const int q0 = (int)(W * ticket / nn), q1 = (int)(W * (ticket + 1) / nn);
-        noise_waves(a.seed, nbase, a.k_offset, a.H, q0 + (w0 ? wave - 1 : wave), q1, w0 ? NROLES * TB / 64 - 1 : NROLES * TB / 64,
-                    z.eps[nslot], tid & 63);
-      }
-      if (tid == 0 && z.clk)
-        __hip_atomic_fetch_max(z.clk + kClkServer + 8 * (seq & 7) + 3, (uint64_t)__builtin_amdgcn_s_memrealtime(),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int q0 = (int)(W * (2 * ticket) / S), q1 = (int)(W * (2 * ticket + 2) / S);
+      noise_waves(a.seed, nbase, a.k_offset, a.H, q0 + wave, q1, NROLES * TB / 64, z.eps[nslot], tid & 63);
+#if defined(MPPI_DIAG_W0)  // diagnostic builds: workgroup 0's per-wave noise ends (unused block slots)
+      if (blockIdx.x == 0 && (tid & 63) == 0 && z.clk) z.clk[kClkBase + 2 * 4000 + wave] = __builtin_amdgcn_s_memrealtime();
+#endif
     }
     if (blk >= 0) {
       __builtin_amdgcn_s_setprio(0);  // the rollout waves' priorities do not carry into the finish
@@ -3977,12 +4007,29 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
       // a finish that gave up publishes the failure (the host stops the server and re-arms the count)
       if (!ok && tid == 0)
         __hip_atomic_store(z.f.done, seq | kDoneFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (nslot >= 0 && blk < z.fin_groups - 1) {  // its share of the normals of step + 2 (see above)
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int q0 = (int)(W * (2 * nn + blk) / S), q1 = (int)(W * (2 * nn + blk + 1) / S);
+        noise_waves(a.seed, nbase, a.k_offset, a.H, q0 + wave, q1, NROLES * TB / 64, z.eps[nslot], tid & 63);
+      }
     }
     // this CU's L1 forgets the step's normals rows before a later step reads rewritten ones
     // (asynchronous: the next poll's wait covers it)
+#if !defined(MPPI_DIAG_NOFENCE)  // (diagnostic builds: without the invalidate, to time it)
     if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
     expect = seq + 1;
+    head = ticket == z.nroll - 1;
+#if defined(MPPI_DIAG_W0)
+    if (blockIdx.x == 0 && (tid & 63) == 0 && z.clk) z.clk[kClkBase + 2 * 4000 + 16 + (tid >> 6)] = __builtin_amdgcn_s_memrealtime();
+    if (blockIdx.x == 0 && tid == 0 && z.clk) z.clk[kClkBase + 2 * 4000 + 32] = seq;
+#endif
     __syncthreads();  // every wave is done with this step's LDS and command words
+    if (tid == 0 && z.clk) {  // the latest end of a noise share (3) and of any workgroup's step (7)
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (blk < 0) __hip_atomic_fetch_max(z.clk + kClkServer + 8 * (seq & 7) + 3, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_max(z.clk + kClkServer + 8 * (seq & 7) + 7, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

@@ -290,7 +290,9 @@ int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
  *                        re-armed, so the next step is correct (0: give up at once, the test
  *                        hook).
  *   "record_tree_finish" 1: the record-tree finish (mppi_finish_kernel) at every record count
- *                        (default 0: the column-split finish wherever its shape fits). */
+ *                        (default 0: the column-split finish wherever its shape fits).
+ *   "tail_streams"       the server's deferred optimal rollouts round-robin over 1, 2 or 4
+ *                        side streams (default 4: one per tail slot, none waits for another). */
 int mppi_set_option(mppi_ctx* ctx, const char* name, int64_t value);
 int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_t* launches);
 /* HIP-event time of the deferred optimal-rollout kernels (side stream). */
