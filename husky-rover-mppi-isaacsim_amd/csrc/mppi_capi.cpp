@@ -142,8 +142,8 @@ struct mppi_ctx {
   uint64_t srv_idle_us = 2000;
   int64_t srv_launches = 0, srv_steps = 0, srv_failed = 0;
   uint64_t fin_wait_ticks = 200000000ull;  // a finish's record wait bound (2 s at 100 MHz; mppi_set_option)
-  int tail_streams = kTailSlots;  // server: deferred tails round-robin over this many streams (one per slot by
-                                  // default; mppi_set_option "tail_streams": 1, 2 or 4)
+  int tail_streams = 2;  // server: deferred tails alternating over the tail and the noise stream, or on the
+                         // tail stream only (mppi_set_option "tail_streams": 2 or 1)
   // the server's tail of the last step, launched once its completion word was seen (at the next
   // step's command, or when its outputs are wanted): no kernel waits on the GPU for its inputs
   bool tail_deferred = false;
@@ -180,7 +180,6 @@ struct mppi_ctx {
   // deferred optimal rollout (mppi_set_async_tail): side stream + buffers
   bool async_tail = false;
   hipStream_t tail_stream = nullptr;
-  hipStream_t tail_more[kTailSlots - 1] = {};  // the server's other tail streams
   hipEvent_t ev_fin_done = nullptr;
   hipEvent_t ev_tail[kTailSlots] = {};  // per slot: tail done
   bool tail_pending = false;       // the latest tail's outputs are not merged into out_host yet
@@ -750,14 +749,16 @@ int prepare_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, int mode, 
 }
 
 // The deferred optimal rollout on a side stream: after the context stream's finish (event), or, for
-// the resident server (its finish has published: f.clk set), at once.  The server's tails go to the
-// stream of their slot (tail_streams = 4): beside a server workgroup a tail takes about two step
-// periods (~175 us against ~52 us alone at C3), so on one or two streams each waited for the one
-// before it and the host for the slot (measured: every other command ~15 us late with two).
+// the resident server (its finish has published: f.clk set), at once.  The server's tails alternate
+// over the tail and the noise stream (tail_streams = 2): beside a server workgroup a tail takes about
+// two step periods (~175 us against ~52 us alone at C3), so on one stream each waited for the one
+// before it and the host for the slot.  More streams than the process's hardware queues
+// (GPU_MAX_HW_QUEUES, 4 by default: torch's, the context's, the tail's and the noise stream's)
+// share a queue, and a tail queued behind the resident server on the context's queue waited for it
+// (measured with one stream per slot: every fourth command 66-102 us late).
 int enqueue_tail(mppi_ctx* c, const FinishArgs& f, int par) {
   const bool server = f.clk != nullptr;
-  const int si = server ? par % c->tail_streams : 0;
-  hipStream_t ts = si == 0 ? c->tail_stream : c->tail_more[si - 1];
+  hipStream_t ts = (server && c->tail_streams == 2 && (par & 1)) ? c->noise_stream : c->tail_stream;
   if (!server) {
     HIP_TRY(hipEventRecord(c->ev_fin_done, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->tail_stream, c->ev_fin_done, 0));
@@ -1277,9 +1278,6 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
     if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(MPPI_EHIP, "hipEventCreate failed"));
   if (hipEventCreateWithFlags(&c->ev_fin_done, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->tail_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->tail_more[0], hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->tail_more[1], hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->tail_more[2], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithPriority(&c->noise_stream, hipStreamNonBlocking, c->prio_least) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_prev_roll, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->eps_ev[0], hipEventDisableTiming) != hipSuccess ||
@@ -1322,8 +1320,6 @@ void mppi_destroy(mppi_ctx* c) {
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->tail_stream) hipStreamSynchronize(c->tail_stream);
-  for (hipStream_t t : c->tail_more)
-    if (t) hipStreamSynchronize(t);
   if (c->noise_stream) hipStreamSynchronize(c->noise_stream);
   if (c->Z_owned && c->Z) hipFree(c->Z);
   if (c->ntab) hipFree(c->ntab);
@@ -1367,8 +1363,6 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->bin_ci) hipFree(c->bin_ci);
   if (c->noise_stream) hipStreamDestroy(c->noise_stream);
   if (c->tail_stream) hipStreamDestroy(c->tail_stream);
-  for (hipStream_t t : c->tail_more)
-    if (t) hipStreamDestroy(t);
   if (c->inj1) hipFree(c->inj1);
   if (c->inj2) hipFree(c->inj2);
   for (auto& e : c->ev)
@@ -1653,8 +1647,8 @@ int mppi_set_option(mppi_ctx* c, const char* name, int64_t value) {
     c->srv_idle_us = (uint64_t)value;
     return MPPI_OK;
   }
-  if (n == "tail_streams") {  // the server's deferred tails round-robin over 1, 2 or 4 streams
-    if (value != 1 && value != 2 && value != 4) return fail(MPPI_EINVAL, "tail_streams must be 1, 2 or 4");
+  if (n == "tail_streams") {  // the server's deferred tails on the tail stream, or alternating with the noise stream
+    if (value != 1 && value != 2) return fail(MPPI_EINVAL, "tail_streams must be 1 or 2");
     c->tail_streams = (int)value;
     return MPPI_OK;
   }

@@ -291,8 +291,8 @@ int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
  *                        hook).
  *   "record_tree_finish" 1: the record-tree finish (mppi_finish_kernel) at every record count
  *                        (default 0: the column-split finish wherever its shape fits).
- *   "tail_streams"       the server's deferred optimal rollouts round-robin over 1, 2 or 4
- *                        side streams (default 4: one per tail slot, none waits for another). */
+ *   "tail_streams"       the server's deferred optimal rollouts on the tail stream (1) or
+ *                        alternating over the tail and the noise stream (2, default). */
 int mppi_set_option(mppi_ctx* ctx, const char* name, int64_t value);
 int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_t* launches);
 /* HIP-event time of the deferred optimal-rollout kernels (side stream). */

@@ -11,11 +11,11 @@ from mppi_amd import _lib, scene  # noqa: E402
 
 Z, hw, cm = scene.scene_c3()
 H = int(sys.argv[1]) if len(sys.argv) > 1 else 100
-for async_tail, ts in ((True, 1), (True, 4), (False, 1)):
+for async_tail, ts in ((True, 1), (True, 2), (False, 1)):
     eng = _lib.Engine(_lib.make_params(65536, H), 0)
     if os.environ.get("MPPI_RESIDENT", "1") != "0":
         eng.set_option("tail_streams", ts)
-    elif ts == 4:
+    elif ts == 2:
         continue
     eng.set_dem(Z, hw)
     eng.set_costmap(cm, hw)
