@@ -500,6 +500,11 @@ def pmc_traffic(path, kernel, K_local, H):
 
 def main():
     args = parse()
+    # stdout carries the one JSON line only: libraries print banners there (RCCL's version banner at
+    # communicator init, from the shard leg's group), so fd 1 goes to stderr until the line is written
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -726,7 +731,8 @@ def main():
             rec["costmap_builder"] = costmap_bench(local_rank, cpu=args.cpu_baseline_seconds > 0)
         if cpu is not None:
             rec["cpu_baseline"] = cpu
-        print(json.dumps(rec), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(rec) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
 

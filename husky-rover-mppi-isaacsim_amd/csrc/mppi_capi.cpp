@@ -141,6 +141,9 @@ struct mppi_ctx {
   double srv_last_us = 0;     // host time of the last command
   uint64_t srv_idle_us = 2000;
   int64_t srv_launches = 0, srv_steps = 0, srv_failed = 0;
+  int srv_cmd_noise = -1;     // the normals slot the last command asked the server's noise phase for
+  int fail_kind = 0;          // the last failed wait: 1 finish gave up, 2 launch retired, 3 timeout
+  bool srv_warned = false;
   uint64_t fin_wait_ticks = 200000000ull;  // a finish's record wait bound (2 s at 100 MHz; mppi_set_option)
   int tail_streams = 2;  // server: deferred tails alternating over the tail and the noise stream, or on the
                          // tail stream only (mppi_set_option "tail_streams": 2 or 1)
@@ -561,11 +564,13 @@ int wait_done(mppi_ctx* c) {
   const unsigned want = c->wait_seq;
   const double t0 = now_us();
   std::string why;
+  c->fail_kind = 0;
   for (uint64_t i = 0;; ++i) {
     const unsigned v = __atomic_load_n(c->done, __ATOMIC_ACQUIRE);
     if (v == want) return MPPI_OK;
     if (v == (want | kDoneFail)) {
       why = "the finish gave up waiting for the step's records";
+      c->fail_kind = 1;
       break;
     }
     if ((i & 255) == 255) {
@@ -573,12 +578,14 @@ int wait_done(mppi_ctx* c) {
       if (e == hipSuccess) {
         if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == want) return MPPI_OK;
         why = "the step's launch retired without publishing its outputs";
+        c->fail_kind = 2;
         c->srv_running = false;  // (an idle server has exited: the stream is empty)
         break;
       }
       if (e != hipErrorNotReady) return fail(MPPI_EHIP, std::string("step failed: ") + hipGetErrorString(e));
       if (now_us() - t0 > 10e6) {
         why = "the step did not complete within 10 s";
+        c->fail_kind = 3;
         break;
       }
     }
@@ -587,6 +594,8 @@ int wait_done(mppi_ctx* c) {
   ++c->srv_failed;
   quiesce(c);
   rearm_counters(c);
+  // the normals the failed step's server was to generate may be incomplete: regenerate them
+  if (c->last_resident && c->srv_cmd_noise >= 0) c->eps_step[c->srv_cmd_noise] = -1;
   return fail(MPPI_EHIP, why);
 }
 
@@ -982,6 +991,7 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   d.tail_slot = par;
   d.mode = c->async_tail ? 2 : 1;
   d.noise_slot = noise_slot;
+  c->srv_cmd_noise = noise_slot;
   d.noise_n_base_lo = (unsigned)((step + 2) * nb);
   d.noise_n_base_hi = (unsigned)(((step + 2) * nb) >> 32);
   unsigned* cw = reinterpret_cast<unsigned*>(cmd);
@@ -1088,6 +1098,23 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   if (rc) return rc;
   c->last_resident = resident;
   remember(c, proj, step, mode, pl);
+  if (resident && !c->trace) {
+    rc = copy_outputs(c, out);
+    // a server that never ran the command (it cannot hold all its workgroups on the device at once,
+    // e.g. under a counter-collecting profiler that serializes dispatches): separate launches from
+    // now on, this step again (it published nothing and changed no state)
+    if (rc == MPPI_EHIP && c->fail_kind == 2) {
+      if (!c->srv_warned)
+        std::fprintf(stderr, "mppi: the resident step server could not run here; using separate launches\n");
+      c->srv_warned = true;
+      c->resident = false;
+      c->last_resident = false;
+      rc = enqueue_step(c, proj, step, mode, pl);
+      if (rc) return rc;
+      return copy_outputs(c, out);
+    }
+    return rc;
+  }
   if (!c->trace) return copy_outputs(c, out);
   const double t2 = now_us();
   rc = copy_outputs(c, out);
