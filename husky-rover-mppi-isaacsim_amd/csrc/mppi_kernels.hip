@@ -1094,14 +1094,13 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
           u.z = clampf(nom_r[q] + sg_r[q] * u.z, lo_r[q], hi_r[q]);
           u.w = clampf(nom_r[q] + sg_r[q] * u.w, lo_r[q], hi_r[q]);
         }
-        double x0 = (double)w.x, x1 = (double)w.y, x2 = (double)w.z, x3 = (double)w.w;  // j == 1: S
-        if (j >= 2) {
-          x0 = x0 * (double)u.x;
-          x1 = x1 * (double)u.y;
-          x2 = x2 * (double)u.z;
-          x3 = x3 * (double)u.w;
-        }
-        gs[g] = (x0 + x1) + (x2 + x3);
+        if (j < 2) u = make_float4(1.f, 1.f, 1.f, 1.f);  // j == 1: S, the weights alone
+        // (w0 u0 + w1 u1) + (w2 u2 + w3 u3) in float64: a product of two floats is exact in a
+        // double, so fma(w0, u0, w1 u1) is the rounded sum of the exact products (one product and
+        // one fma instead of two products and an add per pair; same bits)
+        const double a = __builtin_fma((double)w.x, (double)u.x, (double)w.y * (double)u.y);
+        const double b = __builtin_fma((double)w.z, (double)u.z, (double)w.w * (double)u.w);
+        gs[g] = a + b;
       }
       const double ls = ((gs[0] + gs[1]) + (gs[2] + gs[3])) + ((gs[4] + gs[5]) + (gs[6] + gs[7]));
       // (line 0 + line 1), (line 2 + line 3): left + right; then the half; then the row
