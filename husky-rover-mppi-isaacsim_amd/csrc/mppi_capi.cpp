@@ -52,6 +52,7 @@ constexpr int kEpsSlots = 3;
 struct Plan {
   int traj_per_block = 256;
   int block = 256, blocks = 0;
+  int grid = 0;  // rollout workgroups (the role-split kernel runs blocks beyond one per CU in turn)
   int wx0 = 0, wy0 = 0, W = 1, Wr = 1;
   size_t lds_bytes = 0, fin_lds_bytes = 0, fin_tree_bytes = 0;
   int fin_win_offset = 0;
@@ -290,9 +291,11 @@ Plan make_plan(const mppi_ctx* c) {
   const size_t ring_rows = pl.roles ? (size_t)(4 + 4) * PAIR_RING + 2 : (size_t)(PAIR_RING_IN + 4) * PAIR_RING + 1;
   pl.lds_bytes = ring_rows * TB * sizeof(float) + 4 * (TB / 64) * sizeof(int) +
                  (size_t)((2 * H + 3) & ~3) * sizeof(float) + scratch;
-  // only at one workgroup per CU: the cache takes the CU's spare LDS, which at larger K
-  // (C5: 4 workgroups per CU) would cost a co-resident rollout workgroup instead
-  if (pl.blocks <= c->num_cus) {
+  // only at one workgroup per CU (the role-split kernel always: beyond one block per CU its
+  // workgroups run the blocks in turn; the pair kernel up to one block per CU): the cache takes
+  // the CU's spare LDS, which a co-resident pair workgroup (C5: 4 per CU) would need instead
+  pl.grid = pl.roles ? std::min(pl.blocks, std::max(c->num_cus, 1)) : pl.blocks;
+  if (pl.roles || pl.blocks <= c->num_cus) {
     // the rest of the CU's LDS keeps the sampled controls of the first steps ([2][T][TB]
     // floats, 16-byte aligned after the scratch), so the leaf reduction re-reads only the
     // other steps' normals from HBM (all workgroups reduce at once: a bandwidth burst)
@@ -715,7 +718,7 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   }
   if (pl.blocks == 0) return MPPI_OK;
   if (c->timing && !dump_args) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-  HIP_TRY(launch_rollout_pair(a, pl.blocks, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr, pl.roles));
+  HIP_TRY(launch_rollout_pair(a, pl.grid, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr, pl.roles));
   if (c->timing && !dump_args) {
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     c->ev_roll_pending = true;
@@ -915,7 +918,10 @@ void remember(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
 // completion word.  No launch and no kernel boundary on the step's path: the gap between two steps
 // is the host's round trip (completion word seen -> next command) plus one poll of pinned memory.
 bool server_shape(const mppi_ctx* c, const Plan& pl, int mode, int* P, int* ncol, int* groups, size_t* lds) {
-  if (!c->resident || mode != 0 || !pl.roles || !c->colfin || c->timing != 0 || pl.blocks < 1) return false;
+  // (every workgroup of the server must be resident at once: one rollout block per CU at most)
+  if (!c->resident || mode != 0 || !pl.roles || !c->colfin || c->timing != 0 || pl.blocks < 1 ||
+      pl.blocks > std::max(c->num_cus, 1))
+    return false;
   size_t cf_lds = 0;
   // the finish runs in the workgroups holding the last `groups` tickets: at most one per rollout workgroup
   if (!colfin_shape(pl.blocks, H_of(c), P, ncol, groups, &cf_lds, pl.blocks)) return false;

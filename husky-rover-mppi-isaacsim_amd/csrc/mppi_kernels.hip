@@ -986,7 +986,7 @@ template <int TB, int NT, bool EPS = false, bool WT = false>
 __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
                                              unsigned char* scratch, const float* ub_block,
                                              const float* unom = nullptr, const float* ucache = nullptr,
-                                             int uc_steps = 0);
+                                             int uc_steps = 0, int blk = -1);
 
 // =====================================================================  leaf records (shared)
 // Softmax leaf records (DEFINED replacement of critics_warp.py:338-376) for the
@@ -1003,7 +1003,8 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
 template <int TB, int NT, bool EPS, bool WT>
 __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
                                              unsigned char* scratch, const float* ub_block,
-                                             const float* unom, const float* ucache, int uc_steps) {
+                                             const float* unom, const float* ucache, int uc_steps, int blk) {
+  if (blk < 0) blk = blockIdx.x;  // the block whose record this is (a workgroup may run several)
   constexpr int NL = TB / 256;
   constexpr int NWL = TB / 64;   // waves' worth of trajectories
   const int tid = thread_id<WT, NT>(), lane = tid & 63;
@@ -1136,14 +1137,14 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
       }
     }
     if constexpr (WT)
-      __hip_atomic_store(a.nodes + (size_t)blockIdx.x * E + j, val[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.nodes + (size_t)blk * E + j, val[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else
-      a.nodes[(size_t)blockIdx.x * E + j] = val[0];
+      a.nodes[(size_t)blk * E + j] = val[0];
     if (j == 0 && a.rec_m) {  // m again in the contiguous array (one line per 32 records to read)
       if constexpr (WT)
-        __hip_atomic_store(a.rec_m + blockIdx.x, lm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.rec_m + blk, lm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else
-        a.rec_m[blockIdx.x] = lm[0];
+        a.rec_m[blk] = lm[0];
     }
   }
 #ifdef MPPI_STAMPS
@@ -1793,7 +1794,7 @@ constexpr int ROLE_CHAIN = 0, ROLE_PROD = 1, ROLE_WHEEL = 2, ROLE_COST = 3, NROL
 // FUSED: returns the workgroup's ticket (its rank among the workgroups that have completed their
 // records, from the record counter rec_cnt); otherwise -1.
 template <int TB, int PROJ, int MODE, bool DUMP, bool FUSED>
-__device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cnt, int* ticket_lds = nullptr) {
+__device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigned* rec_cnt, int* ticket_lds = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   constexpr int NT = NROLES * TB;
   constexpr int NG = TB / 64;  // trajectory groups (waves per role)
@@ -1824,7 +1825,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
   int* f_chain = flags + NG + grp;
   int* f_wheel = flags + 2 * NG + grp;
   int* f_cost = flags + 3 * NG + grp;
-  const int64_t kl = (int64_t)blockIdx.x * TB + tj;
+  const int64_t kl = (int64_t)blk * TB + tj;
   const bool valid = kl < a.K;
   const int H = a.H;
   Dem<false> dem;
@@ -1958,8 +1959,8 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
   else if (role == ROLE_PROD) {
     // ---------------- sampling + wheel filter + sin/cos, normals prefetched two steps ahead
     // (even / odd steps in their own registers: no loop-carried copy of a load in flight)
-    const float* eps_row = (MODE == 0) ? a.eps + (size_t)blockIdx.x * (2 * H) * TB + tj : nullptr;
-    float* ust = a.ustore + (size_t)blockIdx.x * (2 * H) * TB + tj;
+    const float* eps_row = (MODE == 0) ? a.eps + (size_t)blk * (2 * H) * TB + tj : nullptr;
+    float* ust = a.ustore + (size_t)blk * (2 * H) * TB + tj;
     float L = a.wl, R = a.wr;
     int seen_cost = 0;
     float eA1 = 0.f, eA2 = 0.f, eB1 = 0.f, eB2 = 0.f;
@@ -2164,10 +2165,11 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
   }
   __syncthreads();
   if constexpr (MODE == 0)  // rows hold the normals; the leaf recomputes the sampled controls
-    leaf_records<TB, NT, true, FUSED>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB, unom_lds,
-                                      ucache, a.ucache_steps);
+    leaf_records<TB, NT, true, FUSED>(a, cost_lds, scratch, a.eps + (size_t)blk * (2 * H) * TB, unom_lds,
+                                      ucache, a.ucache_steps, blk);
   else
-    leaf_records<TB, NT, false, FUSED>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
+    leaf_records<TB, NT, false, FUSED>(a, cost_lds, scratch, a.ustore + (size_t)blk * (2 * H) * TB, nullptr, nullptr,
+                                       0, blk);
   if (clk_wg) a.clk[6] = __builtin_amdgcn_s_memrealtime();  // workgroup 0's leaf record written
   if (clk_any) a.clk[kClkBase + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
   if constexpr (FUSED) {  // the record is written through: count it (D8: complete, then a relaxed count)
@@ -2186,10 +2188,16 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, unsigned* rec_cn
   return -1;
 }
 
+// One workgroup per CU at most: a grid smaller than the blocks runs them in turn (block blockIdx.x,
+// + gridDim.x, ...), each a whole role-split rollout and leaf record.
 template <int TB, int PROJ, int MODE, bool DUMP>
 __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const RolloutArgs a_in) {
   RolloutArgs a = a_in;
-  roles_body<TB, PROJ, MODE, DUMP, false>(a, nullptr);
+  const int nblk = (int)((a.K + TB - 1) / TB);
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    roles_body<TB, PROJ, MODE, DUMP, false>(a, blk, nullptr);
+    if (blk + (int)gridDim.x < nblk) __syncthreads();  // (the next block reuses the LDS)
+  }
 }
 
 // =====================================================================  finish kernel
@@ -3951,7 +3959,7 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
     const int64_t W = 4 * (int64_t)z.nroll * ((a.H + 1) >> 1);
     const int nn = z.nroll - z.fin_groups;
     const int64_t S = 2 * (int64_t)nn + z.fin_groups - 1;
-    const int ticket = roles_body<TB, PROJ, 0, false, true>(a, z.rec_cnt, sh);
+    const int ticket = roles_body<TB, PROJ, 0, false, true>(a, (int)blockIdx.x, z.rec_cnt, sh);
     if (ticket == z.nroll - 1 && tid == 0 && z.clk) z.clk[kClkServer + 8 * (seq & 7) + 1] = __builtin_amdgcn_s_memrealtime();
     const int blk = ticket - (z.nroll - z.fin_groups);
     if (blk < 0 && nslot >= 0) {
