@@ -558,9 +558,14 @@ def main():
     # no host wait) in a pass of their own; --timed-events records them inside the timed region
     # (same kernel time within 0.5 %, but ~6 % fewer steps/s: profiles/r02_notes.md)
     nt = max(args.steps // 4, 10)
+    srv0 = run.eng.server_time()
     el = timed_run(torch, dist, run, args.proj, args.warmup, args.steps, s0, not args.sync,
                    kernel_timing=2 if args.timed_events else 0)
     head_info = run.eng.launch_info()   # the schedule the timed steps ran on
+    srv1 = run.eng.server_time()
+    n_srv = srv1[2] - srv0[2]   # the server's own clock over that pass (its warm-up steps included)
+    srv_roll_us = (srv1[0] - srv0[0]) / n_srv if n_srv > 0 else None
+    srv_step_us = (srv1[1] - srv0[1]) / n_srv if n_srv > 0 else None
     if not args.timed_events:
         timed_run(torch, dist, run, args.proj, args.warmup, nt, 2 * s0, not args.sync, kernel_timing=2)
     roll_ms, _, n_roll = run.eng.timing()
@@ -673,6 +678,10 @@ def main():
                 "schedule": ("resident step server (mppi_step_server_kernel)" if head_info.get("resident")
                              else "separate launches (rollout, finish, deferred tail)"),
                 "server_launches": head_info.get("server_launches"),
+                "server_rollout_us": round(srv_roll_us, 2) if srv_roll_us else None,
+                "server_step_us": round(srv_step_us, 2) if srv_step_us else None,
+                "server_clock_steps": n_srv,
+                "server_clock": "s_memrealtime on the server: command seen -> last rollout ticket / -> completion word, averaged",
                 "finish_kernel_avg_ms": round(fin_ms / max(n_fin, 1), 5),
                 "chain": {"instructions_per_step": chain_static(),
                           "cycles_per_step": round(clock["cycles_per_step"], 1),
@@ -698,6 +707,8 @@ def main():
                 "traffic_source": traffic_src,
                 "kernel": kernel,
                 "kernel_avg_ms": round(k_avg_ms, 5),
+                "kernel_timing": "HIP events around each launch of a separate-launch pass (mppi_set_timing(2)): "
+                                 "the launch waits for the side streams' work, so no noise or tail kernel runs beside it",
                 "algorithmic_bytes_per_launch": alg_bytes,
             },
         }

@@ -154,6 +154,7 @@ struct mppi_ctx {
   FinishArgs tail_def{};
   int tail_def_par = 0;
   hipEvent_t ev_prev_roll = nullptr;  // recorded after the last rollout that read an eps slot
+  hipEvent_t ev_side[2] = {nullptr, nullptr};  // timing mode 2: the side streams' work so far
   // finish: column-split u_opt slice records / first tree level, arrival counter
   double* level1 = nullptr;       // finish kernel first-level records
   size_t level1_cap = 0;
@@ -717,6 +718,14 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     a.d_u2 = dump_args->d_u2;
   }
   if (pl.blocks == 0) return MPPI_OK;
+  if (c->timing == 2 && !dump_args) {
+    // the rollout kernel's own time: nothing already enqueued on the side streams (the noise of a
+    // later step, the previous step's deferred optimal rollout) runs beside the timed launch
+    HIP_TRY(hipEventRecord(c->ev_side[0], c->noise_stream));
+    HIP_TRY(hipEventRecord(c->ev_side[1], c->tail_stream));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_side[0], 0));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_side[1], 0));
+  }
   if (c->timing && !dump_args) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   HIP_TRY(launch_rollout_pair(a, pl.grid, pl.lds_bytes, c->stream, proj, mode, dump_args != nullptr, pl.roles));
   if (c->timing && !dump_args) {
@@ -1305,7 +1314,8 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   if (hipMemset(c->u_nom[0], 0, 2 * H * sizeof(float)) != hipSuccess ||
       hipMemset(c->u_nom[1], 0, 2 * H * sizeof(float)) != hipSuccess ||
       hipMemset(c->cost, 0, std::max<int64_t>(p.num_trajectories, 1) * sizeof(float)) != hipSuccess ||
-      hipMemset(c->relay, 0, 64 * sizeof(unsigned)) != hipSuccess)
+      hipMemset(c->relay, 0, 64 * sizeof(unsigned)) != hipSuccess ||
+      hipMemset(c->clk, 0, kClkWords * sizeof(uint64_t)) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "hipMemset failed"));
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(MPPI_EHIP, "hipEventCreate failed"));
@@ -1313,6 +1323,8 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipStreamCreateWithFlags(&c->tail_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithPriority(&c->noise_stream, hipStreamNonBlocking, c->prio_least) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_prev_roll, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_side[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_side[1], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->eps_ev[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->eps_ev[1], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->eps_ev[2], hipEventDisableTiming) != hipSuccess)
@@ -1382,6 +1394,8 @@ void mppi_destroy(mppi_ctx* c) {
     if (c->eps_ev[i]) hipEventDestroy(c->eps_ev[i]);
   }
   if (c->ev_prev_roll) hipEventDestroy(c->ev_prev_roll);
+  for (hipEvent_t e : c->ev_side)
+    if (e) hipEventDestroy(e);
   if (c->bin_tile_of) hipFree(c->bin_tile_of);
   if (c->level1) hipFree(c->level1);
   if (c->level1_cnt) hipFree(c->level1_cnt);
@@ -1743,6 +1757,19 @@ int mppi_get_timing(mppi_ctx* c, double* roll, double* fin, int64_t* n) {
   if (roll) *roll = c->t_roll;
   if (fin) *fin = c->t_fin;
   if (n) *n = c->launches;
+  return MPPI_OK;
+}
+
+int mppi_get_server_time(mppi_ctx* c, double* roll_us, double* step_us, int64_t* steps) {
+  if (!c) return fail(MPPI_EINVAL, "null context");
+  HIP_TRY(hipSetDevice(c->device));
+  uint64_t v[4] = {0, 0, 0, 0};
+  // (a side stream: the context stream may hold the running server)
+  HIP_TRY(hipMemcpyAsync(v, c->clk + kClkSums, sizeof(v), hipMemcpyDeviceToHost, c->noise_stream));
+  HIP_TRY(hipStreamSynchronize(c->noise_stream));
+  if (roll_us) *roll_us = (double)v[0] / 100.0;
+  if (step_us) *step_us = (double)v[2] / 100.0;
+  if (steps) *steps = (int64_t)std::min(v[1], v[3]);
   return MPPI_OK;
 }
 

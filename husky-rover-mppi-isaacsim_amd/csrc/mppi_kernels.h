@@ -126,7 +126,9 @@ constexpr int kClkBase = 8, kClkBlocks = 4096;
 // 0 the head saw the command, 1 the last rollout ticket, 2 the completion word stored, 3 the
 // latest end of a noise share (atomic max), 4 the deferred tail started, 5 the tail ended,
 // 6 the head started polling for the command, 7 the latest end of any workgroup's step
-constexpr int kClkServer = kClkBase + 2 * kClkBlocks, kClkWords = kClkServer + 64;
+// then (resident server, always on) [kClkServer + 64, + 68): the sums of (last ticket - command seen)
+// and (completion word - command seen) in 100 MHz ticks, and their step counts
+constexpr int kClkServer = kClkBase + 2 * kClkBlocks, kClkSums = kClkServer + 64, kClkWords = kClkSums + 8;
 // The finish's phase-2 LDS (finish_phase2): uo[2][PS] v w sin cos[H] chain[12H] out[16H]
 // lr[2][PS] floats, PS = the filter rows' stride (a multiple of 4 floats, >= H + 32 for the
 // filter's read-ahead); the DEM window (LDS finish) starts at fin_phase2_floats(H) floats.

@@ -3918,7 +3918,9 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
         }
       }
       if (tid == 0) cmd_lds[31] = ok;
-      if (tid == 0 && head && z.clk && ok) z.clk[kClkServer + 8 * (cmd_lds[0] & 7)] = __builtin_amdgcn_s_memrealtime();
+      if (tid == 0 && head && z.clk && ok)  // (write-through: the last ticket and the finish read it)
+        __hip_atomic_store(z.clk + kClkServer + 8 * (cmd_lds[0] & 7), (uint64_t)__builtin_amdgcn_s_memrealtime(),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (!cmd_lds[31]) return;  // stop, or idle: the host relaunches
@@ -3960,7 +3962,13 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
     const int nn = z.nroll - z.fin_groups;
     const int64_t S = 2 * (int64_t)nn + z.fin_groups - 1;
     const int ticket = roles_body<TB, PROJ, 0, false, true>(a, (int)blockIdx.x, z.rec_cnt, sh);
-    if (ticket == z.nroll - 1 && tid == 0 && z.clk) z.clk[kClkServer + 8 * (seq & 7) + 1] = __builtin_amdgcn_s_memrealtime();
+    if (ticket == z.nroll - 1 && tid == 0 && z.clk) {  // the rollout's time on the server, summed
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      z.clk[kClkServer + 8 * (seq & 7) + 1] = now;
+      const uint64_t t0 = __hip_atomic_load(z.clk + kClkServer + 8 * (seq & 7), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(z.clk + kClkSums, now - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(z.clk + kClkSums + 1, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const int blk = ticket - (z.nroll - z.fin_groups);
     if (blk < 0 && nslot >= 0) {
       // shares 2t, 2t + 1 of the normals of step + 2 while the finish workgroups reduce the records
@@ -4009,7 +4017,13 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
         f.wl = a.wl;
         f.wr = a.wr;
         ok = colfin_body<true>(f, z.fin_P, z.fin_ncol, blk, z.fin_groups, z.rec_cnt);
-        if (ok && blk == z.fin_groups - 1 && tid == 0 && z.clk) z.clk[kClkServer + 8 * (seq & 7) + 2] = __builtin_amdgcn_s_memrealtime();
+        if (ok && blk == z.fin_groups - 1 && tid == 0 && z.clk) {  // and the whole step's
+          const uint64_t now = __builtin_amdgcn_s_memrealtime();
+          z.clk[kClkServer + 8 * (seq & 7) + 2] = now;
+          const uint64_t t0 = __hip_atomic_load(z.clk + kClkServer + 8 * (seq & 7), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(z.clk + kClkSums + 2, now - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(z.clk + kClkSums + 3, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
       // a finish that gave up publishes the failure (the host stops the server and re-arms the count)
       if (!ok && tid == 0)

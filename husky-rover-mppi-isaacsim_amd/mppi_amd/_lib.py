@@ -93,6 +93,8 @@ _PROTOS = {
     "mppi_get_tail_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "mppi_get_launch_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]),
     "mppi_get_chain_clock": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int32]),
+    "mppi_get_server_time": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                       C.POINTER(C.c_int64)]),
     "mppi_bilinear_query": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
     "mppi_selftest": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.POINTER(C.c_int64)]),
     "mppi_bilinear_tiles": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
@@ -472,6 +474,12 @@ class Engine:
                 "finish_records", "finish_ncol", "finish_groups", "ucache_steps", "resident",
                 "server_launches", "server_steps", "server_failed_steps")
         return dict(zip(keys, [int(v) for v in info]))
+
+    def server_time(self):
+        """mppi_get_server_time: (rollout us summed, step us summed, steps) on the resident server."""
+        r, st, n = C.c_double(0), C.c_double(0), C.c_int64(0)
+        self._c(self.lib.mppi_get_server_time(self.ctx, C.byref(r), C.byref(st), C.byref(n)), "mppi_get_server_time")
+        return r.value, st.value, n.value
 
     def chain_clock(self):
         """mppi_get_chain_clock: shader MHz, cycles per chain step, chain us and cycles of the last rollout."""

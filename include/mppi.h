@@ -264,8 +264,10 @@ int mppi_dump_rollouts(mppi_ctx* ctx, float* traj, float* heading, float* left_w
 /* HIP-event timing of the rollout kernel and of the combine/optimal-rollout
  * kernel, measured on the context stream around each launch.  enable: 0 off,
  * 1 rollout, finish and deferred-tail events (the host waits for the stream and
- * for each tail to collect them), 2 rollout events only (no host wait: the
- * pipelined schedule undisturbed; the finish time reads 0).  While timing is on,
+ * for each tail to collect them), 2 rollout events only (no host wait; each
+ * rollout launch waits for the work already on the side streams, so no noise or
+ * deferred-tail kernel runs beside it: the kernel's own time; the finish time
+ * reads 0).  While timing is on,
  * steps run as separate launches (rollout, finish, tail), not on the resident
  * server, whose per-step kernel time no launch event brackets. */
 int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
@@ -317,6 +319,12 @@ int mppi_get_launch_info(mppi_ctx* ctx, int64_t* info, int32_t n);
  * [8] = first -> last record written, [9] = first start -> last record (0 where not measured);
  * out[10 + b] = first start -> workgroup b's record.  Waits for the context stream. */
 int mppi_get_chain_clock(mppi_ctx* ctx, double* out, int32_t n);
+
+/* The resident step server's own clock (s_memrealtime, 100 MHz), summed over the steps it has
+ * served since mppi_create: roll_us = command seen -> last rollout ticket (the rollout of all
+ * workgroups, on the server), step_us = command seen -> completion word; steps = the steps summed.
+ * Does not stop the server. */
+int mppi_get_server_time(mppi_ctx* ctx, double* roll_us, double* step_us, int64_t* steps);
 
 /* Standalone DEM bilinear kernel: for n query points
  * (x[i], y[i]) in device memory, heights[i] = corner lookup + bilinear exactly
