@@ -3955,15 +3955,12 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
     const uint64_t nbase = ((uint64_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_hi) << 32) |
                            (uint32_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_lo);
     // the normals of step + 2 (when commanded): W wave-units (one Philox block of 64 trajectories
-    // each) in static shares by weight: a workgroup outside the finish with ticket t weighs
-    // 5 nn - 2 t (from its record on: the earlier its record, the more it takes, 2.5x .. 1.5x the
-    // unit nn), a finish workgroup but the last 2 nn (after its columns, ~10 us later); the last
-    // finish workgroup runs phase 2 and heads the next poll.  Cumulative weight before ticket t:
-    // 5 nn t - t (t - 1); the finish workgroups' start at 4 nn^2 + nn.
+    // each) in S static shares, two per workgroup outside the finish (ticket t: shares 2t, 2t + 1,
+    // from its record on) and one per finish workgroup but the last (blk: share 2 nn + blk, after
+    // its columns, ~10 us later); the last finish workgroup runs phase 2 and heads the next poll
     const int64_t W = 4 * (int64_t)z.nroll * ((a.H + 1) >> 1);
-    const int64_t nn = z.nroll - z.fin_groups;
-    const int64_t S0 = 4 * nn * nn + nn;
-    const int64_t S = S0 + 2 * nn * (z.fin_groups - 1);
+    const int nn = z.nroll - z.fin_groups;
+    const int64_t S = 2 * (int64_t)nn + z.fin_groups - 1;
     const int ticket = roles_body<TB, PROJ, 0, false, true>(a, (int)blockIdx.x, z.rec_cnt, sh);
     if (ticket == z.nroll - 1 && tid == 0 && z.clk) {  // the rollout's time on the server, summed
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -3978,8 +3975,7 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
       // and the host turns the step around (static: no claims)
       __builtin_amdgcn_s_setprio(0);
       const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-      const int64_t t0 = ticket, t1 = ticket + 1;
-      const int q0 = (int)(W * (5 * nn * t0 - t0 * (t0 - 1)) / S), q1 = (int)(W * (5 * nn * t1 - t1 * (t1 - 1)) / S);
+      const int q0 = (int)(W * (2 * ticket) / S), q1 = (int)(W * (2 * ticket + 2) / S);
       noise_waves(a.seed, nbase, a.k_offset, a.H, q0 + wave, q1, NROLES * TB / 64, z.eps[nslot], tid & 63);
 #if defined(MPPI_DIAG_W0)  // diagnostic builds: workgroup 0's per-wave noise ends (unused block slots)
       if (blockIdx.x == 0 && (tid & 63) == 0 && z.clk) z.clk[kClkBase + 2 * 4000 + wave] = __builtin_amdgcn_s_memrealtime();
@@ -4034,7 +4030,7 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
         __hip_atomic_store(z.f.done, seq | kDoneFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       if (nslot >= 0 && blk < z.fin_groups - 1) {  // its share of the normals of step + 2 (see above)
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-        const int q0 = (int)(W * (S0 + 2 * nn * blk) / S), q1 = (int)(W * (S0 + 2 * nn * (blk + 1)) / S);
+        const int q0 = (int)(W * (2 * nn + blk) / S), q1 = (int)(W * (2 * nn + blk + 1) / S);
         noise_waves(a.seed, nbase, a.k_offset, a.H, q0 + wave, q1, NROLES * TB / 64, z.eps[nslot], tid & 63);
       }
     }
