@@ -718,9 +718,10 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     a.d_u2 = dump_args->d_u2;
   }
   if (pl.blocks == 0) return MPPI_OK;
-  if (c->timing == 2 && !dump_args) {
+  if (c->timing && !dump_args) {
     // the rollout kernel's own time: nothing already enqueued on the side streams (the noise of a
-    // later step, the previous step's deferred optimal rollout) runs beside the timed launch
+    // later step, the previous step's deferred optimal rollout) runs beside the timed launch (both
+    // modes, so that a kernel trace of the timing passes averages isolated launches only)
     HIP_TRY(hipEventRecord(c->ev_side[0], c->noise_stream));
     HIP_TRY(hipEventRecord(c->ev_side[1], c->tail_stream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_side[0], 0));

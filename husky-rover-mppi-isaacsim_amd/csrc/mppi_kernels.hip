@@ -34,11 +34,15 @@ namespace mppi {
 // template flag F:
 //   F = false  the IEEE operators `/` and sqrtf (hipcc's generic expansions);
 //   F = true   fast paths that are bit-identical on a checked operand range:
-//     division: the arithmetic of LLVM's AMDGPU fdiv expansion (v_rcp_f32, one
-//       Newton step on the reciprocal, two fma quotient corrections) without its
-//       v_div_scale / v_div_fixup steps, which are the identity when |a|, |b| lie
-//       in [2^-40, 2^40] (a = +-0 handled by a select); the refined reciprocal is
-//       shared by all quotients with one divisor and needs no VCC;
+//     division: v_rcp_f32, one Newton step on the reciprocal (y), q0 = a y and ONE
+//       fma residual correction q1 = q0 + (a - b q0) y (Markstein); LLVM's fdiv
+//       expansion applies a second correction and the v_div_scale / v_div_fixup
+//       steps, which are the identity when |a|, |b| lie in [2^-40, 2^40] (a = +-0
+//       handled by a select).  q1 equals the IEEE quotient for EVERY pair of
+//       significands (2^46 pairs, exhaustive, on MI355X: profiles/ubench/div1_check.hip,
+//       profiles/r04_div1_check.txt), and exponents scale all of it exactly in that
+//       range.  The refined reciprocal is shared by all quotients with one divisor
+//       and needs no VCC;
 //     sqrt: LLVM's expansion (v_sqrt_f32 + one-ulp fma correction) without the
 //       small-input scaling, valid for x = 0 or x in [2^-96, 2^128).
 // A fast-path rollout-step ORs "operand outside its range" into a per-lane
@@ -81,11 +85,9 @@ __device__ __forceinline__ float dv(float a, const Recip& r, bool& bad) {
     const float q0 = a * r.y;
     const float e0 = __builtin_fmaf(-r.b, q0, a);
     const float q1 = __builtin_fmaf(e0, r.y, q0);
-    const float e1 = __builtin_fmaf(-r.b, q1, a);
-    const float q2 = __builtin_fmaf(e1, r.y, q1);
     const bool zero = (a == 0.0f);
     bad |= !(zero || div_ok(a));
-    return zero ? q0 : q2;  // q0 = a*y carries the IEEE sign of a zero quotient
+    return zero ? q0 : q1;  // q0 = a*y carries the IEEE sign of a zero quotient
   }
 }
 template <bool F>
@@ -394,10 +396,7 @@ __device__ __forceinline__ float lean_div(float a, const Recip& r, Lean& l) {
   l.emin = min(l.emin, __builtin_amdgcn_frexp_expf(a));
   const float q0 = a * r.y;
   const float e0 = __builtin_fmaf(-r.b, q0, a);
-  const float q1 = __builtin_fmaf(e0, r.y, q0);
-  const float e1 = __builtin_fmaf(-r.b, q1, a);
-  const float q2 = __builtin_fmaf(e1, r.y, q1);
-  return __builtin_copysignf(q2, a);
+  return __builtin_copysignf(__builtin_fmaf(e0, r.y, q0), a);
 }
 
 // chain3d<true> with the lean guards (see above); DEM corners through 32-bit
@@ -552,9 +551,7 @@ __device__ __forceinline__ float lean_div_s(float a, const Recip& r, Lean& l) {
   l.emin = min(l.emin, __builtin_amdgcn_frexp_expf(a));
   const float q0 = a * r.y;
   const float e0 = __builtin_fmaf(r.b, q0, -a);
-  const float q1 = __builtin_fmaf(-e0, r.y, q0);
-  const float e1 = __builtin_fmaf(r.b, q1, -a);
-  return __builtin_fmaf(-e1, r.y, q1);
+  return __builtin_fmaf(-e0, r.y, q0);
 }
 // (a.x, a.y) / r.b, each lane lean_div_s (G = 0: numerators proven in range, no guard)
 template <int G = 1>
@@ -563,9 +560,7 @@ __device__ __forceinline__ f2 lean_div2(f2 a, const Recip& r, Lean& l) {
   const f2 b = bc2(r.b), y = bc2(r.y);
   const f2 q0 = a * y;
   const f2 e0 = pk_fma(b, q0, -a);
-  const f2 q1 = pk_fma(-e0, y, q0);
-  const f2 e1 = pk_fma(b, q1, -a);
-  return pk_fma(-e1, y, q1);
+  return pk_fma(-e0, y, q0);
 }
 // (a.x, a.y, az) / r.b: lean_div2 and lean_div_s with their dependent steps interleaved, so the
 // scalar chain's instructions fill the wait states between the packed chain's dependent steps
@@ -584,12 +579,8 @@ __device__ __forceinline__ void lean_div3(f2 a, float az, const Recip& r, Lean& 
   const float q0z = az * r.y;
   const f2 e0 = pk_fma(b, q0, -a);
   const float e0z = __builtin_fmaf(r.b, q0z, -az);
-  const f2 q1 = pk_fma(-e0, y, q0);
-  const float q1z = __builtin_fmaf(-e0z, r.y, q0z);
-  const f2 e1 = pk_fma(b, q1, -a);
-  const float e1z = __builtin_fmaf(r.b, q1z, -az);
-  qxy = pk_fma(-e1, y, q1);
-  qz = __builtin_fmaf(-e1z, r.y, q1z);
+  qxy = pk_fma(-e0, y, q0);
+  qz = __builtin_fmaf(-e0z, r.y, q0z);
 }
 // cross(n, o).xy = (ny oz - nz oy, nz ox - nx oz), as (ny oz, -nx oz) + (-nz oy, nz ox)
 __device__ __forceinline__ f2 cross_xy(f2 nxy, float nz, f2 oxy, float oz) {
@@ -1162,6 +1153,9 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
 //                  consume p-L (needs chained > p - L)           -> consumed = p - L + 1
 // with L = PAIR_LAG; deadlock-free for 0 < L < D (the chain's waits are always
 // satisfied by side iterations that do not wait on it).  Bitwise identical results.
+#ifndef MPPI_EPS_NT
+#define MPPI_EPS_NT 0  // A/B builds: the producer's loads of rows the leaf does not re-read are non-temporal
+#endif
 #ifndef MPPI_PAIR_LAG
 #define MPPI_PAIR_LAG 6  // measured: 6 beats 2 and 4 at D = 8 (profiles/r01_notes.md)
 #endif
@@ -1971,7 +1965,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       eB1 = eps_row[(size_t)t1 * TB];
       eB2 = eps_row[(size_t)(H + t1) * TB];
     }
-    auto prod = [&](int p, float& e1r, float& e2r) __attribute__((always_inline)) {
+    auto prod = [&](auto nt_tag, int p, float& e1r, float& e2r) __attribute__((always_inline)) {
       float u1, u2;
       if constexpr (MODE == 0) {
         const int ti = min(p + 1, H - 1);
@@ -2012,16 +2006,27 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       lds_store_release(f_prod, p + 1);
       if constexpr (MODE == 0) {  // the normals of step p + 2 into the registers just freed
         const int tn = min(p + 2, H - 1);
-        e1r = eps_row[(size_t)tn * TB];
-        e2r = eps_row[(size_t)(H + tn) * TB];
+        if constexpr (decltype(nt_tag)::value) {  // rows the leaf takes from LDS: streamed past the L2
+          e1r = __builtin_nontemporal_load(eps_row + (size_t)tn * TB);
+          e2r = __builtin_nontemporal_load(eps_row + (size_t)(H + tn) * TB);
+        } else {
+          e1r = eps_row[(size_t)tn * TB];
+          e2r = eps_row[(size_t)(H + tn) * TB];
+        }
       }
     };
     int p = 0;
-    for (; p + 1 < H; p += 2) {
-      prod(p, eA1, eA2);
-      prod(p + 1, eB1, eB2);
+    if constexpr (MPPI_EPS_NT != 0 && MODE == 0) {
+      for (; p + 3 < a.ucache_steps && p + 1 < H; p += 2) {  // steps p + 2, p + 3 cached for the leaf
+        prod(std::true_type{}, p, eA1, eA2);
+        prod(std::true_type{}, p + 1, eB1, eB2);
+      }
     }
-    if (p < H) prod(p, eA1, eA2);
+    for (; p + 1 < H; p += 2) {
+      prod(std::false_type{}, p, eA1, eA2);
+      prod(std::false_type{}, p + 1, eB1, eB2);
+    }
+    if (p < H) prod(std::false_type{}, p, eA1, eA2);
   } else if (role == ROLE_WHEEL) {
     // ---------------- wheel contacts of the even steps (the slope critic reads lw / rw at i,
     // i + 2 for even i, critics_warp.py:220-267) and the slope critic.  Contact sets A / B

@@ -264,10 +264,10 @@ int mppi_dump_rollouts(mppi_ctx* ctx, float* traj, float* heading, float* left_w
 /* HIP-event timing of the rollout kernel and of the combine/optimal-rollout
  * kernel, measured on the context stream around each launch.  enable: 0 off,
  * 1 rollout, finish and deferred-tail events (the host waits for the stream and
- * for each tail to collect them), 2 rollout events only (no host wait; each
- * rollout launch waits for the work already on the side streams, so no noise or
- * deferred-tail kernel runs beside it: the kernel's own time; the finish time
- * reads 0).  While timing is on,
+ * for each tail to collect them), 2 rollout events only (no host wait; the finish
+ * time reads 0).  In both modes each rollout launch waits for the work already on
+ * the side streams, so no noise or deferred-tail kernel runs beside it: the
+ * kernel's own time.  While timing is on,
  * steps run as separate launches (rollout, finish, tail), not on the resident
  * server, whose per-step kernel time no launch event brackets. */
 int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
