@@ -966,7 +966,11 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   // the server's noise phase runs mostly in the workgroups outside the finish: with fewer than a
   // quarter of them, or fewer than two (few records: every rollout workgroup may hold a finish
   // column) the noise kernel does it
-  const bool srv_noise = pl.blocks - groups >= 2 && (int64_t)(pl.blocks - groups) * 4 >= (int64_t)pl.blocks;
+#ifndef MPPI_SRV_HOST_NOISE
+#define MPPI_SRV_HOST_NOISE 0  // A/B builds: the noise kernel beside the server at every size
+#endif
+  const bool srv_noise = !MPPI_SRV_HOST_NOISE && pl.blocks - groups >= 2 &&
+                         (int64_t)(pl.blocks - groups) * 4 >= (int64_t)pl.blocks;
   int noise_slot = -1;
   for (int d = 1; d <= 2; ++d) {
     const uint64_t target = step + (uint64_t)d;
