@@ -1025,12 +1025,16 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
 #endif
   // rows (leaf, j), j in [1, E): the pairwise tree over the leaf's 256 trajectories in index
   // order = (half 0) + (half 1), half = ((line 0 + line 1) + (line 2 + line 3)), line = 32
-  // trajectories (8 float4 groups, a pairwise tree of its own).  One LINE per thread (eight
-  // units of a row in eight adjacent lanes, combined by lane shuffles in the same order), the
-  // loads of all of a thread's lines issued before any is used: the re-read normals rows come
-  // from HBM / MALL, and one line after another per thread left that latency exposed 4 times.
+  // trajectories (8 float4 groups, a pairwise tree of its own).  One LINE per thread, the loads
+  // of all of a thread's lines issued before any is used: the re-read normals rows come from HBM /
+  // MALL, and one line after another per thread left that latency exposed 4 times.  A wave holds
+  // 8 rows x 8 lines: lane = 8 k + (row & 7) for line k of the row, so the eight units of a row sit
+  // 8 lanes apart and combine by lane shuffles (xor 8, 16, 32) in the same order, and the lanes that
+  // an LDS read serves together (8 consecutive) read 8 different rows of the control cache (row
+  // stride UCACHE_ROW: 4 banks apart, conflict-free) or the same weights (a broadcast); with the
+  // eight lines of one row in 8 consecutive lanes every 16-byte read hit the same 4 banks 8 times.
   const int NR = NL * (E - 1);
-  const int NU = 8 * NR;                     // units (row, half, line)
+  const int NU = ((NR + 7) >> 3) << 6;       // unit slots: 8 rows per wave (the last wave partly empty)
   constexpr int LR = 1;                      // lines in flight per thread
   for (int u0 = 0; u0 < NU; u0 += LR * NT) {
     float4 uq[LR][8];
@@ -1040,9 +1044,10 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
     const float4* w4r[LR];
 #pragma unroll
     for (int q = 0; q < LR; ++q) {
-      const int it = u0 + q * NT + tid;      // 8 consecutive units of a row share 8 adjacent lanes
-      const int itc = min(it, NU - 1);
-      const int r = itc >> 3, half = (itc >> 2) & 1, line = itc & 3;
+      const int it = u0 + q * NT + tid;      // unit slot: row 8 (it >> 6) + (it & 7), line (it >> 3) & 7
+      const int k = (it >> 3) & 7;
+      const int r = min(((it >> 6) << 3) + (it & 7), NR - 1);
+      const int half = k >> 2, line = k & 3;
       const int leaf = r / (E - 1), j = 1 + r - leaf * (E - 1);
       jr[q] = j;
       const int tr0 = 256 * leaf + 128 * half + 32 * line;  // first trajectory of the line
@@ -1096,11 +1101,11 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
       }
       const double ls = ((gs[0] + gs[1]) + (gs[2] + gs[3])) + ((gs[4] + gs[5]) + (gs[6] + gs[7]));
       // (line 0 + line 1), (line 2 + line 3): left + right; then the half; then the row
-      const double s2 = ls + __shfl_xor(ls, 1, 64);
-      const double hs = s2 + __shfl_xor(s2, 2, 64);
-      const double rs = hs + __shfl_xor(hs, 4, 64);
-      if (it < NU && (it & 7) == 0) {
-        const int r = it >> 3;
+      const double s2 = ls + __shfl_xor(ls, 8, 64);
+      const double hs = s2 + __shfl_xor(s2, 16, 64);
+      const double rs = hs + __shfl_xor(hs, 32, 64);
+      const int r = ((it >> 6) << 3) + (it & 7);
+      if (r < NR && ((it >> 3) & 7) == 0) {
         const int leaf = r / (E - 1);
         red[leaf * E + jr[q]] = rs;
       }
