@@ -714,6 +714,11 @@ def main():
         }
         if c4 is not None:
             rec["c4"] = c4
+        # (the shard leg before the bilinear one: after the C4 and bilinear legs the plain K = 131 072
+        # step of this leg measured 0.28-0.29 ms instead of 0.17, an interaction not reproduced with
+        # either leg alone, profiles/r04_notes.md; the sharded step was unaffected)
+        if world == 1 and devices is None and not args.no_shard:
+            rec["c4_shard"] = shard_bench(torch, local_rank, args.proj)
         if world == 1 and devices is None and not args.no_bilinear:
             rec["bilinear_roofline"] = bilinear_bench(torch, torch.device("cuda", local_rank))
         if world == 1 and devices is None and not args.no_c5 and args.config != "c2":
@@ -723,8 +728,6 @@ def main():
             r2.close()
             rec["c2"] = {"workload": CONFIGS["c2"][5], "steps_per_s": round(200 / t2, 3),
                          "ms_per_step": round(t2 / 200 * 1e3, 4)}
-        if world == 1 and devices is None and not args.no_shard:
-            rec["c4_shard"] = shard_bench(torch, local_rank, args.proj)
         if world == 1 and devices is None and not args.no_c5 and args.config != "c5":
             r5 = Runner("c5", local_rank, 1, solo=True)
             t5 = timed_run(torch, None, r5, args.proj, 10, 50, 0, not args.sync)
