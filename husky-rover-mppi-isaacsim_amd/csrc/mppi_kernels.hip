@@ -2907,8 +2907,13 @@ template <bool RECS_WT>
 __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol, int blk, int nblk,
                                             unsigned* rec_cnt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  // the separate-launch finish (mppi_colfin_kernel: C4, C5, the K-sharded group step) outranks the
+  // noise kernel of step + 2 that runs beside it: the sharded C4 step 0.1915 -> 0.179-0.180 ms
+  // (profiles/r04_notes.md).  Not in the resident server (RECS_WT), whose noise runs in its own
+  // workgroups after their records (there the priority measured no gain, r02_notes.md).
+  if constexpr (!RECS_WT) __builtin_amdgcn_s_setprio(3);
 #if MPPI_FIN_PRIO
-  __builtin_amdgcn_s_setprio(3);  // the serial step path outranks the next step's noise waves
+  __builtin_amdgcn_s_setprio(3);
 #endif
 #ifdef MPPI_STAMPS
   if (blk == 0) FIN_STAMP(0);
