@@ -3679,6 +3679,23 @@ __global__ __launch_bounds__(256) void mppi_selftest_kernel(int what, int64_t n,
                                                             unsigned long long* bad_count) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   unsigned long long local = 0;
+  if (what == 4) {  // the chain's quotient (refined reciprocal, ONE correction: lean_div_s) against a / b
+    // for every significand of a and the divisor significands (seed + 8191 k) mod 2^23, k = i >> 23
+    // (profiles/ubench/div1_check.hip ran all 2^46 pairs); b in [1, 2), exponents scale exactly
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      const float a = bits_f(0x3F800000u | (uint32_t)(i & 0x7FFFFF));
+      const float b = bits_f(0x3F800000u | (uint32_t)(((uint64_t)(i >> 23) * 8191u + seed) & 0x7FFFFFu));
+      Lean l;
+      lean_init(l);
+      Recip r;
+      r.b = b;
+      const float y0 = __builtin_amdgcn_rcpf(b);
+      r.y = __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+      if (f_bits(lean_div_s(a, r, l)) != f_bits(a / b)) ++local;
+    }
+    if (local) atomicAdd(bad_count, local);
+    return;
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const U4 r = philox4x32_10(U4{(uint32_t)i, (uint32_t)(i >> 32), 0x5e1fu, 0x7e57u}, (uint32_t)seed,
                                (uint32_t)(seed >> 32));

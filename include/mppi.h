@@ -367,8 +367,11 @@ int mppi_rollout_python25d(mppi_ctx* ctx, int64_t n, int32_t H, const double* x0
  * the shared-reciprocal division against IEEE a/b, what = 1 the sqrt path
  * against IEEE sqrtf, what = 2 / 3 the lean normalisation of the pair kernel's
  * chain (sqrt of a squared norm and three quotients; 3 with one dominant
- * component) against IEEE sqrtf and a/b, on n random operands; *mismatches
- * receives the count of in-range results that differ in any bit (0 expected). */
+ * component) against IEEE sqrtf and a/b, on n random operands; what = 4 the
+ * chain's quotient (refined reciprocal, one residual correction) against a/b
+ * for every significand of a and n / 2^23 divisor significands ((seed + 8191 k)
+ * mod 2^23); *mismatches receives the count of in-range results that differ in
+ * any bit (0 expected). */
 int mppi_selftest(mppi_ctx* ctx, int32_t what, int64_t n, uint64_t seed, int64_t* mismatches);
 
 #ifdef __cplusplus

@@ -15,3 +15,15 @@ def test_fast_paths_bitwise(what, name):
     for seed in (1, 2, 3):
         bad = eng.selftest(what, n=1 << 24, seed=seed)
         assert bad == 0, f"{name}: {bad} of 2^24 results differ from IEEE"
+
+
+def test_one_correction_quotient_exhaustive_slice():
+    """The chain's quotient with ONE residual correction (lean_div_s) equals IEEE a / b for every
+    significand of a and 3 x 32768 divisor significands (2^38 pairs per seed); all 2^46 pairs ran in
+    profiles/ubench/div1_check.hip (profiles/r04_div1_check.txt)."""
+    st = hp.oracle_state()
+    Z, hw, cm = hp.c3_scene()
+    eng = hp.engine_for(64, 4, Z, hw, cm, st)
+    for seed in (0, 1, 4093):
+        bad = eng.selftest(4, n=1 << 38, seed=seed)
+        assert bad == 0, f"{bad} of 2^38 quotients differ from IEEE"
