@@ -24,7 +24,10 @@ struct ServerCmd {
   unsigned noise_n_base_hi;
   unsigned pad1[7];
 };
-constexpr int kTailSlots = 4;                 // deferred optimal rollouts in flight (mppi_capi.cpp)
+#ifndef MPPI_TAIL_SLOTS
+#define MPPI_TAIL_SLOTS 4  // A/B builds
+#endif
+constexpr int kTailSlots = MPPI_TAIL_SLOTS;   // deferred optimal rollouts in flight (mppi_capi.cpp)
 constexpr int kCmdWords = 25;                 // the words a step reads (seq .. noise_n_base_hi)
 constexpr unsigned kDoneFail = 0x80000000u;   // done | kDoneFail: the step's finish gave up
 struct FinishArgs {
