@@ -3193,10 +3193,6 @@ __global__ __launch_bounds__(TAIL_THREADS) void mppi_tail_kernel(const FinishArg
   Dem<false> dem;
   dem.init(f.Z, nullptr, f.rows, f.grid, 0, 0, 1, 1, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
   dem.N = f.ntab;
-#ifndef MPPI_TAIL_PRIO
-#define MPPI_TAIL_PRIO 0  // A/B builds: the tail's waves above the rollout's side roles
-#endif
-  if (MPPI_TAIL_PRIO) __builtin_amdgcn_s_setprio(MPPI_TAIL_PRIO);
   optimal_rollout<false>(f, dem, vb, snb, csb, chain, H, f.tail_out, tid, TAIL_THREADS);
   if (tid == 0 && f.clk) f.clk[kClkServer + 8 * (f.seq & 7) + 5] = __builtin_amdgcn_s_memrealtime();
 }
