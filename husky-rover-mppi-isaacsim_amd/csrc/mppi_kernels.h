@@ -144,7 +144,8 @@ __host__ __device__ inline int fin_phase2_floats(int H) { return 4 * fin_plane_s
 // over PAIR_RING-deep rings.
 constexpr int PAIR_TRAJ = 256;
 #ifndef MPPI_PAIR_D
-#define MPPI_PAIR_D 8
+#define MPPI_PAIR_D 6  // round 4: 6 beats 8 at C3 by ~1.4 % (the control cache holds 48 steps instead
+                       // of 40), C4 and the C4 shard unchanged (profiles/r04_notes.md)
 #endif
 constexpr int PAIR_RING = MPPI_PAIR_D;  // = PAIR_D in mppi_kernels.hip
 // sin / cos / 1 - cos of the Rodrigues angle computed by the side wave at production and handed to

@@ -1162,7 +1162,7 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
 #define MPPI_EPS_NT 0  // A/B builds: the producer's loads of rows the leaf does not re-read are non-temporal
 #endif
 #ifndef MPPI_PAIR_LAG
-#define MPPI_PAIR_LAG 6  // measured: 6 beats 2 and 4 at D = 8 (profiles/r01_notes.md)
+#define MPPI_PAIR_LAG 4  // the largest even lag below D = 6 (at D = 8, 6 beat 2 and 4: profiles/r01_notes.md)
 #endif
 #ifndef MPPI_FLAG_CACHE
 #define MPPI_FLAG_CACHE 1  // diagnostic builds: 0 = read the partner's counter at every wait
