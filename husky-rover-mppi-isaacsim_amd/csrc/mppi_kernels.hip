@@ -1786,7 +1786,8 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 #define MPPI_DIAG_SIDE 0  // diagnostic builds: 1 wheel / cost roles idle, 2 also a constant producer
 #endif
 #ifndef MPPI_PROD_PRIO
-#define MPPI_PROD_PRIO MPPI_SIDE_PRIO  // the producer's (the chain waits on it each step)
+#define MPPI_PROD_PRIO 1  // the producer's (the chain waits on it each step): 1 above the wheel and
+                          // cost roles, +1.3 % C3 steps/s with 6-deep rings (profiles/r04_notes.md)
 #endif
 constexpr int ROLE_CHAIN = 0, ROLE_PROD = 1, ROLE_WHEEL = 2, ROLE_COST = 3, NROLES = 4;
 
