@@ -53,9 +53,8 @@ struct Plan {
   int traj_per_block = 256;
   int block = 256, blocks = 0;
   int grid = 0;  // rollout workgroups (the role-split kernel runs blocks beyond one per CU in turn)
-  int wx0 = 0, wy0 = 0, W = 1, Wr = 1;
+  int W = 1, Wr = 1;  // the DEM window every lane of the step can touch (mppi_get_launch_info)
   size_t lds_bytes = 0, fin_lds_bytes = 0, fin_tree_bytes = 0;
-  int fin_win_offset = 0;
   int ucache_steps = 0;   // pair kernel: steps whose sampled controls stay in LDS for the leaf
   bool roles = false;     // the role-split rollout kernel (mppi_rollout_roles_kernel)
 };
@@ -98,7 +97,6 @@ struct mppi_ctx {
   size_t nodes_cap = 0;
   double* scratch0 = nullptr;
   double* scratch1 = nullptr;
-  double* record = nullptr;  // single-rank root record (unused output)
   float* ustore = nullptr;   // sampled controls of the current step [blocks][2][H][block]
   size_t ustore_cap = 0;
   float* stage = nullptr;     // pinned [16H]: the finish kernel stores the outputs here directly
@@ -142,9 +140,17 @@ struct mppi_ctx {
   double srv_last_us = 0;     // host time of the last command
   uint64_t srv_idle_us = 2000;
   int64_t srv_launches = 0, srv_steps = 0, srv_failed = 0;
+  int64_t srv_relaunches = 0;  // commands a leaving server did not take, served by a relaunch (wait_done)
   int srv_cmd_noise = -1;     // the normals slot the last command asked the server's noise phase for
   int fail_kind = 0;          // the last failed wait: 1 finish gave up, 2 launch retired, 3 timeout
   bool srv_warned = false;
+  // the server launch of the command wait_done waits for (a relaunch serves the same command)
+  bool srv_cmd_live = false;
+  Plan srv_pl;
+  int srv_P = 0, srv_ncol = 0, srv_groups = 0;
+  size_t srv_lds = 0;
+  unsigned srv_exit_after = 0;  // test hook mppi_set_option("server_exit_after"): the next launch's head
+                                // leaves after serving this many commands (0: off)
   uint64_t fin_wait_ticks = 200000000ull;  // a finish's record wait bound (2 s at 100 MHz; mppi_set_option)
   int tail_streams = 2;  // server: deferred tails alternating over the tail and the noise stream, or on the
                          // tail stream only (mppi_set_option "tail_streams": 2 or 1)
@@ -251,33 +257,17 @@ int check_ready(mppi_ctx* c) {
   return MPPI_OK;
 }
 
-// DEM cell of a point, float32 like Dem::cell (projection_warp.py:39-40).
-void host_cell(const mppi_ctx* c, float x, float y, int& i, int& j) {
-  float fi = (x - c->x_min) / c->res;
-  fi = std::fmin(std::fmax(fi, -1.0f), (float)c->cols);
-  i = (int)fi;
-  float fj = (y + c->y_min) / c->res;
-  fj = std::fmin(std::fmax(fj, -(float)c->rows), 1.0f);
-  j = -(int)fj;
-}
-
-// Launch geometry: the rollouts of one step stay within H*dt*|v|max (+ wheel
-// offset) of the robot, so a square DEM window of that radius holds every
-// cell any lane can touch; it is staged into LDS when it fits.
+// Launch geometry.  The rollouts of one step stay within H*dt*|v|max (+ wheel offset) of the robot:
+// the square DEM window of that radius (every cell any lane can touch) is reported, not staged.
 Plan make_plan(const mppi_ctx* c) {
   Plan pl;
   const int H = H_of(c);
   const double vabs = std::max(std::fabs((double)c->p.v_min_linear), std::fabs((double)c->p.v_max_linear));
   const double reach = (double)H * (double)c->p.dt * vabs + std::fabs((double)c->p.wheel_offset) * 1.01 + 0.01;
   const int Rc = (int)std::ceil(reach / (double)c->res) + 3;
-  int i0, j0;
-  host_cell(c, c->st.x, c->st.y, i0, j0);
   const int64_t span = 2 * (int64_t)Rc + 2;
-  // the square DEM window every lane of the step can touch (reported by mppi_get_launch_info)
   pl.W = (int)std::min<int64_t>(span, c->cols);
   pl.Wr = (int)std::min<int64_t>(span, c->rows);
-  pl.wx0 = std::min(std::max(i0 - Rc, 0), c->cols - pl.W);
-  pl.wy0 = std::min(std::max(j0 - Rc, 0), c->rows - pl.Wr);
   const int64_t K = c->p.num_trajectories;
   // rollout kernel: chain + side waves per 64 trajectories, DEM and normals through L1/L2,
   // rings [D][PAIR_RING_IN + 4][TB] + cost[TB] + flags + nominal + leaf scratch in LDS (profiles/r01_notes.md)
@@ -312,8 +302,7 @@ Plan make_plan(const mppi_ctx* c) {
   // finish kernel: tree phase [16][2H+2] doubles + 64 x (15 PairScale + 16 m); phase 2
   // uo[2][PS] v[H] w[H] sin[H] cos[H] chain[12H] out[16H] lr[2][PS] floats (fin_phase2_floats)
   pl.fin_tree_bytes = (size_t)16 * (2 * H + 2) * sizeof(double) + (size_t)64 * (15 * 16 + 16 * 4);
-  pl.fin_win_offset = (int)(((size_t)fin_phase2_floats(H) * sizeof(float) + 15) / 16 * 16);
-  pl.fin_lds_bytes = std::max(pl.fin_tree_bytes, (size_t)pl.fin_win_offset);
+  pl.fin_lds_bytes = std::max(pl.fin_tree_bytes, ((size_t)fin_phase2_floats(H) * sizeof(float) + 15) / 16 * 16);
   return pl;
 }
 
@@ -463,11 +452,6 @@ void fill_finish(const mppi_ctx* c, const Plan& pl, const mppi_state& st, Finish
   f.res = c->res;
   f.rinv_res = c->rinv_res;
   f.cdiv_res = c->rinv_res != 0.0f;
-  f.wx0 = pl.wx0;
-  f.wy0 = pl.wy0;
-  f.W = pl.W;
-  f.Wr = pl.Wr;
-  f.win_offset = pl.fin_win_offset;
   f.x0 = st.x;
   f.y0 = st.y;
   f.h0x = st.heading[0];
@@ -558,9 +542,55 @@ void rearm_counters(mppi_ctx* c) {
   if (hipMemsetAsync(c->level1_cnt, 0, 128, c->stream) == hipSuccess) hipStreamSynchronize(c->stream);
 }
 
-// Spin until the finish has published c->wait_seq (all outputs in pinned host memory).  A finish
-// that gave up (done | kDoneFail), a launch that retired without publishing, a stream error or
-// 10 s without completion fail the step; the server is stopped and the counters re-armed.
+// Launch the resident server for the posted command `seq` (its first), with the plan of the last
+// server_step (c->srv_pl ...).  The relay needs no reset: its seq word is older than this command,
+// and its stop word holds the first seq of the launch that wrote it, never this one's.
+int launch_server(mppi_ctx* c, unsigned seq) {
+  const Plan& pl = c->srv_pl;
+  RolloutArgs a;
+  fill_rollout(c, pl, c->st, 0, c->u_nom[c->cur], a);  // (state, nominal buffer: from each command)
+  ServerArgs z;
+  std::memset(&z, 0, sizeof(z));
+  fill_finish(c, pl, c->st, z.f);
+  z.f.recs = c->nodes;
+  z.f.rec_m = c->rec_m;
+  z.f.n_recs = pl.blocks;
+  z.f.level1 = c->level1;
+  z.f.level1_cnt = c->level1_cnt;
+  z.f.done = c->done;
+  z.nroll = pl.blocks;
+  z.fin_P = c->srv_P;
+  z.fin_ncol = c->srv_ncol;
+  z.fin_groups = c->srv_groups;
+  z.rec_cnt = c->level1_cnt + 16;
+  z.cmd = c->cmd;
+  z.relay = c->relay;
+  z.clk = c->clk;
+  for (int i = 0; i < kEpsSlots; ++i) z.eps[i] = c->eps[i];
+  z.u_nom[0] = c->u_nom[0];
+  z.u_nom[1] = c->u_nom[1];
+  for (int i = 0; i < kTailSlots; ++i) {
+    z.tail_in[i] = c->tail_in[i];
+    z.tail_out[i] = c->tail_host[i];
+  }
+  z.first_seq = seq;
+  z.wait_ticks = c->fin_wait_ticks;
+  z.idle_ticks = c->srv_idle_us * 100;
+  z.exit_after = c->srv_exit_after;
+  c->srv_exit_after = 0;  // (the hook applies to one launch)
+  HIP_TRY(launch_step_server(a, z, c->srv_lds, c->stream, c->srv_proj));
+  c->srv_running = true;
+  ++c->srv_launches;
+  return MPPI_OK;
+}
+
+// Spin until the finish has published c->wait_seq (all outputs in pinned host memory).  A server
+// that retired without taking the posted command (its head left on the idle limit just before the
+// command was posted: an exit is all-or-nothing, so nothing of the step ran) is relaunched with the
+// same command, counted in srv_relaunches; a fresh launch that retires without serving it fails the
+// step.  A finish that gave up (done | kDoneFail), any other launch that retired without publishing,
+// a stream error or 10 s without completion fail the step; the server is stopped and the counters
+// re-armed.
 int wait_done(mppi_ctx* c) {
   if (c->timing == 1) {  // the finish's timing events need the stream to retire
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -569,9 +599,10 @@ int wait_done(mppi_ctx* c) {
   const double t0 = now_us();
   std::string why;
   c->fail_kind = 0;
+  bool relaunched = false;
   for (uint64_t i = 0;; ++i) {
     const unsigned v = __atomic_load_n(c->done, __ATOMIC_ACQUIRE);
-    if (v == want) return MPPI_OK;
+    if (v == want) break;
     if (v == (want | kDoneFail)) {
       why = "the finish gave up waiting for the step's records";
       c->fail_kind = 1;
@@ -580,13 +611,27 @@ int wait_done(mppi_ctx* c) {
     if ((i & 255) == 255) {
       const hipError_t e = hipStreamQuery(c->stream);
       if (e == hipSuccess) {
-        if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == want) return MPPI_OK;
-        why = "the step's launch retired without publishing its outputs";
-        c->fail_kind = 2;
+        if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) == want) break;
         c->srv_running = false;  // (an idle server has exited: the stream is empty)
+        if (c->srv_cmd_live && !relaunched) {
+          relaunched = true;
+          ++c->srv_relaunches;
+          const int rc = launch_server(c, want);
+          if (rc) {
+            c->srv_cmd_live = false;
+            return rc;
+          }
+          continue;
+        }
+        why = relaunched ? "a freshly launched step server retired without serving the step"
+                         : "the step's launch retired without publishing its outputs";
+        c->fail_kind = 2;
         break;
       }
-      if (e != hipErrorNotReady) return fail(MPPI_EHIP, std::string("step failed: ") + hipGetErrorString(e));
+      if (e != hipErrorNotReady) {
+        c->srv_cmd_live = false;
+        return fail(MPPI_EHIP, std::string("step failed: ") + hipGetErrorString(e));
+      }
       if (now_us() - t0 > 10e6) {
         why = "the step did not complete within 10 s";
         c->fail_kind = 3;
@@ -595,6 +640,8 @@ int wait_done(mppi_ctx* c) {
     }
     __builtin_ia32_pause();
   }
+  c->srv_cmd_live = false;
+  if (c->fail_kind == 0) return MPPI_OK;
   ++c->srv_failed;
   quiesce(c);
   rearm_counters(c);
@@ -745,6 +792,11 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
 // next slot, ordering the context stream after the tail that last used them.
 int prepare_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, int mode, double* record_out,
                    FinishArgs& f, int& par) {
+  // a server step's deferred tail (its completion word was seen) takes its slot first, so the slot
+  // picked below is not the one it still has to read and write
+  const int rc = flush_tail(c);
+  if (rc) return rc;
+  c->srv_cmd_live = false;
   fill_finish(c, pl, st, f);
   if (mode == 1 && c->async_tail) mode = 2;
   f.mode = mode;
@@ -924,8 +976,10 @@ void remember(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
 // workgroups (C1-C3).  Per step the host waits (normally not at all) for the step's normals and the
 // tail slot it reuses, writes the command (state, slots, nominal buffer, the slot for the normals of
 // step + 2 that the server's noise phase generates, then seq), launches the server if it is not
-// running, enqueues the deferred optimal rollout (in-kernel gate on fin_done), and spins on the
-// completion word.  No launch and no kernel boundary on the step's path: the gap between two steps
+// running, launches the PREVIOUS step's deferred optimal rollout (flush_tail: its completion word has
+// been seen) and spins on the completion word.  This step's tail stays on the host (tail_deferred)
+// until the next step, sync_tail (get_outputs and every call that quiesces before reading the DEM)
+// or prepare_finish (any separate-launch finish: it takes the slot after the deferred one).  No launch and no kernel boundary on the step's path: the gap between two steps
 // is the host's round trip (completion word seen -> next command) plus one poll of pinned memory.
 bool server_shape(const mppi_ctx* c, const Plan& pl, int mode, int* P, int* ncol, int* groups, size_t* lds) {
   // (every workgroup of the server must be resident at once: one rollout block per CU at most)
@@ -942,9 +996,7 @@ bool server_shape(const mppi_ctx* c, const Plan& pl, int mode, int* P, int* ncol
 int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int ncol, int groups, size_t lds) {
   if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
   const double tq = c->trace ? now_us() : 0.0;
-  // a server idle for more than half its limit may be exiting: stop it and start a fresh one
-  if (c->srv_running && (proj != c->srv_proj || now_us() - c->srv_last_us > 0.5 * (double)c->srv_idle_us))
-    quiesce(c);
+  if (c->srv_running && proj != c->srv_proj) quiesce(c);
   // (first step: the buffers are allocated before the server holds pointers to them)
   if (c->srv_running && (c->nodes_cap < (size_t)pl.blocks * E_of(c) || c->eps_cap < (size_t)pl.blocks * 2 * H_of(c) * 256))
     quiesce(c);
@@ -966,10 +1018,7 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   // the server's noise phase runs mostly in the workgroups outside the finish: with fewer than a
   // quarter of them, or fewer than two (few records: every rollout workgroup may hold a finish
   // column) the noise kernel does it
-#ifndef MPPI_SRV_HOST_NOISE
-#define MPPI_SRV_HOST_NOISE 0  // A/B builds: the noise kernel beside the server at every size
-#endif
-  const bool srv_noise = !MPPI_SRV_HOST_NOISE && pl.blocks - groups >= 2 &&
+  const bool srv_noise = pl.blocks - groups >= 2 &&
                          (int64_t)(pl.blocks - groups) * 4 >= (int64_t)pl.blocks;
   int noise_slot = -1;
   for (int d = 1; d <= 2; ++d) {
@@ -1014,46 +1063,24 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   c->srv_cmd_noise = noise_slot;
   d.noise_n_base_lo = (unsigned)((step + 2) * nb);
   d.noise_n_base_hi = (unsigned)(((step + 2) * nb) >> 32);
+  // a server idle for more than half its limit may be leaving: stop it and start a fresh one.  This
+  // is checked after the host's waits above, right before the command is posted; a head that leaves
+  // anyway (a slower host) never relays the command, and wait_done relaunches the server with it
+  if (c->srv_running && now_us() - c->srv_last_us > 0.5 * (double)c->srv_idle_us) quiesce(c);
   unsigned* cw = reinterpret_cast<unsigned*>(cmd);
   const unsigned* dw = reinterpret_cast<const unsigned*>(&d);
   for (int i = 2; i < kCmdWords; ++i) __atomic_store_n(cw + i, dw[i], __ATOMIC_RELAXED);
   __atomic_store_n(&cmd->seq, seq, __ATOMIC_RELEASE);
+  c->srv_pl = pl;
+  c->srv_P = P;
+  c->srv_ncol = ncol;
+  c->srv_groups = groups;
+  c->srv_lds = lds;
+  c->srv_proj = proj;
+  c->srv_cmd_live = true;
   if (!c->srv_running) {
-    // (no reset of the relay: its seq word is older than this command, and its stop word holds
-    // the first seq of the launch that wrote it, never this one's)
-    RolloutArgs a;
-    fill_rollout(c, pl, c->st, step, c->u_nom[c->cur], a);
-    ServerArgs z;
-    std::memset(&z, 0, sizeof(z));
-    fill_finish(c, pl, c->st, z.f);
-    z.f.recs = c->nodes;
-    z.f.rec_m = c->rec_m;
-    z.f.n_recs = pl.blocks;
-    z.f.level1 = c->level1;
-    z.f.level1_cnt = c->level1_cnt;
-    z.f.done = c->done;
-    z.nroll = pl.blocks;
-    z.fin_P = P;
-    z.fin_ncol = ncol;
-    z.fin_groups = groups;
-    z.rec_cnt = c->level1_cnt + 16;
-    z.cmd = c->cmd;
-    z.relay = c->relay;
-    z.clk = c->clk;
-    for (int i = 0; i < kEpsSlots; ++i) z.eps[i] = c->eps[i];
-    z.u_nom[0] = c->u_nom[0];
-    z.u_nom[1] = c->u_nom[1];
-    for (int i = 0; i < kTailSlots; ++i) {
-      z.tail_in[i] = c->tail_in[i];
-      z.tail_out[i] = c->tail_host[i];
-    }
-    z.first_seq = seq;
-    z.wait_ticks = c->fin_wait_ticks;
-    z.idle_ticks = c->srv_idle_us * 100;
-    HIP_TRY(launch_step_server(a, z, lds, c->stream, proj));
-    c->srv_running = true;
-    c->srv_proj = proj;
-    ++c->srv_launches;
+    rc = launch_server(c, seq);
+    if (rc) return rc;
   }
   c->srv_last_us = now_us();
   if (c->trace) {
@@ -1118,26 +1145,23 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   if (rc) return rc;
   c->last_resident = resident;
   remember(c, proj, step, mode, pl);
-  if (resident && !c->trace) {
-    rc = copy_outputs(c, out);
-    // a server that never ran the command (it cannot hold all its workgroups on the device at once,
-    // e.g. under a counter-collecting profiler that serializes dispatches): separate launches from
-    // now on, this step again (it published nothing and changed no state)
-    if (rc == MPPI_EHIP && c->fail_kind == 2) {
-      if (!c->srv_warned)
-        std::fprintf(stderr, "mppi: the resident step server could not run here; using separate launches\n");
-      c->srv_warned = true;
-      c->resident = false;
-      c->last_resident = false;
-      rc = enqueue_step(c, proj, step, mode, pl);
-      if (rc) return rc;
-      return copy_outputs(c, out);
-    }
-    return rc;
-  }
-  if (!c->trace) return copy_outputs(c, out);
-  const double t2 = now_us();
+  const double t2 = c->trace ? now_us() : 0.0;
   rc = copy_outputs(c, out);
+  // a freshly launched server that retired without serving its first command (it cannot hold all
+  // its workgroups on the device at once): separate launches from now on, this step again (it
+  // published nothing and changed no state).  A server that left on its idle limit as the command
+  // was posted is not this case: wait_done relaunched it.
+  if (resident && rc == MPPI_EHIP && c->fail_kind == 2) {
+    if (!c->srv_warned)
+      std::fprintf(stderr, "mppi: the resident step server could not run here; using separate launches\n");
+    c->srv_warned = true;
+    c->resident = false;
+    c->last_resident = false;
+    rc = enqueue_step(c, proj, step, mode, pl);
+    if (rc) return rc;
+    rc = copy_outputs(c, out);
+  }
+  if (!c->trace) return rc;
   const double t3 = now_us();
   if (c->tr_prev_done > 0) {
     c->tr_sum[0] += c->tr_t0 - c->tr_prev_done;
@@ -1308,8 +1332,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
       hipMalloc(&c->uopt, (size_t)2 * H * sizeof(unsigned long long)) != hipSuccess ||
       hipHostMalloc(&c->cmd, sizeof(ServerCmd), hipHostMallocDefault) != hipSuccess ||
       hipMalloc(&c->relay, 64 * sizeof(unsigned)) != hipSuccess ||
-      hipMalloc(&c->clk, kClkWords * sizeof(uint64_t)) != hipSuccess ||
-      hipMalloc(&c->record, (2 * H + 2) * sizeof(double)) != hipSuccess)
+      hipMalloc(&c->clk, kClkWords * sizeof(uint64_t)) != hipSuccess)
     return cleanup(fail(MPPI_EHIP, "device allocation failed"));
   for (int i = 0; i < kTailSlots; ++i)
     if (hipMalloc(&c->tail_in[i], 3 * H * sizeof(float)) != hipSuccess ||
@@ -1382,7 +1405,6 @@ void mppi_destroy(mppi_ctx* c) {
   if (c->nodes) hipFree(c->nodes);
   if (c->scratch0) hipFree(c->scratch0);
   if (c->scratch1) hipFree(c->scratch1);
-  if (c->record) hipFree(c->record);
   if (c->ustore) hipFree(c->ustore);
   if (c->stage) hipHostFree(c->stage);
   if (c->done) hipHostFree(c->done);
@@ -1708,6 +1730,11 @@ int mppi_set_option(mppi_ctx* c, const char* name, int64_t value) {
     c->colfin = value == 0;
     return MPPI_OK;
   }
+  if (n == "server_exit_after") {  // test hook: the next server launch's head leaves after this many commands
+    if (value < 0 || value > 1000000) return fail(MPPI_EINVAL, "server_exit_after must be in [0, 1e6]");
+    c->srv_exit_after = (unsigned)value;
+    return MPPI_OK;
+  }
   if (n == "finish_wait_ticks") {  // the server finish's record wait bound (100 MHz ticks; 0: give up at once)
     if (value < 0) return fail(MPPI_EINVAL, "finish_wait_ticks must be >= 0");
     c->fin_wait_ticks = (uint64_t)value;
@@ -1824,23 +1851,16 @@ int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
       const uint64_t x = v[kClkServer + 8 * ((last + 1 + r) & 7) + k];
       if (idx < n) out[idx] = x && lo != UINT64_MAX ? (double)(x - lo) / 100.0 : 0.0;
     }
-  // then (diagnostic builds with MPPI_DIAG_W0) workgroup 0's per-wave stamps of its last step: 16
-  // noise ends, 16 end-of-step arrivals (same origin), then that step's seq
-  for (int k = 0; k < 33; ++k) {
-    const int idx = 10 + nb + 64 + k;
-    const uint64_t x = v[kClkBase + 2 * 4000 + k];
-    if (idx < n) out[idx] = k == 32 ? (double)x : (x && lo != UINT64_MAX ? ((double)x - (double)lo) / 100.0 : 0.0);
-  }
   return MPPI_OK;
 }
 
 int mppi_get_launch_info(mppi_ctx* c, int64_t* info, int32_t n) {
   if (!c || !info) return fail(MPPI_EINVAL, "null argument");
   const Plan& pl = c->last_plan;
-  const int64_t v[15] = {0, pl.block, pl.blocks, pl.W, pl.Wr, (int64_t)pl.lds_bytes, c->fin_kind,
+  const int64_t v[16] = {0, pl.block, pl.blocks, pl.W, pl.Wr, (int64_t)pl.lds_bytes, c->fin_kind,
                          c->fin_P, c->fin_ncol, c->fin_groups, pl.ucache_steps, c->last_resident ? 1 : 0,
-                         c->srv_launches, c->srv_steps, c->srv_failed};
-  for (int i = 0; i < n && i < 15; ++i) info[i] = v[i];
+                         c->srv_launches, c->srv_steps, c->srv_failed, c->srv_relaunches};
+  for (int i = 0; i < n && i < 16; ++i) info[i] = v[i];
   return MPPI_OK;
 }
 

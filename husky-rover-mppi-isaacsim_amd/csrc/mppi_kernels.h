@@ -24,10 +24,8 @@ struct ServerCmd {
   unsigned noise_n_base_hi;
   unsigned pad1[7];
 };
-#ifndef MPPI_TAIL_SLOTS
-#define MPPI_TAIL_SLOTS 4  // A/B builds
-#endif
-constexpr int kTailSlots = MPPI_TAIL_SLOTS;   // deferred optimal rollouts in flight (mppi_capi.cpp)
+constexpr int kTailSlots = 4;  // deferred optimal rollouts in flight (mppi_capi.cpp; 8 / 16 measured
+                               // within noise, profiles/r04_notes.md)
 constexpr int kCmdWords = 25;                 // the words a step reads (seq .. noise_n_base_hi)
 constexpr unsigned kDoneFail = 0x80000000u;   // done | kDoneFail: the step's finish gave up
 struct FinishArgs {
@@ -51,8 +49,6 @@ struct FinishArgs {
   float x_min, y_min, res;
   float rinv_res;
   int cdiv_res;
-  int wx0, wy0, W, Wr;
-  int win_offset;  // LDS byte offset of the window
   float x0, y0, h0x, h0y, h0z, wl, wr;
   float ok, oa, rwheel, vmin, vmax, wmin, wmax, dt, off;
   // deferred optimal rollout (mode 2 / mppi_tail_kernel)
@@ -134,7 +130,7 @@ constexpr int kClkBase = 8, kClkBlocks = 4096;
 constexpr int kClkServer = kClkBase + 2 * kClkBlocks, kClkSums = kClkServer + 64, kClkWords = kClkSums + 8;
 // The finish's phase-2 LDS (finish_phase2): uo[2][PS] v w sin cos[H] chain[12H] out[16H]
 // lr[2][PS] floats, PS = the filter rows' stride (a multiple of 4 floats, >= H + 32 for the
-// filter's read-ahead); the DEM window (LDS finish) starts at fin_phase2_floats(H) floats.
+// filter's read-ahead).
 __host__ __device__ inline int fin_plane_stride(int H) { return ((H + 3) & ~3) + 32; }
 __host__ __device__ inline int fin_phase2_floats(int H) { return 4 * fin_plane_stride(H) + 32 * H; }
 
@@ -143,19 +139,12 @@ __host__ __device__ inline int fin_phase2_floats(int H) { return 4 * fin_plane_s
 // chain wave and a side wave per 64 trajectories, synchronised through LDS progress counters
 // over PAIR_RING-deep rings.
 constexpr int PAIR_TRAJ = 256;
-#ifndef MPPI_PAIR_D
-#define MPPI_PAIR_D 6  // round 4: 6 beats 8 at C3 by ~1.4 % (the control cache holds 48 steps instead
-                       // of 40), C4 and the C4 shard unchanged (profiles/r04_notes.md)
-#endif
-constexpr int PAIR_RING = MPPI_PAIR_D;  // = PAIR_D in mppi_kernels.hip
-// sin / cos / 1 - cos of the Rodrigues angle computed by the side wave at production and handed to
-// the chain through the ring, off the chain's serial path (the chain is then chain_wave_3d, as in
-// the role-split kernel); 0 = the chain computes them (the unpacked chain3d_lean step)
-#ifndef MPPI_SC_SIDE
-#define MPPI_SC_SIDE 1
-#endif
-constexpr int PAIR_RING_IN = MPPI_SC_SIDE ? 4 : 2;  // floats per trajectory and step, side -> chain
-                                                    // (v, sin, cos, 1 - cos) or (v, w)
+// ring depth: round 4, 6 beats 8 at C3 by ~1.4 % (the control cache holds 48 steps instead of 40),
+// C4 and the C4 shard unchanged (profiles/r04_notes.md)
+constexpr int PAIR_RING = 6;  // = PAIR_D in mppi_kernels.hip
+// floats per trajectory and step, side -> chain: (v, sin, cos, 1 - cos) of the Rodrigues angle,
+// computed by the side wave at production, off the chain's serial path
+constexpr int PAIR_RING_IN = 4;
 hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
                                int mode, bool dump, bool roles = false);
 // The role-split rollout kernel (mppi_rollout_roles_kernel): the same 256 trajectories per
@@ -164,8 +153,8 @@ hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hip
 constexpr int ROLES_WAVES_PER_TRAJ_WAVE = 4;
 // The resident step server (mppi_step_server_kernel): one workgroup per 256 trajectories of the
 // role-split rollout, resident across steps.  Per step every workgroup waits for cmd->seq to reach
-// the next sequence number (or cmd->stop, or idle_ticks of the 100 MHz clock without a command:
-// then it exits), runs its rollout and writes its record through, and takes a ticket from rec_cnt;
+// the next sequence number (or cmd->stop; the head also leaves after idle_ticks of the 100 MHz
+// clock without a command, and the others leave on the stop it relays), runs its rollout and writes its record through, and takes a ticket from rec_cnt;
 // the workgroups holding the last fin_groups tickets run the column-split finish (each after rec_cnt
 // reaches nroll, or wait_ticks: then the step publishes done | kDoneFail); the other workgroups
 // generate the normals of step + 2 meanwhile (ServerCmd::noise_slot, a static share per ticket;
@@ -185,8 +174,10 @@ struct ServerArgs {
   float* tail_out[kTailSlots];  // its outputs per slot (pinned)
   unsigned first_seq;
   uint64_t wait_ticks;        // a finish's record wait bound
-  uint64_t idle_ticks;        // exit after this long without a command
-  uint64_t* clk;              // optional: the server stamps [kClkServer, kClkServer + 4) of RolloutArgs::clk
+  uint64_t idle_ticks;        // the head leaves after this long without a command (and relays the stop)
+  unsigned exit_after;        // test hook (0: off): the head leaves at its poll after serving this many
+                              // commands, whether or not the next one was posted
+  uint64_t* clk;             // optional: the server stamps [kClkServer, kClkServer + 4) of RolloutArgs::clk
 };
 hipError_t launch_step_server(const RolloutArgs& a, const ServerArgs& z, size_t lds, hipStream_t st, int proj);
 // record tree finish (mppi_finish_kernel): the fallback where the column-split shape does not fit

@@ -12,7 +12,7 @@
 //   mppi_tail_kernel  the rest of the optimal rollout, on a side stream.
 //   mppi_noise_kernel the Philox sampling normals, two steps ahead, on a side stream.
 // mppi_finish_kernel (the record tree) is the finish where the column split does not fit
-// (MPPI_COLFIN=0 selects it everywhere).
+// (mppi_set_option "record_tree_finish" selects it everywhere).
 //
 // Numerics: compile with -ffp-contract=off.  Every float op is one IEEE f32
 // operation in the reference's source order; transcendentals come from
@@ -134,30 +134,22 @@ __device__ __forceinline__ int trunc_clamped(float f, float lo, float hi) {
 }
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
 
-template <bool LDS>
 struct Dem {
   const float* Z;    // global DEM (row-major rows x grid)
-  const float* win;  // LDS window (Wr x W), LDS only
-  int rows, grid, wx0, wy0, W, Wr;
+  int rows, grid;
   float x_min, y_min, res;
   Recip rres;  // fast-path reciprocal of res (res is validated on the host)
   float rinv;  // verified reciprocal for cdiv_f (cdiv != 0)
   int cdiv;
   const float4* N = nullptr;  // per-cell normals (normal_cell), global path only
 
-  __device__ __forceinline__ void init(const float* Z_, const float* win_, int rows_, int grid_,
-                                       int wx0_, int wy0_, int W_, int Wr_, float x_min_,
-                                       float y_min_, float res_, float rinv_ = 0.0f, int cdiv_ = 0) {
+  __device__ __forceinline__ void init(const float* Z_, int rows_, int grid_, float x_min_, float y_min_,
+                                       float res_, float rinv_ = 0.0f, int cdiv_ = 0) {
     rinv = rinv_;
     cdiv = cdiv_;
     Z = Z_;
-    win = win_;
     rows = rows_;
     grid = grid_;
-    wx0 = wx0_;
-    wy0 = wy0_;
-    W = W_;
-    Wr = Wr_;
     x_min = x_min_;
     y_min = y_min_;
     res = res_;
@@ -186,13 +178,7 @@ struct Dem {
   __device__ __forceinline__ float at(int row, int col) const {
     row = clampi(row, 0, rows - 1);
     col = clampi(col, 0, grid - 1);
-    if constexpr (LDS) {
-      const int r = clampi(row - wy0, 0, Wr - 1);
-      const int c = clampi(col - wx0, 0, W - 1);
-      return win[r * W + c];
-    } else {
-      return Z[(size_t)row * grid + col];
-    }
+    return Z[(size_t)row * grid + col];
   }
   // projection_warp.py:8-48
   template <bool F>
@@ -201,32 +187,17 @@ struct Dem {
     cell<F>(x, y, i, j, bad);
     const int r0 = clampi(j, 0, rows - 1), r1 = clampi(j + 1, 0, rows - 1);
     const int c0 = clampi(i, 0, grid - 1), c1 = clampi(i + 1, 0, grid - 1);
-    if constexpr (LDS) {
-      const int a0 = clampi(r0 - wy0, 0, Wr - 1) * W, a1 = clampi(r1 - wy0, 0, Wr - 1) * W;
-      const int b0 = clampi(c0 - wx0, 0, W - 1), b1 = clampi(c1 - wx0, 0, W - 1);
-      q[0] = win[a0 + b0];
-      q[1] = win[a0 + b1];
-      q[2] = win[a1 + b0];
-      q[3] = win[a1 + b1];
-    } else {
-      q[0] = Z[(size_t)r0 * grid + c0];
-      q[1] = Z[(size_t)r0 * grid + c1];
-      q[2] = Z[(size_t)r1 * grid + c0];
-      q[3] = Z[(size_t)r1 * grid + c1];
-    }
+    q[0] = Z[(size_t)r0 * grid + c0];
+    q[1] = Z[(size_t)r0 * grid + c1];
+    q[2] = Z[(size_t)r1 * grid + c0];
+    q[3] = Z[(size_t)r1 * grid + c1];
   }
   // normal of the cell (i, j) from the table: i in [-1, grid], j in [-1, rows] as cell()
   // returns them; i = grid selects the same corners as i = grid - 1 (both clamp to the last
   // column), so the table has (rows + 1) x (grid + 1) entries
   __device__ __forceinline__ float4 normal_cell(int i, int j) const {
     const int ii = min(i, grid - 1) + 1, jj = min(j, rows - 1) + 1;
-#if defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 1  // diagnostic builds only: one cell (L1 hits)
-    return N[(uint32_t)((jj * (grid + 1) + ii) & 0)];
-#elif defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 2  // diagnostic: no load
-    return make_float4(__builtin_bit_cast(float, jj) * 1e-30f, __builtin_bit_cast(float, ii) * 1e-30f, 1.0f, 0.f);
-#else
     return N[(uint32_t)(jj * (grid + 1) + ii)];
-#endif
   }
   // cell() + at() in two instructions per index: clamp(trunc(clamp(f, -1, grid)), 0, grid - 1)
   // == trunc(med3(f, 0, grid - 1)) and clamp(-trunc(clamp(f, -rows, 1)), 0, rows - 1)
@@ -244,13 +215,7 @@ struct Dem {
     }
     const int col = (int)__builtin_amdgcn_fmed3f(fi, 0.0f, (float)(grid - 1));
     const int row = -(int)__builtin_amdgcn_fmed3f(fj, (float)(1 - rows), 0.0f);
-    if constexpr (LDS) {
-      const int r = clampi(row - wy0, 0, Wr - 1);
-      const int c = clampi(col - wx0, 0, W - 1);
-      return win[r * W + c];
-    } else {
-      return Z[(size_t)row * grid + col];
-    }
+    return Z[(size_t)row * grid + col];
   }
 };
 
@@ -285,8 +250,8 @@ struct StepOut {
 // Serial part of one 3D rollout-step (projection_warp.py:314-326): position
 // update, corner lookup, normal, tangent projection, Rodrigues yaw.  (sn, cs)
 // = dm_sincosf(w*dt).  Leaves the new heading in s and the quad / normal in q, n.
-template <bool F, bool LDS>
-__device__ __forceinline__ void chain3d(const Dem<LDS>& dem, float res_half_neg, float res_sq,
+template <bool F>
+__device__ __forceinline__ void chain3d(const Dem& dem, float res_half_neg, float res_sq,
                                         float dt, float v, float sn, float cs, Traj& s,
                                         float (&q)[4], float& nx, float& ny, float& nz, bool& bad) {
   {  // _update_position :207-223
@@ -331,10 +296,10 @@ __device__ __forceinline__ void chain3d(const Dem<LDS>& dem, float res_half_neg,
   }
 }
 
-// ---------------------------------------------------------------------  lean chain
-// The pair kernel's chain wave issues about one VALU op per 4 cycles on its own,
-// so its step time is mostly instruction count.  chain3d_lean computes the same
-// values as chain3d<true> with fewer instructions:
+// ---------------------------------------------------------------------  lean guards
+// A chain wave issues about one instruction per ~5 cycles on its own, so its step time is mostly
+// instruction count.  The chains (chain_wave_3d, tail_chain_3d) compute the values of chain3d<true>
+// with fewer instructions:
 //  * range guards folded into running extrema instead of a compare-and-OR per
 //    operand: the smallest frexp exponent over the numerators (a zero numerator
 //    has exponent 0 and passes) and the min / max bit pattern of the squared
@@ -348,9 +313,6 @@ __device__ __forceinline__ void chain3d(const Dem<LDS>& dem, float res_half_neg,
 // divisors in [2^-40, 2^40] and every quotient / residual normal).  A lane out
 // of range redoes the step with chain3d<false> (IEEE), so results never depend
 // on the path; mppi_selftest (what 2, 3) checks the primitives bitwise.
-#ifndef MPPI_LEAN_CHAIN
-#define MPPI_LEAN_CHAIN 1  // diagnostic builds: 0 = chain3d<true> in the pair kernel
-#endif
 struct Lean {
   int emin;      // min frexp exponent of the numerators
   int nlo, nhi;  // min / max bit pattern of the squared norms
@@ -399,88 +361,13 @@ __device__ __forceinline__ float lean_div(float a, const Recip& r, Lean& l) {
   return __builtin_copysignf(__builtin_fmaf(e0, r.y, q0), a);
 }
 
-// chain3d<true> with the lean guards (see above); DEM corners through 32-bit
-// offsets from the uniform base (rows * grid < 2^29, checked by mppi_set_dem).
-__device__ __forceinline__ float dem_at32(const float* Z, int off) {
-  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(Z) + (uint32_t)(off << 2));
-}
-// NTAB: the normal comes from the per-cell table (dem.N, the IEEE normal of the same
-// four corners) and q is not filled in.
-template <bool NTAB = false>
-__device__ __forceinline__ void chain3d_lean(const Dem<false>& dem, float res_half_neg, float res_sq,
-                                             float dt, float v, float sn, float cs, Traj& s, float (&q)[4],
-                                             float& nx, float& ny, float& nz, bool& bad) {
-  Lean l;
-  lean_init(l);
-  {  // _update_position :207-223
-    const Recip r = lean_norm((s.hx * s.hx + s.hy * s.hy) + s.hz * s.hz, l);
-    const float ux = lean_div(s.hx, r, l), uy = lean_div(s.hy, r, l);
-    s.x = s.x + (ux * v) * dt;
-    s.y = s.y + (uy * v) * dt;
-  }
-  if constexpr (NTAB) {  // projection_warp.py:8-48 + _normal_on_grid :129-151 (per-cell table)
-    int i, j;
-    dem.template cell<true>(s.x, s.y, i, j, bad);
-    const float4 nv = dem.normal_cell(i, j);
-    nx = nv.x;
-    ny = nv.y;
-    nz = nv.z;
-  } else {
-    {  // projection_warp.py:8-48
-      int i, j;
-      dem.template cell<true>(s.x, s.y, i, j, bad);
-      const int r0 = clampi(j, 0, dem.rows - 1), r1 = clampi(j + 1, 0, dem.rows - 1);
-      const int c0 = clampi(i, 0, dem.grid - 1), c1 = clampi(i + 1, 0, dem.grid - 1);
-      const int o0 = r0 * dem.grid, o1 = r1 * dem.grid;
-      q[0] = dem_at32(dem.Z, o0 + c0);
-      q[1] = dem_at32(dem.Z, o0 + c1);
-      q[2] = dem_at32(dem.Z, o1 + c0);
-      q[3] = dem_at32(dem.Z, o1 + c1);
-    }
-    {  // _normal_on_grid :129-151
-      const float vx = res_half_neg * (((q[1] - q[0]) - q[2]) + q[3]);
-      const float vy = res_half_neg * (((q[2] - q[0]) - q[1]) + q[3]);
-      const Recip r = lean_norm((vx * vx + vy * vy) + res_sq * res_sq, l);
-      nx = lean_div(vx, r, l);
-      ny = lean_div(vy, r, l);
-      nz = lean_div(res_sq, r, l);
-    }
-  }
-  float tx, ty, tz;
-  {  // _get_heading_tangent_vector :168-190
-    const float d = (s.hx * nx + s.hy * ny) + s.hz * nz;
-    tx = s.hx - d * nx;
-    ty = s.hy - d * ny;
-    tz = s.hz - d * nz;
-    const Recip r = lean_norm((tx * tx + ty * ty) + tz * tz, l);
-    tx = lean_div(tx, r, l);
-    ty = lean_div(ty, r, l);
-    tz = lean_div(tz, r, l);
-  }
-  {  // _update_orientation :225-248 (Rodrigues about n)
-    const Recip ro = lean_norm((tx * tx + ty * ty) + tz * tz, l);
-    const float ox = lean_div(tx, ro, l), oy = lean_div(ty, ro, l), oz = lean_div(tz, ro, l);
-    const float crx = ny * oz - nz * oy, cry = nz * ox - nx * oz, crz = nx * oy - ny * ox;
-    const float dn = (nx * ox + ny * oy) + nz * oz;
-    const float omc = 1.0f - cs;
-    const float rx = (ox * cs + crx * sn) + (nx * dn) * omc;
-    const float ry = (oy * cs + cry * sn) + (ny * dn) * omc;
-    const float rz = (oz * cs + crz * sn) + (nz * dn) * omc;
-    const Recip r = lean_norm((rx * rx + ry * ry) + rz * rz, l);
-    s.hx = lean_div(rx, r, l);
-    s.hy = lean_div(ry, r, l);
-    s.hz = lean_div(rz, r, l);
-  }
-  bad |= lean_bad(l);
-}
-
 // ---------------------------------------------------------------------  packed chain (roles kernel)
 // The role-split kernel's chain wave is bound by its own instruction issue (one wave issues
 // about one instruction per 5 cycles, whatever its type), so the serial step is written with
 // packed-FP32 instructions (v_pk_mul / v_pk_add / v_pk_fma: the x and y components in one
 // instruction, each lane an ordinary IEEE f32 operation, results unchanged) wherever the
-// reference computes the same operation on x and y.  Range guards and the IEEE redo as
-// chain3d_lean.
+// reference computes the same operation on x and y.  Range guards (Lean) and the IEEE redo as
+// above.
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
@@ -672,8 +559,8 @@ __device__ __forceinline__ f2 advance_step(const Head& h, float v, float dt, f2 
 
 // Height and wheel contacts of a rollout-step (projection_warp.py:318, :333-348),
 // right = offset * cross(normal, current_hv).
-template <bool F, bool LDS>
-__device__ __forceinline__ void wheels3d(const Dem<LDS>& dem, float off, float x, float y,
+template <bool F>
+__device__ __forceinline__ void wheels3d(const Dem& dem, float off, float x, float y,
                                          const float (&q)[4], float nx, float ny, float nz,
                                          float hx, float hy, float hz, StepOut& o, bool& bad) {
   o.z = bilinear<F>(x, y, q, dem.template rr<F>(), bad);
@@ -688,8 +575,8 @@ __device__ __forceinline__ void wheels3d(const Dem<LDS>& dem, float off, float x
 }
 
 // 2D step: projection_warp.py:373-382 (wheels DEFINED as zero).
-template <bool F, bool LDS>
-__device__ __forceinline__ void step2d(const Dem<LDS>& dem, float dt, float v, float sn, float cs,
+template <bool F>
+__device__ __forceinline__ void step2d(const Dem& dem, float dt, float v, float sn, float cs,
                                        Traj& s, StepOut& o, bool& bad) {
   {
     const Recip r = rc<F>(sq<F>((s.hx * s.hx + s.hy * s.hy) + s.hz * s.hz, bad), bad);
@@ -1158,17 +1045,8 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
 //                  consume p-L (needs chained > p - L)           -> consumed = p - L + 1
 // with L = PAIR_LAG; deadlock-free for 0 < L < D (the chain's waits are always
 // satisfied by side iterations that do not wait on it).  Bitwise identical results.
-#ifndef MPPI_EPS_NT
-#define MPPI_EPS_NT 0  // A/B builds: the producer's loads of rows the leaf does not re-read are non-temporal
-#endif
-#ifndef MPPI_PAIR_LAG
-#define MPPI_PAIR_LAG 4  // the largest even lag below D = 6 (at D = 8, 6 beat 2 and 4: profiles/r01_notes.md)
-#endif
-#ifndef MPPI_FLAG_CACHE
-#define MPPI_FLAG_CACHE 1  // diagnostic builds: 0 = read the partner's counter at every wait
-#endif
-constexpr int PAIR_D = MPPI_PAIR_D;
-constexpr int PAIR_LAG = MPPI_PAIR_LAG;
+constexpr int PAIR_D = PAIR_RING;
+constexpr int PAIR_LAG = 4;  // the largest even lag below D = 6 (at D = 8, 6 beat 2 and 4: profiles/r01_notes.md)
 static_assert(PAIR_LAG > 0 && PAIR_LAG < PAIR_D, "ring depth must exceed the consume lag");
 static_assert(PAIR_LAG % 2 == 0, "the side loop pairs even and odd steps");
 
@@ -1215,7 +1093,7 @@ __device__ __forceinline__ void lds_wait_ge(const int* f, int target, int& seen,
 }
 
 template <int TB, int NC, bool DUMP>
-__device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<false>& dem, const Traj& s, int tj,
+__device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem& dem, const Traj& s, int tj,
                                               bool valid, int64_t kl, const float* ring_in, float* ring_out,
                                               const int* f_prod, int* f_chain, const int* const (&f_cons)[NC],
                                               int& seen_prod, int (&seen_cons)[NC], WaitStat& ws) {
@@ -1265,13 +1143,7 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem<fa
         const int ti = (int)__builtin_amdgcn_fmed3f(f.x, -1.0f, fi_hi);  // min(i, grid - 1)
         const int tjj = (int)__builtin_amdgcn_fmed3f(f.y, fj_lo, 1.0f);  // -min(j, rows - 1)
         const int idx = __mul24(tjj, -nrow) + (ti + ncol0);
-#if defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 1  // diagnostic builds only: one cell (L1 hits)
-        nv = *reinterpret_cast<const float4*>(nbase + ((uint32_t)(idx << 4) & 0u));
-#elif defined(MPPI_DIAG_NTAB) && MPPI_DIAG_NTAB == 2  // diagnostic: no load
-        nv = make_float4(__builtin_bit_cast(float, idx) * 1e-30f, 0.f, 1.0f, 0.f);
-#else
         nv = *reinterpret_cast<const float4*>(nbase + (uint32_t)(idx << 4));
-#endif
       };
       auto read_in = [&](int t, float& v, float& sn, float& cs, float& om, int need) __attribute__((always_inline)) {
         if (need) lds_wait_ge(f_prod, need, seen_prod, ws);
@@ -1411,8 +1283,8 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   const int64_t kl = (int64_t)blockIdx.x * TB + tj;
   const bool valid = kl < a.K;
   const int H = a.H;
-  Dem<false> dem;
-  dem.init(a.Z, nullptr, a.rows, a.grid, 0, 0, 1, 1, a.x_min, a.y_min, a.res, a.rinv_res, a.cdiv_res);
+  Dem dem;
+  dem.init(a.Z, a.rows, a.grid, a.x_min, a.y_min, a.res, a.rinv_res, a.cdiv_res);
   dem.N = a.ntab;
   const float res_half_neg = (-a.res) / 2.0f;
   const float res_sq = a.res * a.res;
@@ -1471,9 +1343,7 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   // once it has acquired that value, so a cached value that already covers the target
   // needs no LDS read and no fence (the partner usually runs several steps ahead).
   auto wait_ge = [&](const int* f, int target, int& seen) __attribute__((always_inline)) {
-#if MPPI_FLAG_CACHE
     if (seen >= target) return;
-#endif
 #ifdef MPPI_STAMPS
     const uint64_t t0 = dbg_stamp();
 #endif
@@ -1488,7 +1358,6 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   if (!side) {
     // ---------------- chain wave: the serial projection, one step per iteration
     int seen_prod = 0, seen_cons = 0;
-#if MPPI_SC_SIDE
     if constexpr (PROJ == 3) {
       const int* cons[1] = {f_cons};
       int seen_c[1] = {0};
@@ -1499,43 +1368,17 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
       st_wait += ws.wait;
 #endif
     } else
-#endif
-    for (int sc = 0; sc < H; ++sc) {
+    for (int sc = 0; sc < H; ++sc) {  // 2D: the planar step (projection_warp.py:353-382)
       wait_ge(f_prod, sc + 1, seen_prod);
       wait_ge(f_cons, sc - D + 1, seen_cons);
       const float* ri = ring_in + (sc % D) * RI * TB + tj;
       const float v = ri[0];
-      float sn, cs;  // sin/cos of the Rodrigues angle: independent of the chain state
-#if MPPI_SC_SIDE
-      sn = ri[TB];
-      cs = ri[2 * TB];
-#else
-      dm_sincosf(ri[TB] * a.dt, &sn, &cs);
-#endif
-      float cx = 0.f, cy = 0.f, z = 0.f;
-      float q[4];
-      if constexpr (PROJ == 3) {
-        float nx, ny, nz;
-        bool bad = false;
-        const Traj saved = s;
-#if MPPI_LEAN_CHAIN
-        chain3d_lean<true>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-        if constexpr (DUMP) dem.template corners<false>(s.x, s.y, q, nobad);  // heights: dump only
-#else
-        chain3d<kChainFast, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-#endif
-        if (__builtin_expect(bad, 0)) {  // operand outside the fast range: IEEE redo
-          s = saved;
-          chain3d<false, false>(dem, res_half_neg, res_sq, a.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-        }
-        cx = a.off * (ny * s.hz - nz * s.hy);
-        cy = a.off * (nz * s.hx - nx * s.hz);
-        if constexpr (DUMP) z = bilinear<false>(s.x, s.y, q, dem.template rr<false>(), nobad);
-      } else {
-        StepOut o;
-        step2d<false, false>(dem, a.dt, v, sn, cs, s, o, nobad);
-        z = o.z;
-      }
+      const float sn = ri[TB], cs = ri[2 * TB];  // sin/cos of the Rodrigues angle (side wave)
+      const float cx = 0.f, cy = 0.f;
+      StepOut o;
+      step2d<false>(dem, a.dt, v, sn, cs, s, o, nobad);
+      const float z = o.z;
+      (void)z;
       float* ro = ring_out + (sc % D) * 4 * TB + tj;
       ro[0] = s.x;
       ro[TB] = s.y;
@@ -1603,7 +1446,6 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
         const float wp = clampf(((-L) + R) / a.rwheel, a.wmin, a.wmax);
         float* ri = ring_in + (p % D) * RI * TB + tj;
         ri[0] = vp;
-#if MPPI_SC_SIDE
         {
           float sn, cs;
           if (a.small_angle) dm_sincosf_small(wp * a.dt, &sn, &cs);
@@ -1612,9 +1454,6 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
           ri[2 * TB] = cs;
           ri[3 * TB] = 1.0f - cs;
         }
-#else
-        ri[TB] = wp;
-#endif
         if constexpr (DUMP) {
           if (valid) {
             const size_t o1 = (size_t)kl * H + p;
@@ -1772,23 +1611,12 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 //   PROD  step p : cost > p - D   (ring_in slot p % D read by CHAIN and COST; COST waited on CHAIN)
 //   WHEEL / COST step s : chained > s
 // Deadlock-free: no wave waits on a later step of a wave that waits on it.
-#ifndef MPPI_COLFIN_FENCED
-#define MPPI_COLFIN_FENCED 0  // 1: release / acquire at agent scope around the finish handoffs (D8)
-#endif
-#ifndef MPPI_SIDE_PRIO
-// issue priority of the producer / wheel / cost waves (the chain's is 3).  0, level with the
-// deferred optimal rollout of the previous step (mppi_tail_kernel) on the CU they share: at 2 the
-// tail, starved, ran ~105 us and into the next finish, and pipelined C3 steps alternated between
-// ~98 and ~120 us (profiles/r02_notes.md); 0: ~9900 against ~9200 steps/s
-#define MPPI_SIDE_PRIO 0
-#endif
-#ifndef MPPI_DIAG_SIDE
-#define MPPI_DIAG_SIDE 0  // diagnostic builds: 1 wheel / cost roles idle, 2 also a constant producer
-#endif
-#ifndef MPPI_PROD_PRIO
-#define MPPI_PROD_PRIO 1  // the producer's (the chain waits on it each step): 1 above the wheel and
-                          // cost roles, +1.3 % C3 steps/s with 6-deep rings (profiles/r04_notes.md)
-#endif
+// Issue priorities: the chain 3; the producer 1 (the chain waits on it each step: +1.3 % C3 steps/s
+// with 6-deep rings, profiles/r04_notes.md); the wheel and cost waves 0, level with the deferred
+// optimal rollout of the previous step (mppi_tail_kernel) on the CU they share: at 2 the tail,
+// starved, ran ~105 us and into the next finish, and pipelined C3 steps alternated between ~98 and
+// ~120 us (profiles/r02_notes.md; 0: ~9900 against ~9200 steps/s).
+constexpr int kProdPrio = 1, kSidePrio = 0;
 constexpr int ROLE_CHAIN = 0, ROLE_PROD = 1, ROLE_WHEEL = 2, ROLE_COST = 3, NROLES = 4;
 
 // FUSED: returns the workgroup's ticket (its rank among the workgroups that have completed their
@@ -1818,8 +1646,8 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
   const int tj = grp * 64 + (tid & 63);  // trajectory within the workgroup
   if (a.wave_prio) {  // above the deferred optimal rollout (priority 0); the chain above all
     if (role == ROLE_CHAIN) __builtin_amdgcn_s_setprio(3);
-    else if (role == ROLE_PROD) __builtin_amdgcn_s_setprio(MPPI_PROD_PRIO);
-    else __builtin_amdgcn_s_setprio(MPPI_SIDE_PRIO);
+    else if (role == ROLE_PROD) __builtin_amdgcn_s_setprio(kProdPrio);
+    else __builtin_amdgcn_s_setprio(kSidePrio);
   }
   int* f_prod = flags + grp;
   int* f_chain = flags + NG + grp;
@@ -1828,8 +1656,8 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
   const int64_t kl = (int64_t)blk * TB + tj;
   const bool valid = kl < a.K;
   const int H = a.H;
-  Dem<false> dem;
-  dem.init(a.Z, nullptr, a.rows, a.grid, 0, 0, 1, 1, a.x_min, a.y_min, a.res, a.rinv_res, a.cdiv_res);
+  Dem dem;
+  dem.init(a.Z, a.rows, a.grid, a.x_min, a.y_min, a.res, a.rinv_res, a.cdiv_res);
   dem.N = a.ntab;
   const float res_half_neg = (-a.res) / 2.0f;
   const float res_sq = a.res * a.res;
@@ -1911,7 +1739,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       const float v = ri[0], sn = ri[TB], cs = ri[2 * TB];
       const float cx = 0.f, cy = 0.f;
       StepOut o;
-      step2d<false, false>(dem, a.dt, v, sn, cs, s, o, nobad);
+      step2d<false>(dem, a.dt, v, sn, cs, s, o, nobad);
       const float z = o.z;
       float* ro = ring_out + (sc % D) * 4 * TB + tj;
       ro[0] = s.x;
@@ -1928,34 +1756,6 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       lds_store_release(f_chain, sc + 1);
     }
   }
-#if MPPI_DIAG_SIDE  // diagnostic builds only: the side roles keep the protocol and skip their work
-  else if (role == ROLE_PROD && MPPI_DIAG_SIDE >= 2) {
-    int seen_cost = 0;
-    for (int p = 0; p < H; ++p) {
-      wait_ge(f_cost, p - D + 1, seen_cost);
-      float* ri = ring_in + (p % D) * RI * TB + tj;
-      const float sn = 0.0123f * (float)(tj & 7) - 0.04f, cs = 0.99f;
-      ri[0] = 0.9f;
-      ri[TB] = sn;
-      ri[2 * TB] = cs;
-      ri[3 * TB] = 1.0f - cs;
-      lds_store_release(f_prod, p + 1);
-    }
-  } else if (role == ROLE_WHEEL) {
-    int seen_chain = 0;
-    for (int sc = 0; sc < H; sc += 2) {
-      wait_ge(f_chain, sc + 1, seen_chain);
-      lds_store_release(f_wheel, min(sc + 2, H));
-    }
-    sw_lds[tj] = 0.f;
-  } else if (role == ROLE_COST) {
-    int seen_chain = 0;
-    for (int sc = 0; sc < H; ++sc) {
-      wait_ge(f_chain, sc + 1, seen_chain);
-      lds_store_release(f_cost, sc + 1);
-    }
-  }
-#endif
   else if (role == ROLE_PROD) {
     // ---------------- sampling + wheel filter + sin/cos, normals prefetched two steps ahead
     // (even / odd steps in their own registers: no loop-carried copy of a load in flight)
@@ -1971,7 +1771,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       eB1 = eps_row[(size_t)t1 * TB];
       eB2 = eps_row[(size_t)(H + t1) * TB];
     }
-    auto prod = [&](auto nt_tag, int p, float& e1r, float& e2r) __attribute__((always_inline)) {
+    auto prod = [&](int p, float& e1r, float& e2r) __attribute__((always_inline)) {
       float u1, u2;
       if constexpr (MODE == 0) {
         const int ti = min(p + 1, H - 1);
@@ -2012,27 +1812,16 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       lds_store_release(f_prod, p + 1);
       if constexpr (MODE == 0) {  // the normals of step p + 2 into the registers just freed
         const int tn = min(p + 2, H - 1);
-        if constexpr (decltype(nt_tag)::value) {  // rows the leaf takes from LDS: streamed past the L2
-          e1r = __builtin_nontemporal_load(eps_row + (size_t)tn * TB);
-          e2r = __builtin_nontemporal_load(eps_row + (size_t)(H + tn) * TB);
-        } else {
-          e1r = eps_row[(size_t)tn * TB];
-          e2r = eps_row[(size_t)(H + tn) * TB];
-        }
+        e1r = eps_row[(size_t)tn * TB];
+        e2r = eps_row[(size_t)(H + tn) * TB];
       }
     };
     int p = 0;
-    if constexpr (MPPI_EPS_NT != 0 && MODE == 0) {
-      for (; p + 3 < a.ucache_steps && p + 1 < H; p += 2) {  // steps p + 2, p + 3 cached for the leaf
-        prod(std::true_type{}, p, eA1, eA2);
-        prod(std::true_type{}, p + 1, eB1, eB2);
-      }
-    }
     for (; p + 1 < H; p += 2) {
-      prod(std::false_type{}, p, eA1, eA2);
-      prod(std::false_type{}, p + 1, eB1, eB2);
+      prod(p, eA1, eA2);
+      prod(p + 1, eB1, eB2);
     }
-    if (p < H) prod(std::false_type{}, p, eA1, eA2);
+    if (p < H) prod(p, eA1, eA2);
   } else if (role == ROLE_WHEEL) {
     // ---------------- wheel contacts of the even steps (the slope critic reads lw / rw at i,
     // i + 2 for even i, critics_warp.py:220-267) and the slope critic.  Contact sets A / B
@@ -2187,11 +1976,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-#if MPPI_COLFIN_FENCED
-      *ticket_lds = (int)__hip_atomic_fetch_add(rec_cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-#else
       *ticket_lds = (int)__hip_atomic_fetch_add(rec_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
     }
     __syncthreads();
     return *ticket_lds;
@@ -2219,9 +2004,6 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_rollout_roles_kernel(const R
 // (MPPI_isaac.py:672-692) and the 3D rollout of the optimal sequence (:696-720):
 // only the serial chain (chain3d) runs on one lane, sin/cos, heights and wheel
 // contacts are computed by all lanes around it.
-#ifndef MPPI_FIN_PRIO
-#define MPPI_FIN_PRIO 0
-#endif
 constexpr int FIN_THREADS = 1024;
 constexpr int FIN_LDS_NODES = 16;
 constexpr int FIN_GROUP_CHUNK = 64;    // groups per scale-table fill (15 PairScale + 16 m each)
@@ -2234,8 +2016,7 @@ __device__ __forceinline__ double group8_apply(const PairScale* ps, const double
 }
 
 // Robot pose with the heading projected on the DEM (projection_warp.py:306-310).
-template <bool LDS>
-__device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>& dem, const float* qpre = nullptr) {
+__device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem& dem, const float* qpre = nullptr) {
   const float res_half_neg = (-f.res) / 2.0f;
   const float res_sq = f.res * f.res;
   Traj s;
@@ -2272,7 +2053,7 @@ __device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem<LDS>
 // while those two steps run, and is read from the lane holding it (v_readlane); a position more
 // than 3 cells from that centre loads its entry directly.  Arithmetic as the rollout chain
 // (advance_step / orient_step, correctly rounded, IEEE redo out of range), so every value is
-// chain3d_lean's.  Writes x, y (0, 1), n (6..8) and the new heading (9..11) of each step into
+// the rollout chain's.  Writes x, y (0, 1), n (6..8) and the new heading (9..11) of each step into
 // chain[12 t ..] (lane 0).
 constexpr int TAIL_WIN = 8, TAIL_WIN_LO = 3;  // neighbourhood cells [c - 3, c + 4] per axis
 // Every lane computes the same values, so the cell of a position is taken wave-uniform (readfirstlane):
@@ -2281,7 +2062,7 @@ constexpr int TAIL_WIN = 8, TAIL_WIN_LO = 3;  // neighbourhood cells [c - 3, c +
 // then advance_step<true, false> of the next position, both redone with IEEE operators if the guards
 // fail).  Each step's v / sin / cos are read one step ahead.  Every lane stores the step's record
 // (same values, same LDS words).
-__device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem<false>& dem, const float* vb,
+__device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& dem, const float* vb,
                                               const float* snb, const float* csb, float* chain, int H, int lane,
                                               const float* qpre) {
   const f2 cell_off = f2{-f.x_min, f.y_min};
@@ -2401,8 +2182,7 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem<fal
 
 // Step 0 of the optimal rollout on one lane (no barrier): traj | hv | lw | rw of the
 // first step into out[0..12), the layout optimal_rollout uses for nsteps = 1.
-template <bool LDS>
-__device__ __forceinline__ void first_step(const FinishArgs& f, const Dem<LDS>& dem, float v, float sn, float cs,
+__device__ __forceinline__ void first_step(const FinishArgs& f, const Dem& dem, float v, float sn, float cs,
                                            float* out, const float* qpre) {
   const float res_half_neg = (-f.res) / 2.0f;
   const float res_sq = f.res * f.res;
@@ -2410,14 +2190,14 @@ __device__ __forceinline__ void first_step(const FinishArgs& f, const Dem<LDS>& 
   const Traj saved = s;
   float q[4], nx, ny, nz;
   bool bad = false;
-  chain3d<kChainFast, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+  chain3d<kChainFast>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
   if (kChainFast && __builtin_expect(bad, 0)) {
     s = saved;
-    chain3d<false, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
+    chain3d<false>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
   }
   StepOut o;
   bool bad2 = false;
-  wheels3d<false, LDS>(dem, f.off, s.x, s.y, q, nx, ny, nz, s.hx, s.hy, s.hz, o, bad2);
+  wheels3d<false>(dem, f.off, s.x, s.y, q, nx, ny, nz, s.hx, s.hy, s.hz, o, bad2);
   out[0] = s.x; out[1] = s.y; out[2] = o.z;
   out[3] = s.hx; out[4] = s.hy; out[5] = s.hz;
   out[6] = o.lx; out[7] = o.ly; out[8] = o.lz;
@@ -2425,58 +2205,27 @@ __device__ __forceinline__ void first_step(const FinishArgs& f, const Dem<LDS>& 
 }
 
 // The 3D rollout of the optimal sequence for `nsteps` steps from the robot pose
-// (projection_warp.py:306-348 on one trajectory): the serial chain on lane 0
-// (12 floats per step into LDS `chain`), then heights and wheel contacts on all
-// lanes.  Writes traj[3n] | hv[3n] | lw[3n] | rw[3n] at `out`.
-template <bool LDS>
-__device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem<LDS>& dem, const float* vb,
+// (projection_warp.py:306-348 on one trajectory): the serial chain on wave 0 (12 floats per step
+// into LDS `chain`), then heights and wheel contacts on all lanes.  Writes traj[3n] | hv[3n] |
+// lw[3n] | rw[3n] at `out`.
+__device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem& dem, const float* vb,
                                                 const float* snb, const float* csb, float* chain,
                                                 int nsteps, float* out, int tid, int nthreads,
                                                 const float* qpre = nullptr) {
-  const float res_half_neg = (-f.res) / 2.0f;
-  const float res_sq = f.res * f.res;
-  if constexpr (!LDS && MPPI_LEAN_CHAIN) {  // the serial chain on wave 0 (tail_chain_3d)
-    if (tid < 64) tail_chain_3d(f, dem, vb, snb, csb, chain, nsteps, tid, qpre);
-  } else if (tid == 0) {  // the serial chain (projection_warp.py:306-326)
-    Traj s = initial_pose(f, dem);
-    float vn = vb[0], sn_n = snb[0], cs_n = csb[0];
-    for (int t = 0; t < nsteps; ++t) {
-      const float v = vn, sn = sn_n, cs = cs_n;
-      const int tn = min(t + 1, nsteps - 1);  // prefetch the next step's inputs from LDS
-      vn = vb[tn];
-      sn_n = snb[tn];
-      cs_n = csb[tn];
-      const Traj saved = s;
-      float q[4], nx, ny, nz;
-      bool bad = false;
-      if constexpr (!LDS && MPPI_LEAN_CHAIN)  // the rollout chain's arithmetic (bitwise equal)
-        chain3d_lean<true>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-      else
-        chain3d<kChainFast, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-      if (kChainFast && __builtin_expect(bad, 0)) {
-        s = saved;
-        chain3d<false, LDS>(dem, res_half_neg, res_sq, f.dt, v, sn, cs, s, q, nx, ny, nz, bad);
-      }
-      float* ch = chain + 12 * t;
-      ch[0] = s.x; ch[1] = s.y;
-      ch[2] = q[0]; ch[3] = q[1]; ch[4] = q[2]; ch[5] = q[3];
-      ch[6] = nx; ch[7] = ny; ch[8] = nz;
-      ch[9] = s.hx; ch[10] = s.hy; ch[11] = s.hz;
-    }
-  }
+  if (tid < 64) tail_chain_3d(f, dem, vb, snb, csb, chain, nsteps, tid, qpre);  // the serial chain, wave 0
   __syncthreads();
   for (int t = tid; t < nsteps; t += nthreads) {  // heights + wheel contacts, all lanes
     const float* ch = chain + 12 * t;
     float q[4] = {ch[2], ch[3], ch[4], ch[5]};
-    if constexpr (!LDS && MPPI_LEAN_CHAIN) {  // the chain read the normal table: corners here
+    {  // the chain read the normal table: corners here
       bool unused = false;
       dem.template corners<false>(ch[0], ch[1], q, unused);
     }
     StepOut o;
     bool bad = false;
-    wheels3d<kFastMath, LDS>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
+    wheels3d<kFastMath>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
     if (kFastMath && bad)
-      wheels3d<false, LDS>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
+      wheels3d<false>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
     float* o_traj = out + 3 * t;
     float* o_hv = out + 3 * nsteps + 3 * t;
     float* o_lw = out + 6 * nsteps + 3 * t;
@@ -2507,9 +2256,7 @@ __device__ __forceinline__ void signal_done(const FinishArgs& f) {
 // (V/S of the root record); the optimal-sequence filter, the outputs, and the
 // optimal rollout (whole, or step 0 with the rest deferred, f.mode 2), then the
 // completion word.  Called by all `nthreads` threads of one workgroup; smem holds
-// uo[2][PS] v[H] w[H] sn[H] cs[H] chain[12H] out[16H] lr[2][PS] floats (fin_phase2_floats, then
-// the DEM window for LDS).
-template <bool LDS>
+// uo[2][PS] v[H] w[H] sn[H] cs[H] chain[12H] out[16H] lr[2][PS] floats (fin_phase2_floats).
 // qpre: the DEM corners of the robot's cell, loaded at the start of the finish by waves 0 and
 // nthreads / 64 - 1 (the waves that use them here), or nullptr.
 __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, unsigned char* smem, int tid,
@@ -2536,21 +2283,12 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
     // inputs (u*k)*(1-a) in parallel, only the recurrences L = L*a + in on two lanes
     uo[tid < H ? tid : PS + (tid - H)] = (ures * f.ok) * one_m_a;
   }
-  float* win = reinterpret_cast<float*>(smem + f.win_offset);
-  if constexpr (LDS) {
-    const int lane = tid & 63, wave = tid >> 6;
-    for (int r = wave; r < f.Wr; r += nthreads / 64) {
-      const float* src = f.Z + (size_t)(f.wy0 + r) * f.grid + f.wx0;
-      float* dst = win + r * f.W;
-      for (int c2 = lane; c2 < f.W; c2 += 64) dst[c2] = src[c2];
-    }
-  }
   __syncthreads();
 #ifdef MPPI_STAMPS
   FIN_STAMP(2);
 #endif
-  Dem<LDS> dem;
-  dem.init(f.Z, win, f.rows, f.grid, f.wx0, f.wy0, f.W, f.Wr, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
+  Dem dem;
+  dem.init(f.Z, f.rows, f.grid, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
   dem.N = f.ntab;
   const int lane = tid & 63, wave = tid >> 6;
   if (wave == 0) {
@@ -2626,7 +2364,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
       const float w0 = clampf(((-L0) + R0) / f.rwheel, f.wmin, f.wmax);
       float sn0, cs0;
       dm_sincosf(w0 * f.dt, &sn0, &cs0);
-      first_step<LDS>(f, dem, v0, sn0, cs0, ostage + 4 * H, qpre);
+      first_step(f, dem, v0, sn0, cs0, ostage + 4 * H, qpre);
     }
   }
   __syncthreads();
@@ -2654,7 +2392,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
 #endif
   // mode 1: the whole optimal rollout; mode 2: its first step only (the pose the
   // closed loop needs now), the rest runs in mppi_tail_kernel on a side stream
-  if (f.mode != 2) optimal_rollout<LDS>(f, dem, vb, snb, csb, chain, H, ostage + 4 * H, tid, nthreads, qpre);
+  if (f.mode != 2) optimal_rollout(f, dem, vb, snb, csb, chain, H, ostage + 4 * H, tid, nthreads, qpre);
   __syncthreads();
   for (int i = tid; i < nout; i += nthreads) store_out(f.out + i, ostage[i]);
 #ifdef MPPI_STAMPS
@@ -2666,12 +2404,8 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
 #endif
 }
 
-template <bool LDS>
 __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishArgs f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-#if MPPI_FIN_PRIO
-  __builtin_amdgcn_s_setprio(3);
-#endif
   const int tid = threadIdx.x;
   const int H = f.H;
   const int E = 2 * H + 2;
@@ -2874,7 +2608,7 @@ root_ready:
   // u_opt = V / S (DEFINED; zero when no trajectory has a finite cost)
   const float ures = (tid < 2 * H && S > 0.0) ? (float)(lnode[2 + tid] / S) : 0.0f;
   __syncthreads();  // lnode is dead from here on
-  finish_phase2<LDS>(f, ures, smem_raw, tid, FIN_THREADS);
+  finish_phase2(f, ures, smem_raw, tid, FIN_THREADS);
 }
 
 // ---------------------------------------------------------------------  column-split finish
@@ -2913,9 +2647,6 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
   // (profiles/r04_notes.md).  Not in the resident server (RECS_WT), whose noise runs in its own
   // workgroups after their records (there the priority measured no gain, r02_notes.md).
   if constexpr (!RECS_WT) __builtin_amdgcn_s_setprio(3);
-#if MPPI_FIN_PRIO
-  __builtin_amdgcn_s_setprio(3);
-#endif
 #ifdef MPPI_STAMPS
   if (blk == 0) FIN_STAMP(0);
 #endif
@@ -2930,8 +2661,8 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
   {
     const int w = tid >> 6;
     if (f.mode != 0 && (w == 0 || w == FIN_THREADS / 64 - 1)) {
-      Dem<false> d0;
-      d0.init(f.Z, nullptr, f.rows, f.grid, 0, 0, 1, 1, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
+      Dem d0;
+      d0.init(f.Z, f.rows, f.grid, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
       bool unused = false;
       d0.template corners<false>(f.x0, f.y0, qpre, unused);
     }
@@ -3167,7 +2898,7 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
   FIN_STAMP(6);
   FIN_STAMP(1);
 #endif
-  finish_phase2<false>(f, ures, smem_raw, tid, FIN_THREADS, qpre);
+  finish_phase2(f, ures, smem_raw, tid, FIN_THREADS, qpre);
   return true;
 }
 
@@ -3191,10 +2922,10 @@ __global__ __launch_bounds__(TAIL_THREADS) void mppi_tail_kernel(const FinishArg
   for (int i = tid; i < 3 * H; i += TAIL_THREADS)
     vb[i] = __hip_atomic_load(f.tail_in + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  Dem<false> dem;
-  dem.init(f.Z, nullptr, f.rows, f.grid, 0, 0, 1, 1, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
+  Dem dem;
+  dem.init(f.Z, f.rows, f.grid, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
   dem.N = f.ntab;
-  optimal_rollout<false>(f, dem, vb, snb, csb, chain, H, f.tail_out, tid, TAIL_THREADS);
+  optimal_rollout(f, dem, vb, snb, csb, chain, H, f.tail_out, tid, TAIL_THREADS);
   if (tid == 0 && f.clk) f.clk[kClkServer + 8 * (f.seq & 7) + 5] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -3206,8 +2937,8 @@ __global__ __launch_bounds__(256) void mppi_bilinear_kernel(const float* __restr
                                                             float res, const float* __restrict__ xs,
                                                             const float* __restrict__ ys,
                                                             float* __restrict__ hs, int64_t n) {
-  Dem<false> dem;
-  dem.init(Z, nullptr, rows, grid, 0, 0, 1, 1, x_min, y_min, res);
+  Dem dem;
+  dem.init(Z, rows, grid, x_min, y_min, res);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const float x = xs[i], y = ys[i];
@@ -3719,7 +3450,7 @@ __global__ __launch_bounds__(256) void mppi_selftest_kernel(int what, int64_t n,
       const float want = sqrtf(x);
       const float got = sq<true>(x, flagged);
       if (!flagged && f_bits(want) != f_bits(got)) ++local;
-    } else {  // 2, 3: lean normalisation (a, b, c) / sqrt(a^2 + b^2 + c^2) of chain3d_lean
+    } else {  // 2, 3: lean normalisation (a, b, c) / sqrt(a^2 + b^2 + c^2) (lean_norm / lean_div)
       const U4 r2 = philox4x32_10(U4{(uint32_t)i, (uint32_t)(i >> 32), 0x5e1fu, 0x1ea4u}, (uint32_t)seed,
                                   (uint32_t)(seed >> 32));
       // what 3: c dominant (exponent in [-30, 30)), a and b anywhere in [-50, 50]
@@ -3786,7 +3517,7 @@ hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hip
 }
 
 hipError_t launch_finish(const FinishArgs& f, size_t lds, hipStream_t st, int groups) {
-  hipLaunchKernelGGL(mppi_finish_kernel<false>, dim3(groups), dim3(FIN_THREADS), lds, st, f);
+  hipLaunchKernelGGL(mppi_finish_kernel, dim3(groups), dim3(FIN_THREADS), lds, st, f);
   return hipGetLastError();
 }
 
@@ -3825,7 +3556,7 @@ hipError_t launch_tail(const FinishArgs& f, hipStream_t st) {
 // (j + 1, i + 1) for the cell indices i in [-1, grid - 1], j in [-1, rows - 1] that
 // Dem::cell produces (i = grid and j = rows select the same clamped corners as grid - 1
 // and rows - 1).  IEEE float operations in the reference order, i.e. exactly the normal
-// the rollout chain computed per step before (chain3d<false> / chain3d_lean agree on
+// the rollout chain computed per step before (chain3d<false> / the lean chains agree on
 // it bit for bit), so reading it from the table changes no result.
 __global__ __launch_bounds__(256) void mppi_normal_table_kernel(const float* __restrict__ Z, int rows, int grid,
                                                                 float res, float4* __restrict__ out) {
@@ -3861,9 +3592,9 @@ __global__ __launch_bounds__(256) void mppi_noise_kernel(uint64_t seed, uint64_t
 
 // =====================================================================  resident step server
 // One launch serves a sequence of sampled steps (mppi_capi.cpp "resident step server"): workgroup b
-// is rollout block b of every step.  Per step: wave 0 polls cmd->seq (one lane, system scope, s_sleep
-// between polls) until it reaches `expect` (or cmd->stop, or idle_ticks without a command: every
-// wave exits), reads the command words into LDS, and the workgroup runs the role-split rollout with
+// is rollout block b of every step.  Per step: the head's wave 0 polls cmd->seq (one lane, system
+// scope) until it reaches `expect` (or cmd->stop, or idle_ticks without a command: it relays a stop
+// and every workgroup exits), the others poll its relay; each reads the command words into LDS, and the workgroup runs the role-split rollout with
 // the command's state, normals slot and nominal buffer.  Its record is written through and counted
 // (rec_cnt); the workgroups holding the last fin_groups tickets run the column-split finish, each
 // after rec_cnt reaches nroll (bounded by wait_ticks: a finish without every record publishes
@@ -3912,19 +3643,25 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
       // host launches without resetting the relay.
       const unsigned long long* src = head ? reinterpret_cast<const unsigned long long*>(z.cmd)
                                            : reinterpret_cast<const unsigned long long*>(z.relay);
+      // Only the head leaves on its own (idle limit, or the exit_after test hook); the others leave
+      // on the stop it relays.  So an exit is all-or-nothing: either every workgroup serves a command
+      // or none does, and a command the head never relayed leaves no trace of the step (the host sees
+      // the launch retire without a completion word and relaunches the server with that command).
       unsigned ok = 0;
       if (tid == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         if (head && z.clk) z.clk[kClkServer + 8 * (expect & 7) + 6] = t0;
-        for (;;) {
+        const bool forced = head && z.exit_after != 0 && expect - z.first_seq >= z.exit_after;
+        while (!forced) {
           const unsigned long long w = head ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                             : __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if ((int)((unsigned)w - expect) >= 0) {
             ok = 1;
             break;
           }
-          const bool stop = head ? (w >> 32) != 0 : (unsigned)(w >> 32) == z.first_seq;
-          if (stop || __builtin_amdgcn_s_memrealtime() - t0 >= z.idle_ticks) break;
+          if (head ? ((w >> 32) != 0 || __builtin_amdgcn_s_memrealtime() - t0 >= z.idle_ticks)
+                   : (unsigned)(w >> 32) == z.first_seq)
+            break;
           if (!head) __builtin_amdgcn_s_sleep(8);  // (~0.2 us: 255 pollers of one word stay off the rollout's way)
         }
       }
@@ -4010,9 +3747,6 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
       const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
       const int q0 = (int)(W * (2 * ticket) / S), q1 = (int)(W * (2 * ticket + 2) / S);
       noise_waves(a.seed, nbase, a.k_offset, a.H, q0 + wave, q1, NROLES * TB / 64, z.eps[nslot], tid & 63);
-#if defined(MPPI_DIAG_W0)  // diagnostic builds: workgroup 0's per-wave noise ends (unused block slots)
-      if (blockIdx.x == 0 && (tid & 63) == 0 && z.clk) z.clk[kClkBase + 2 * 4000 + wave] = __builtin_amdgcn_s_memrealtime();
-#endif
     }
     if (blk >= 0) {
       __builtin_amdgcn_s_setprio(0);  // the rollout waves' priorities do not carry into the finish
@@ -4031,9 +3765,6 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
       __syncthreads();
       bool ok = !sh[1];
       if (ok) {
-#if MPPI_COLFIN_FENCED
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
         FinishArgs f = z.f;
         const int mode = __builtin_amdgcn_readfirstlane(c.mode);
         const int slot = __builtin_amdgcn_readfirstlane(c.tail_slot);
@@ -4069,15 +3800,9 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
     }
     // this CU's L1 forgets the step's normals rows before a later step reads rewritten ones
     // (asynchronous: the next poll's wait covers it)
-#if !defined(MPPI_DIAG_NOFENCE)  // (diagnostic builds: without the invalidate, to time it)
     if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
     expect = seq + 1;
     head = ticket == z.nroll - 1;
-#if defined(MPPI_DIAG_W0)
-    if (blockIdx.x == 0 && (tid & 63) == 0 && z.clk) z.clk[kClkBase + 2 * 4000 + 16 + (tid >> 6)] = __builtin_amdgcn_s_memrealtime();
-    if (blockIdx.x == 0 && tid == 0 && z.clk) z.clk[kClkBase + 2 * 4000 + 32] = seq;
-#endif
     __syncthreads();  // every wave is done with this step's LDS and command words
     if (tid == 0 && z.clk) {  // the latest end of a noise share (3) and of any workgroup's step (7)
       const uint64_t now = __builtin_amdgcn_s_memrealtime();

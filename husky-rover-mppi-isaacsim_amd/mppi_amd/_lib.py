@@ -468,11 +468,11 @@ class Engine:
         return t.value, n.value
 
     def launch_info(self):
-        info = (C.c_int64 * 15)()
-        self._c(self.lib.mppi_get_launch_info(self.ctx, info, 15), "mppi_get_launch_info")
+        info = (C.c_int64 * 16)()
+        self._c(self.lib.mppi_get_launch_info(self.ctx, info, 16), "mppi_get_launch_info")
         keys = ("reserved", "block", "blocks", "window_cols", "window_rows", "lds_bytes", "finish_kind",
                 "finish_records", "finish_ncol", "finish_groups", "ucache_steps", "resident",
-                "server_launches", "server_steps", "server_failed_steps")
+                "server_launches", "server_steps", "server_failed_steps", "server_relaunches")
         return dict(zip(keys, [int(v) for v in info]))
 
     def server_time(self):

@@ -278,7 +278,8 @@ int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
  *                        finish: C1-C3) run on the resident step server, one launch that stays
  *                        on the GPU across steps and polls a command block in pinned memory
  *                        (mppi_step_server_kernel): no launch and no kernel boundary on a
- *                        step's path.  It leaves after "resident_idle_us" without a step, and
+ *                        step's path.  It leaves after "resident_idle_us" without a step (a
+ *                        step posted as it leaves is served by a relaunch, launch_info[15]), and
  *                        every call on the context other than mppi_step / mppi_set_state /
  *                        mppi_get_outputs / mppi_get_timing stops it first.  While it is
  *                        resident it holds one workgroup slot and ~154 KB of LDS on every CU:
@@ -294,20 +295,24 @@ int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
  *   "record_tree_finish" 1: the record-tree finish (mppi_finish_kernel) at every record count
  *                        (default 0: the column-split finish wherever its shape fits).
  *   "tail_streams"       the server's deferred optimal rollouts on the tail stream (1) or
- *                        alternating over the tail and the noise stream (2, default). */
+ *                        alternating over the tail and the noise stream (2, default).
+ *   "server_exit_after"  test hook: the next server launch leaves at its poll after serving this
+ *                        many steps, whether or not the next step was posted (0: off, default);
+ *                        that step is served by a relaunch. */
 int mppi_set_option(mppi_ctx* ctx, const char* name, int64_t value);
 int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_t* launches);
 /* HIP-event time of the deferred optimal-rollout kernels (side stream). */
 int mppi_get_tail_timing(mppi_ctx* ctx, double* tail_ms, int64_t* launches);
 
-/* Layout/launch facts for the last step (for tests and the bench), up to 15 values:
+/* Layout/launch facts for the last step (for tests and the bench), up to 16 values:
  * info[0]=0 (reserved), [1]=rollout block threads, [2]=rollout blocks, [3]/[4]=cols/rows of
  * the DEM window the step's lanes can touch, [5]=rollout LDS bytes, [6]=finish kind (1 =
  * column-split mppi_colfin_kernel, 0 = record tree mppi_finish_kernel), [7]=records padded
  * (column-split) or records (tree), [8]=columns per finish workgroup, [9]=finish workgroups,
  * [10]=steps whose sampled controls the rollout keeps in LDS, [11]=1 if the step ran on the
  * resident step server (mppi_step_server_kernel), else 0; [12]/[13]/[14] = server launches /
- * steps served / failed steps so far (mppi_set_option "resident"). */
+ * steps served / failed steps so far (mppi_set_option "resident"); [15] = commands posted to a
+ * server that was leaving on its idle limit and served by a relaunch (included in [12]). */
 int mppi_get_launch_info(mppi_ctx* ctx, int64_t* info, int32_t n);
 
 /* Shader clock of the last sampled 3D rollout, from the chain wave of trajectories 0..63

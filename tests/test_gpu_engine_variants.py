@@ -252,3 +252,64 @@ def test_server_finish_gives_up_then_recovers():
     finally:
         eng.close()
         ref.close()
+
+
+@pytest.mark.parametrize("trace", [False, True], ids=["plain", "host-trace"])
+def test_server_leaving_as_step_is_posted_relaunches(trace):
+    """A server whose head leaves just as a step is posted (the test hook
+    mppi_set_option("server_exit_after", 1): the head leaves at its poll after one step, whether or
+    not the next step was posted) never takes that step: only the head leaves on its own and the
+    others follow its relayed stop, so nothing of the step ran.  The host sees the launch retire
+    without a completion word and relaunches the server with the same command: the step completes,
+    counted in launch_info["server_relaunches"], the server stays the schedule, and every output
+    equals the separate launches.  The same with MPPI_HOST_TRACE (the diagnostic path)."""
+    ref = _run(65536, 24, opts={"resident": 0}, steps=4, async_tail=True, states=True)
+    env = {"MPPI_HOST_TRACE": "1"} if trace else {}
+    eng = _engine(65536, 24, env=env, opts={"server_exit_after": 1}, async_tail=True)
+    outs = []
+    try:
+        for i in range(4):
+            eng.set_state(_state(i))
+            eng.step("3d", i, copy=False)
+            o = eng.outputs()
+            outs.append({k: o[k].copy() for k in ALL})
+        info = eng.launch_info()
+        costs = eng.costs()
+    finally:
+        eng.close()
+    _same((outs, costs), ref, f"relaunch trace={trace}")
+    assert info["resident"] == 1 and info["server_relaunches"] == 1, info
+    assert info["server_launches"] == 2 and info["server_steps"] == 4 and info["server_failed_steps"] == 0, info
+
+
+def test_deferred_tail_then_partial_finish():
+    """A server step leaves its optimal rollout deferred on the host (launched at the next call).  A
+    partial step + finish on the same context right after it must first launch that tail, so the
+    finish does not take the tail's slot while it is still to run (round-4 advisor finding).  Every
+    output, the *_sim rows included, equals a context running the same calls as separate launches."""
+    import torch
+
+    def calls(opts):
+        eng = _engine(65536, 24, opts=opts, async_tail=True)
+        rec = torch.zeros(eng.record_len(), dtype=torch.float64, device="cuda")
+        outs = []
+        try:
+            for i in range(4):
+                eng.set_state(_state(i))
+                if i in (1, 3):  # straight after a server step (no get_outputs between)
+                    eng.step_partial(rec.data_ptr(), "3d", i)
+                    eng.step_finish(rec.data_ptr(), 1, copy=False)
+                    o = eng.outputs()
+                    outs.append({k: o[k].copy() for k in ALL})
+                else:
+                    eng.step("3d", i, copy=False)
+            costs = eng.costs()
+            info = eng.launch_info()
+        finally:
+            eng.close()
+        return (outs, costs), info
+
+    ref, _ = calls({"resident": 0})
+    got, info = calls({})
+    assert info["server_steps"] == 2, info
+    _same(got, ref, "deferred tail then partial + finish")
