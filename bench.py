@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 full-step leg (N=1)")
     ap.add_argument("--no-shard", action="store_true", help="skip the C4 per-GPU shard leg (N=1)")
     ap.add_argument("--no-costmap", action="store_true", help="skip the obstacle-costmap builder leg")
+    ap.add_argument("--no-cadence", action="store_true",
+                    help="skip the production-cadence leg (one step per simulator frame, N=1)")
     ap.add_argument("--no-sync-pass", action="store_true",
                     help="skip the synchronous-mode pass (profiling runs: only the headline schedule's launches)")
     ap.add_argument("--sync", action="store_true",
@@ -471,6 +473,84 @@ def shard_bench(torch, device, proj, steps=200, warmup=20):
     return rec
 
 
+def cadence_bench(torch, device, proj, frames=40):
+    """The drop-in controller at its production caller's cadence (visual_terrain_stack_full_terrain.py:
+    466-541: MPPI_step, then world.step(render=True) on the same GPU, one frame per step).  Per frame:
+    one MPPI step (latency = call -> controls in host memory), then a stand-in for the simulator's
+    frame on a stream of its own: a 1 GiB device copy (HBM-bound) and a bf16 4096^3 GEMM (LDS-tiled
+    library kernel), each timed with events, then the host waits out the rest of the frame gap.  Gaps
+    of 2 ms and 16 ms; schedules: the resident step server with the default idle limit (2 ms), with a
+    200 us idle limit, and separate launches.  `slowdown` = the stand-in kernels' time beside the
+    schedule / alone.  C3 (the headline K) and K=1000 (config.yaml's number_of_trajectories)."""
+    from mppi_amd import _lib
+    dev = torch.device("cuda", device)
+    src = torch.ones(1 << 28, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    A = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
+    B = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
+    sim = torch.cuda.Stream(device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+
+    def world_step():
+        with torch.cuda.stream(sim):
+            ev[0].record(sim)
+            dst.copy_(src)
+            ev[1].record(sim)
+            torch.matmul(A, B)
+            ev[2].record(sim)
+        ev[2].synchronize()
+        return ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+
+    for _ in range(5):
+        world_step()
+    alone = np.median(np.array([world_step() for _ in range(20)]), axis=0)
+    out = {"workload": "MPPI_step (3d, deferred optimal rollout) then a simulator frame stand-in on its own "
+                       "stream (1 GiB copy + bf16 4096^3 GEMM), host waits out the frame gap",
+           "alone_copy_ms": round(float(alone[0]), 4), "alone_gemm_ms": round(float(alone[1]), 4), "rows": []}
+    Z, hw, cm = get_scene("scene_c3")
+    start, goal = CONFIGS["c3"][3], CONFIGS["c3"][4]
+    state = _lib.make_state(start[0], start[1], (1.0, 0.0, 0.0), goal_x=goal[0], goal_y=goal[1])
+    for K in (65536, 1000):
+        for sched, opts in (("server", {"resident": 1}), ("server_idle200", {"resident": 1, "resident_idle_us": 200}),
+                            ("separate", {"resident": 0})):
+            eng = _lib.Engine(_lib.make_params(K, 100), device)
+            for k, v in opts.items():
+                eng.set_option(k, v)
+            eng.set_dem(Z, hw)
+            eng.set_costmap(cm, hw)
+            eng.set_state(state)
+            eng.set_async_tail(True)
+            for i in range(10):
+                eng.step(proj, i, copy=False)
+            step = 10
+            for gap_ms in (2.0, 16.0):
+                lat, wk = [], []
+                i0 = eng.launch_info()
+                for _ in range(frames):
+                    t0 = time.perf_counter()
+                    eng.step(proj, step, copy=False)
+                    t1 = time.perf_counter()
+                    step += 1
+                    lat.append((t1 - t0) * 1e3)
+                    wk.append(world_step())
+                    while (time.perf_counter() - t1) * 1e3 < gap_ms:
+                        time.sleep(0.0002)
+                i1 = eng.launch_info()
+                wk = np.median(np.array(wk), axis=0)
+                lat = np.array(lat)
+                out["rows"].append({
+                    "K": K, "schedule": sched, "gap_ms": gap_ms, "frames": frames,
+                    "latency_ms_p50": round(float(np.median(lat)), 4),
+                    "latency_ms_p90": round(float(np.percentile(lat, 90)), 4),
+                    "copy_ms": round(float(wk[0]), 4), "gemm_ms": round(float(wk[1]), 4),
+                    "copy_slowdown": round(float(wk[0] / alone[0]), 3),
+                    "gemm_slowdown": round(float(wk[1] / alone[1]), 3),
+                    "server_launches": i1["server_launches"] - i0["server_launches"],
+                    "server_relaunches": i1["server_relaunches"] - i0["server_relaunches"]})
+            eng.close()
+    return out
+
+
 def chain_static(path=os.path.join(ROOT, "profiles", "isa", "chain_count.json")):
     """The chain step's static instruction count (profiles/isa/chain_count.py) if it was taken
     from the current kernel sources, else None."""
@@ -719,6 +799,8 @@ def main():
         # either leg alone, profiles/r04_notes.md; the sharded step was unaffected)
         if world == 1 and devices is None and not args.no_shard:
             rec["c4_shard"] = shard_bench(torch, local_rank, args.proj)
+        if world == 1 and devices is None and not args.no_cadence:
+            rec["cadence"] = cadence_bench(torch, local_rank, args.proj)
         if world == 1 and devices is None and not args.no_bilinear:
             rec["bilinear_roofline"] = bilinear_bench(torch, torch.device("cuda", local_rank))
         if world == 1 and devices is None and not args.no_c5 and args.config != "c2":

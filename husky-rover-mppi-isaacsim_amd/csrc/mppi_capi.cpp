@@ -4,6 +4,7 @@
 // goal, window bounds) is float32 in the reference's operation order; this
 // file is compiled with -ffp-contract=off like the kernels.
 #include <dlfcn.h>
+#include <sched.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>  // types only: RCCL is opened with dlopen by mppi_group_create
 
@@ -118,13 +119,10 @@ struct mppi_ctx {
   // (mppi_set_option "record_tree_finish")
   int colfin = 1;
   int num_cus = 256;  // compute units of the device (hipDeviceAttributeMultiprocessorCount)
-  // host-side step timeline (env MPPI_HOST_TRACE=1, printed by mppi_destroy): microseconds summed
-  // over steps of [previous done seen -> entry, entry -> launches enqueued, -> wait entered, wait]
+  // host-side step timeline (env MPPI_HOST_TRACE=1, printed by mppi_destroy): per step the host
+  // times (us) of 6 marks (trace_mark), summed as phases over the steps and kept for the last 8
   bool trace = false;
-  double tr_prev_done = 0, tr_sum[4] = {0, 0, 0, 0}, tr_t0 = 0, tr_t1 = 0;
-  double tr_srv[4] = {0, 0, 0, 0};  // server steps: stop / relaunch, normals wait, tail-slot wait, side launches
-  double tr_log[8][5] = {};  // last 8 steps: call, command written, side launches done, completion seen, return
-  int tr_slot = 0;
+  double tr_m[6] = {}, tr_sum[6] = {}, tr_log[8][6] = {}, tr_prev = 0;
   long tr_n = 0;
   int roles = -1;     // rollout kernel: -1 auto (role split at <= 1 workgroup per CU), 0 pair, 1 roles (MPPI_ROLES)
   // Resident step server (mppi_step_server_kernel): sampled steps of the role-split plan run on one
@@ -137,8 +135,9 @@ struct mppi_ctx {
   unsigned* relay = nullptr;  // device [64]: workgroup 0's relay of the command (ServerArgs::relay)
   bool srv_running = false;
   int srv_proj = 0;
-  double srv_last_us = 0;     // host time of the last command
-  uint64_t srv_idle_us = 2000;
+  double srv_last_us = 0;     // host time the server last became idle (its last step completed, or launch)
+  uint64_t srv_idle_us = 200;  // (bench.py cadence leg: at 2000 a simulator kernel needing LDS waited
+                               // out the idle server every frame)
   int64_t srv_launches = 0, srv_steps = 0, srv_failed = 0;
   int64_t srv_relaunches = 0;  // commands a leaving server did not take, served by a relaunch (wait_done)
   int srv_cmd_noise = -1;     // the normals slot the last command asked the server's noise phase for
@@ -152,8 +151,6 @@ struct mppi_ctx {
   unsigned srv_exit_after = 0;  // test hook mppi_set_option("server_exit_after"): the next launch's head
                                 // leaves after serving this many commands (0: off)
   uint64_t fin_wait_ticks = 200000000ull;  // a finish's record wait bound (2 s at 100 MHz; mppi_set_option)
-  int tail_streams = 2;  // server: deferred tails alternating over the tail and the noise stream, or on the
-                         // tail stream only (mppi_set_option "tail_streams": 2 or 1)
   // the server's tail of the last step, launched once its completion word was seen (at the next
   // step's command, or when its outputs are wanted): no kernel waits on the GPU for its inputs
   bool tail_deferred = false;
@@ -246,6 +243,20 @@ int E_of(const mppi_ctx* c) { return 2 * c->p.num_iterations + 2; }
 
 double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// (Re)allocate device buffer p for `bytes` when its capacity `cap` (bytes) is short.  The old
+// contents are dropped; `st`, which may still read the old buffer, is synchronised first.
+template <class T>
+int grow(T*& p, size_t& cap, size_t bytes, hipStream_t st) {
+  if (bytes <= cap) return MPPI_OK;
+  HIP_TRY(hipStreamSynchronize(st));
+  if (p) HIP_TRY(hipFree(p));
+  p = nullptr;
+  cap = 0;
+  HIP_TRY(hipMalloc(&p, bytes));
+  cap = bytes;
+  return MPPI_OK;
 }
 
 int check_ready(mppi_ctx* c) {
@@ -640,8 +651,12 @@ int wait_done(mppi_ctx* c) {
     }
     __builtin_ia32_pause();
   }
+  if (c->fail_kind == 0) {
+    if (c->srv_cmd_live) c->srv_last_us = now_us();  // (the head polls for the next command from here)
+    c->srv_cmd_live = false;
+    return MPPI_OK;
+  }
   c->srv_cmd_live = false;
-  if (c->fail_kind == 0) return MPPI_OK;
   ++c->srv_failed;
   quiesce(c);
   rearm_counters(c);
@@ -739,12 +754,9 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
   int rc = ensure_nodes(c, pl.blocks);
   if (rc) return rc;
-  const size_t ucount = (size_t)pl.blocks * pl.traj_per_block * 2 * H_of(c);
-  if (mode == 1 && ucount > c->ustore_cap) {  // injected controls: the leaf reads them back from here
-    if (c->ustore) HIP_TRY(hipFree(c->ustore));
-    c->ustore = nullptr;
-    HIP_TRY(hipMalloc(&c->ustore, ucount * sizeof(float)));
-    c->ustore_cap = ucount;
+  if (mode == 1) {  // injected controls: the leaf reads them back from here
+    rc = grow(c->ustore, c->ustore_cap, (size_t)pl.blocks * pl.traj_per_block * 2 * H_of(c) * sizeof(float), c->stream);
+    if (rc) return rc;
   }
   RolloutArgs a;
   fill_rollout(c, pl, st, step, unom, a);
@@ -824,7 +836,7 @@ int prepare_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, int mode, 
 
 // The deferred optimal rollout on a side stream: after the context stream's finish (event), or, for
 // the resident server (its finish has published: f.clk set), at once.  The server's tails alternate
-// over the tail and the noise stream (tail_streams = 2): beside a server workgroup a tail takes about
+// over the tail and the noise stream: beside a server workgroup a tail takes about
 // two step periods (~175 us against ~52 us alone at C3), so on one stream each waited for the one
 // before it and the host for the slot.  More streams than the process's hardware queues
 // (GPU_MAX_HW_QUEUES, 4 by default: torch's, the context's, the tail's and the noise stream's)
@@ -832,7 +844,7 @@ int prepare_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, int mode, 
 // (measured with one stream per slot: every fourth command 66-102 us late).
 int enqueue_tail(mppi_ctx* c, const FinishArgs& f, int par) {
   const bool server = f.clk != nullptr;
-  hipStream_t ts = (server && c->tail_streams == 2 && (par & 1)) ? c->noise_stream : c->tail_stream;
+  hipStream_t ts = (server && (par & 1)) ? c->noise_stream : c->tail_stream;
   if (!server) {
     HIP_TRY(hipEventRecord(c->ev_fin_done, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->tail_stream, c->ev_fin_done, 0));
@@ -891,13 +903,8 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
   // first tree level on ceil(n/16) workgroups (one per aligned group of 16 records)
   const int groups = n > 16 ? (n + 15) / 16 : 1;
   if (groups > 1) {
-    if ((size_t)groups > c->level1_cap) {
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      if (c->level1) HIP_TRY(hipFree(c->level1));
-      c->level1 = nullptr;
-      HIP_TRY(hipMalloc(&c->level1, (size_t)groups * E_of(c) * sizeof(double)));
-      c->level1_cap = (size_t)groups;
-    }
+    rc = grow(c->level1, c->level1_cap, (size_t)groups * E_of(c) * sizeof(double), c->stream);
+    if (rc) return rc;
     f.level1 = c->level1;
     f.level1_cnt = c->level1_cnt;
   }
@@ -981,6 +988,12 @@ void remember(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
 // until the next step, sync_tail (get_outputs and every call that quiesces before reading the DEM)
 // or prepare_finish (any separate-launch finish: it takes the slot after the deferred one).  No launch and no kernel boundary on the step's path: the gap between two steps
 // is the host's round trip (completion word seen -> next command) plus one poll of pinned memory.
+// MPPI_HOST_TRACE marks of a step: 0 entry, 1 normals ready, 2 tail slot free (server), 3 command
+// posted / launches enqueued, 4 side launches done (the previous tail), 5 completion seen + copies
+void trace_mark(mppi_ctx* c, int k) {
+  if (c->trace) c->tr_m[k] = now_us();
+}
+
 bool server_shape(const mppi_ctx* c, const Plan& pl, int mode, int* P, int* ncol, int* groups, size_t* lds) {
   // (every workgroup of the server must be resident at once: one rollout block per CU at most)
   if (!c->resident || mode != 0 || !pl.roles || !c->colfin || c->timing != 0 || pl.blocks < 1 ||
@@ -995,7 +1008,6 @@ bool server_shape(const mppi_ctx* c, const Plan& pl, int mode, int* P, int* ncol
 
 int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int ncol, int groups, size_t lds) {
   if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
-  const double tq = c->trace ? now_us() : 0.0;
   if (c->srv_running && proj != c->srv_proj) quiesce(c);
   // (first step: the buffers are allocated before the server holds pointers to them)
   if (c->srv_running && (c->nodes_cap < (size_t)pl.blocks * E_of(c) || c->eps_cap < (size_t)pl.blocks * 2 * H_of(c) * 256))
@@ -1009,9 +1021,9 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   for (int i = 0; i < kEpsSlots; ++i) have |= c->eps_step[i] == (int64_t)step;
   if (!have) quiesce(c);
   int slot = -1;
-  const double te = c->trace ? now_us() : 0.0;
   rc = eps_for_step(c, pl, step, c->noise_stream, true, &slot);
   if (rc) return rc;
+  trace_mark(c, 1);
   // normals of step + 1 (normally generated by the previous step's noise phase; else now, on the
   // noise stream beside this step) and of step + 2 (by this step's noise phase, in the server)
   const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
@@ -1041,13 +1053,12 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
     }
     c->eps_step[v] = (int64_t)target;
   }
-  const double tt = c->trace ? now_us() : 0.0;
   const int par = ((c->tail_deferred ? c->tail_def_par : c->tail_par) + 1) % kTailSlots;
   if (c->async_tail && c->tail_inflight[par]) {  // the tail of kTailSlots steps ago: long done
     HIP_TRY(hipEventSynchronize(c->ev_tail[par]));
     c->tail_inflight[par] = false;
   }
-  const double tc = c->trace ? now_us() : 0.0;
+  trace_mark(c, 2);
   const unsigned seq = ++c->seq;
   c->wait_seq = seq;
   // the command: every field, then seq (release: the server reads the fields after seeing it)
@@ -1063,9 +1074,10 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   c->srv_cmd_noise = noise_slot;
   d.noise_n_base_lo = (unsigned)((step + 2) * nb);
   d.noise_n_base_hi = (unsigned)(((step + 2) * nb) >> 32);
-  // a server idle for more than half its limit may be leaving: stop it and start a fresh one.  This
-  // is checked after the host's waits above, right before the command is posted; a head that leaves
-  // anyway (a slower host) never relays the command, and wait_done relaunches the server with it
+  // a server idle for more than half its limit (since its last step completed) may be leaving: stop
+  // it and start a fresh one.  This is checked after the host's waits above, right before the command
+  // is posted; a head that leaves anyway (a slower host) never relays the command, and wait_done
+  // relaunches the server with it
   if (c->srv_running && now_us() - c->srv_last_us > 0.5 * (double)c->srv_idle_us) quiesce(c);
   unsigned* cw = reinterpret_cast<unsigned*>(cmd);
   const unsigned* dw = reinterpret_cast<const unsigned*>(&d);
@@ -1083,18 +1095,12 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
     if (rc) return rc;
   }
   c->srv_last_us = now_us();
-  if (c->trace) {
-    c->tr_t1 = c->srv_last_us;
-    c->tr_srv[0] += te - tq + (c->srv_last_us - tc);
-    c->tr_srv[1] += tt - te;
-    c->tr_srv[2] += tc - tt;
-  }
+  trace_mark(c, 3);
   ++c->srv_steps;
   c->fin_kind = 1;
   c->fin_P = P;
   c->fin_ncol = ncol;
   c->fin_groups = groups;
-  const double tl = c->trace ? now_us() : 0.0;
   rc = flush_tail(c);  // the previous step's tail (its outputs were published before this call)
   if (rc) return rc;
   if (c->async_tail) {  // rows 1.. of the optimal rollout: launched once this step has published
@@ -1108,15 +1114,7 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
     c->tail_deferred = true;
     c->tail_def_par = par;
   }
-  if (c->trace) {
-    const double tn = now_us();
-    c->tr_srv[3] += tn - tl;
-    c->tr_slot = (int)(c->srv_steps & 7);
-    double* lg = c->tr_log[c->tr_slot];
-    lg[0] = c->tr_t0;
-    lg[1] = c->srv_last_us;
-    lg[2] = tn;
-  }
+  trace_mark(c, 4);
   return MPPI_OK;
 }
 
@@ -1124,13 +1122,13 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
 int enqueue_step(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
   int rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr);
   if (rc) return rc;
-  if (c->trace) c->tr_t1 = now_us();
+  trace_mark(c, 3);
   return enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 1, nullptr, true);
 }
 
 int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out) {
-  if (c && c->trace) c->tr_t0 = now_us();
   int rc = check_ready(c);
+  trace_mark(c, 0);
   if (rc) return rc;
   const Plan pl = make_plan(c);
   int sP = 0, scol = 0, sgroups = 0;
@@ -1145,7 +1143,7 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   if (rc) return rc;
   c->last_resident = resident;
   remember(c, proj, step, mode, pl);
-  const double t2 = c->trace ? now_us() : 0.0;
+  trace_mark(c, 4);
   rc = copy_outputs(c, out);
   // a freshly launched server that retired without serving its first command (it cannot hold all
   // its workgroups on the device at once): separate launches from now on, this step again (it
@@ -1161,19 +1159,16 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
     if (rc) return rc;
     rc = copy_outputs(c, out);
   }
-  if (!c->trace) return rc;
-  const double t3 = now_us();
-  if (c->tr_prev_done > 0) {
-    c->tr_sum[0] += c->tr_t0 - c->tr_prev_done;
-    c->tr_sum[1] += c->tr_t1 - c->tr_t0;
-    c->tr_sum[2] += t2 - c->tr_t1;
-    c->tr_sum[3] += t3 - t2;
-    ++c->tr_n;
-  }
-  c->tr_prev_done = t3;
-  if (c->last_resident) {
-    c->tr_log[c->tr_slot][3] = t3;  // (copy_outputs returns right after the completion word)
-    c->tr_log[c->tr_slot][4] = now_us();
+  if (c->trace) {  // marks a schedule does not set (separate launches: 1, 2) take the one before
+    c->tr_m[5] = now_us();
+    for (int k = 1; k < 6; ++k) c->tr_m[k] = std::max(c->tr_m[k], c->tr_m[k - 1]);
+    if (c->tr_prev > 0) {
+      c->tr_sum[0] += c->tr_m[0] - c->tr_prev;
+      for (int k = 1; k < 6; ++k) c->tr_sum[k] += c->tr_m[k] - c->tr_m[k - 1];
+      std::memcpy(c->tr_log[c->tr_n++ & 7], c->tr_m, sizeof(c->tr_m));
+    }
+    c->tr_prev = c->tr_m[5];
+    std::memset(c->tr_m, 0, sizeof(c->tr_m));
   }
   return rc;
 }
@@ -1230,20 +1225,9 @@ int costmap_stage(CostmapScratch& sc, const double* obstacles, int32_t n, int32_
   }
   if (!sc.range) HIP_TRY(hipMalloc(&sc.range, (2 + 2 * COSTMAP_MAX_SIZE) * sizeof(int32_t)));
   const size_t nobs = (size_t)std::max<int32_t>(n, 1);
-  if (nobs > sc.obs_cap) {
-    HIP_TRY(hipStreamSynchronize(st));
-    if (sc.obs) HIP_TRY(hipFree(sc.obs));
-    sc.obs = nullptr;
-    HIP_TRY(hipMalloc(&sc.obs, nobs * 3 * sizeof(double)));
-    sc.obs_cap = nobs;
-  }
-  if ((size_t)size > sc.xs_cap) {
-    HIP_TRY(hipStreamSynchronize(st));
-    if (sc.xs) HIP_TRY(hipFree(sc.xs));
-    sc.xs = nullptr;
-    HIP_TRY(hipMalloc(&sc.xs, (size_t)size * sizeof(double)));
-    sc.xs_cap = (size_t)size;
-  }
+  int rc = grow(sc.obs, sc.obs_cap, nobs * 3 * sizeof(double), st);
+  if (!rc) rc = grow(sc.xs, sc.xs_cap, (size_t)size * sizeof(double), st);
+  if (rc) return rc;
   obs.assign(nobs * 3, 0.0);
   for (int32_t k = 0; k < n; ++k) {
     const double xg = obstacles[3 * k], yg = obstacles[3 * k + 1], r = obstacles[3 * k + 2];
@@ -1373,21 +1357,17 @@ void mppi_destroy(mppi_ctx* c) {
   if (!c) return;
   quiesce(c);
   if (c->trace && c->tr_n > 0) {
-    std::fprintf(stderr, "mppi host trace (us/step over %ld steps): caller %.1f  enqueue rollout %.1f  "
-                 "enqueue rest %.1f  wait+copy %.1f\n", c->tr_n, c->tr_sum[0] / c->tr_n, c->tr_sum[1] / c->tr_n,
-                 c->tr_sum[2] / c->tr_n, c->tr_sum[3] / c->tr_n);
-    if (c->srv_steps > 0)
-      std::fprintf(stderr, "mppi host trace, server steps (us/step over %ld): stop+relaunch %.1f  normals wait %.1f  "
-                   "tail slot wait %.1f  noise+tail launches %.1f  (server launches %ld)\n", (long)c->srv_steps,
-                   c->tr_srv[0] / c->srv_steps, c->tr_srv[1] / c->srv_steps, c->tr_srv[2] / c->srv_steps,
-                   c->tr_srv[3] / c->srv_steps, (long)c->srv_launches);
-    if (c->srv_steps > 0) {  // the last 8 steps, us from the first: call, command, launches, completion, return
-      const double o = c->tr_log[(c->tr_slot + 1) & 7][0];
-      for (int r = 0; r < 8; ++r) {
-        const double* lg = c->tr_log[(c->tr_slot + 1 + r) & 7];
-        std::fprintf(stderr, "  host step: call %8.1f  cmd %+6.1f  launches %+6.1f  done seen %+6.1f  return %+6.1f\n",
-                     lg[0] - o, lg[1] - lg[0], lg[2] - lg[0], lg[3] - lg[0], lg[4] - lg[0]);
-      }
+    static const char* ph[6] = {"caller", "normals wait", "tail slot wait", "command / launches", "side launches",
+                                "completion + copies"};
+    std::fprintf(stderr, "mppi host trace (us/step over %ld steps; server launches %ld, relaunches %ld):", c->tr_n,
+                 (long)c->srv_launches, (long)c->srv_relaunches);
+    for (int k = 0; k < 6; ++k) std::fprintf(stderr, "  %s %.1f", ph[k], c->tr_sum[k] / c->tr_n);
+    std::fprintf(stderr, "\n");
+    for (long r = std::max(0L, c->tr_n - 8); r < c->tr_n; ++r) {  // the last 8 steps' marks, from entry
+      const double* lg = c->tr_log[r & 7];
+      std::fprintf(stderr, "  host step %ld:", r);
+      for (int k = 1; k < 6; ++k) std::fprintf(stderr, " %+7.1f", lg[k] - lg[0]);
+      std::fprintf(stderr, "\n");
     }
   }
   hipSetDevice(c->device);
@@ -1478,15 +1458,8 @@ static int check_grid(int32_t rows, int32_t cols, float res) {
 // The DEM's per-cell normal table (read by the rollout chain instead of four corners +
 // a normalisation per step); rebuilt whenever the DEM is set.  Ends synchronised.
 static int build_normal_table(mppi_ctx* c) {
-  const size_t bytes = ((size_t)c->rows + 1) * ((size_t)c->cols + 1) * sizeof(float4);
-  if (bytes > c->ntab_cap) {
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->ntab) HIP_TRY(hipFree(c->ntab));
-    c->ntab = nullptr;
-    c->ntab_cap = 0;
-    HIP_TRY(hipMalloc(&c->ntab, bytes));
-    c->ntab_cap = bytes;
-  }
+  const int rc = grow(c->ntab, c->ntab_cap, ((size_t)c->rows + 1) * ((size_t)c->cols + 1) * sizeof(float4), c->stream);
+  if (rc) return rc;
   HIP_TRY(launch_normal_table(c->Z, c->rows, c->cols, c->res, c->ntab, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return MPPI_OK;
@@ -1564,13 +1537,8 @@ int mppi_set_costmap(mppi_ctx* c, const float* cm, int32_t size, float half_widt
   if (!(resolution > 0.0f)) return fail(MPPI_EINVAL, "costmap resolution must be > 0");
   HIP_TRY(hipSetDevice(c->device));
   const size_t bytes = (size_t)size * size * sizeof(float);
-  if (bytes > c->cm_cap) {
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->cm) HIP_TRY(hipFree(c->cm));
-    c->cm = nullptr;
-    HIP_TRY(hipMalloc(&c->cm, bytes));
-    c->cm_cap = bytes;
-  }
+  const int rc = grow(c->cm, c->cm_cap, bytes, c->stream);
+  if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(c->cm, cm, bytes, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->cm_size = size;
@@ -1719,11 +1687,6 @@ int mppi_set_option(mppi_ctx* c, const char* name, int64_t value) {
   if (n == "resident_idle_us") {  // how long an idle server stays resident
     if (value < 100 || value > 1000000) return fail(MPPI_EINVAL, "resident_idle_us must be in [100, 1e6]");
     c->srv_idle_us = (uint64_t)value;
-    return MPPI_OK;
-  }
-  if (n == "tail_streams") {  // the server's deferred tails on the tail stream, or alternating with the noise stream
-    if (value != 1 && value != 2) return fail(MPPI_EINVAL, "tail_streams must be 1 or 2");
-    c->tail_streams = (int)value;
     return MPPI_OK;
   }
   if (n == "record_tree_finish") {  // 1: the record-tree finish (mppi_finish_kernel) at any record count
@@ -1899,12 +1862,8 @@ int mppi_bin_queries(mppi_ctx* c, const float* x, const float* y, int64_t n, flo
                              "histogram (at most " + std::to_string((kLdsBytes - 1024) / sizeof(int)) +
                              "); use mppi_bilinear_query for this DEM");
   const size_t hist = (size_t)bin_chunks(n, nt) * nt;  // [chunks][tiles] per-chunk histograms
-  if (std::max<size_t>(hist, 1) > c->bin_n_cap) {
-    if (c->bin_tile_of) HIP_TRY(hipFree(c->bin_tile_of));
-    c->bin_tile_of = nullptr;
-    HIP_TRY(hipMalloc(&c->bin_tile_of, std::max<size_t>(hist, 1) * sizeof(int)));
-    c->bin_n_cap = std::max<size_t>(hist, 1);
-  }
+  const int rc = grow(c->bin_tile_of, c->bin_n_cap, std::max<size_t>(hist, 1) * sizeof(int), c->stream);
+  if (rc) return rc;
   if ((size_t)nt > c->bin_t_cap) {
     if (c->bin_counts) HIP_TRY(hipFree(c->bin_counts));
     if (c->bin_cursor) HIP_TRY(hipFree(c->bin_cursor));
@@ -1978,14 +1937,8 @@ int mppi_build_costmap(mppi_ctx* c, const double* obstacles, int32_t n, int32_t 
   if (!(res > 0.0f)) return fail(MPPI_EINVAL, "costmap resolution must be > 0");
   HIP_TRY(hipSetDevice(c->device));
   const size_t bytes = (size_t)size * size * sizeof(float);
-  if (bytes > c->cm_cap) {
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->cm) HIP_TRY(hipFree(c->cm));
-    c->cm = nullptr;
-    c->cm_cap = 0;
-    HIP_TRY(hipMalloc(&c->cm, bytes));
-    c->cm_cap = bytes;
-  }
+  rc = grow(c->cm, c->cm_cap, bytes, c->stream);
+  if (rc) return rc;
   std::vector<double> obs, xs;
   rc = costmap_stage(c->cms, obstacles, n, size, half_width, origin_x, origin_y, r_robot, obs, xs, c->stream);
   if (rc) return rc;
@@ -2033,18 +1986,11 @@ int mppi_costmap_builder_build(mppi_costmap_builder* b, const double* obstacles,
   if (rc) return rc;
   HIP_TRY(hipSetDevice(b->device));
   const size_t bytes = (size_t)size * size * sizeof(float);
-  float* dst = out_device;
-  if (!dst) {
-    if (bytes > b->out_cap) {
-      HIP_TRY(hipStreamSynchronize(b->stream));
-      if (b->out) HIP_TRY(hipFree(b->out));
-      b->out = nullptr;
-      b->out_cap = 0;
-      HIP_TRY(hipMalloc(&b->out, bytes));
-      b->out_cap = bytes;
-    }
-    dst = b->out;
+  if (!out_device) {
+    rc = grow(b->out, b->out_cap, bytes, b->stream);
+    if (rc) return rc;
   }
+  float* dst = out_device ? out_device : b->out;
   std::vector<double> obs, xs;
   rc = costmap_stage(b->sc, obstacles, n, size, half_width, origin_x, origin_y, r_robot, obs, xs, b->stream);
   if (rc) return rc;
@@ -2186,6 +2132,10 @@ struct mppi_group {
   // variable.  One RCCL communicator per member, each driven only by its member's thread (the
   // one-thread-per-device use of ncclCommInitAll communicators: no group call needed).
   bool threaded = false;
+  int spin_us = 0;      // how long a worker spins for the next step before it sleeps (granted_cpus)
+  int cpus = 0;         // CPUs this process is granted
+  bool selftest = false;  // mppi_group_selftest: host-only member steps (no GPU work at all), member
+  int fail_member = -1;   // fail_member's failing
   std::vector<std::thread> workers;
   std::atomic<uint64_t> gen{0};
   std::atomic<int> pending{0};
@@ -2267,14 +2217,46 @@ int group_member_step(mppi_group* g, int i) {
   return group_finish(g, i, i == 0 ? g->cur_out : nullptr);
 }
 
+// mppi_group_selftest's member step: no GPU work, ~20 us of host time; member fail_member fails
+int group_selftest_member(mppi_group* g, int i) {
+  std::this_thread::sleep_for(std::chrono::microseconds(20));
+  return i == g->fail_member ? fail(MPPI_EHIP, "injected failure") : MPPI_OK;
+}
+
+// CPUs this process may run on: its affinity set, bounded by its cgroup's CPU quota (cgroup v2)
+int granted_cpus() {
+  cpu_set_t set;
+  int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : (int)std::thread::hardware_concurrency();
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    long q = 0, per = 0;
+    if (std::fscanf(f, "%ld %ld", &q, &per) == 2 && q > 0 && per > 0) n = std::min<int>(n, std::max<long>(1, q / per));
+    std::fclose(f);
+  }
+  return std::max(n, 1);
+}
+
+void group_worker(mppi_group* g, int i);
+
+// Member threads: they spin (200 us, a control loop calls again within microseconds) only while the
+// caller and every worker can hold a CPU of their own; on fewer granted CPUs they sleep at once.
+void start_workers(mppi_group* g) {
+  g->threaded = g->n > 1;
+  g->rc.assign(g->n, MPPI_OK);
+  g->err.assign(g->n, std::string());
+  g->cpus = granted_cpus();
+  g->spin_us = g->n < g->cpus ? 200 : 0;
+  for (int i = 1; g->threaded && i < g->n; ++i) g->workers.emplace_back(group_worker, g, i);
+}
+
 void group_worker(mppi_group* g, int i) {
-  hipSetDevice(g->dev[i]);
-  uint64_t seen = g->gen.load(std::memory_order_acquire);
+  if (!g->ctx.empty()) hipSetDevice(g->dev[i]);
+  uint64_t seen = 0;  // the generation at start_workers (not a load here: a step posted before this
+                      // thread ran would be taken as already seen, and the caller would wait for it)
   for (;;) {
     const auto t0 = std::chrono::steady_clock::now();
     uint64_t now;
     for (int spin = 0; (now = g->gen.load(std::memory_order_acquire)) == seen && !g->stop.load(); ++spin) {
-      if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) {
+      if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(g->spin_us)) {
         std::unique_lock<std::mutex> lk(g->mu);
         g->sleepers.fetch_add(1);
         g->cv.wait(lk, [&] { return g->gen.load() != seen || g->stop.load(); });
@@ -2285,7 +2267,7 @@ void group_worker(mppi_group* g, int i) {
     }
     if (g->stop.load()) return;
     seen = now;
-    const int rc = group_member_step(g, i);
+    const int rc = g->selftest ? group_selftest_member(g, i) : group_member_step(g, i);
     g->rc[i] = rc;
     if (rc) g->err[i] = g_err;
     g->pending.fetch_sub(1, std::memory_order_acq_rel);
@@ -2308,7 +2290,7 @@ int group_step_threaded(mppi_group* g, int proj, uint64_t step, mppi_outputs* ou
     g->gen.fetch_add(1, std::memory_order_acq_rel);
   }
   if (g->sleepers.load() > 0) g->cv.notify_all();
-  g->rc[0] = group_member_step(g, 0);
+  g->rc[0] = g->selftest ? group_selftest_member(g, 0) : group_member_step(g, 0);
   if (g->rc[0]) g->err[0] = g_err;
   while (g->pending.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
   for (int i = 0; i < g->n; ++i)
@@ -2381,18 +2363,33 @@ int mppi_group_create(const mppi_params* params, int32_t n, const int32_t* devic
     }
     g->use_rccl = true;
   }
-  // member threads (n > 1): every member enqueues its own step
-  g->threaded = n > 1;
-  g->rc.assign(n, MPPI_OK);
-  g->err.assign(n, std::string());
-  if (g->threaded) {
-    try {
-      for (int i = 1; i < n; ++i) g->workers.emplace_back(group_worker, g, i);
-    } catch (const std::exception& ex) {
-      return bail(fail(MPPI_EHIP, std::string("group: worker threads: ") + ex.what()));
-    }
+  try {  // member threads (n > 1): every member enqueues its own step
+    start_workers(g);
+  } catch (const std::exception& ex) {
+    return bail(fail(MPPI_EHIP, std::string("group: worker threads: ") + ex.what()));
   }
   *out = g;
+  return MPPI_OK;
+}
+
+int mppi_group_selftest(int32_t n, int32_t fail_member, int32_t steps, int64_t* info) {
+  if (n < 2 || steps < 1 || !info) return fail(MPPI_EINVAL, "group selftest: n >= 2, steps >= 1, info");
+  auto* g = new mppi_group();
+  g->n = n;
+  g->selftest = true;
+  g->fail_member = fail_member;
+  g->dev.assign(n, 0);
+  start_workers(g);
+  int64_t done = 0, failed = 0, named = 0;
+  for (int k = 0; k < steps; ++k) {
+    const int rc = group_step_threaded(g, 3, (uint64_t)k, nullptr);
+    ++done;
+    failed += rc != MPPI_OK;
+    named += rc != MPPI_OK && g_err.find("member " + std::to_string(fail_member) + ": injected") != std::string::npos;
+  }
+  const int64_t v[5] = {done, failed, named, (int64_t)g->workers.size(), g->spin_us};
+  for (int i = 0; i < 5; ++i) info[i] = v[i];
+  mppi_group_destroy(g);
   return MPPI_OK;
 }
 
@@ -2447,8 +2444,8 @@ int mppi_group_info(mppi_group* g, int64_t* info, int32_t n) {
   std::vector<int> devs(g->dev);
   std::sort(devs.begin(), devs.end());
   const int64_t distinct = std::unique(devs.begin(), devs.end()) - devs.begin();
-  const int64_t v[5] = {g->n, distinct, g->use_rccl ? 1 : 0, ranks, g->threaded ? 1 : 0};
-  for (int i = 0; i < n && i < 5; ++i) info[i] = v[i];
+  const int64_t v[7] = {g->n, distinct, g->use_rccl ? 1 : 0, ranks, g->threaded ? 1 : 0, g->spin_us, g->cpus};
+  for (int i = 0; i < n && i < 7; ++i) info[i] = v[i];
   return MPPI_OK;
 }
 

@@ -117,6 +117,7 @@ _PROTOS = {
     "mppi_group_shard": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "mppi_group_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.POINTER(MppiOutputs)]),
     "mppi_group_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]),
+    "mppi_group_selftest": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int64)]),
     "mppi_rollout_python25d": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, _DP, _DP, _DP, _DP, _DP, C.c_double,
                                          C.c_double, C.c_double, C.c_double, _DP, C.POINTER(C.c_int32)]),
 }
@@ -559,10 +560,12 @@ class Group:
         return len(self.members)
 
     def info(self):
-        """mppi_group_info: members, distinct devices, RCCL in use, RCCL ranks, member threads."""
-        v = (C.c_int64 * 5)()
-        _check(self.lib, self.lib.mppi_group_info(self.h, v, 5), "mppi_group_info")
-        return dict(zip(("members", "devices", "rccl", "rccl_ranks", "threaded"), [int(x) for x in v]))
+        """mppi_group_info: members, distinct devices, RCCL in use, RCCL ranks, member threads, their spin
+        (us) and the granted CPUs."""
+        v = (C.c_int64 * 7)()
+        _check(self.lib, self.lib.mppi_group_info(self.h, v, 7), "mppi_group_info")
+        return dict(zip(("members", "devices", "rccl", "rccl_ranks", "threaded", "spin_us", "granted_cpus"),
+                        [int(x) for x in v]))
 
     def _each(self, name, *a, **kw):
         for m in self.members:

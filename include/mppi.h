@@ -248,10 +248,18 @@ int mppi_group_size(mppi_group* group);
 int mppi_group_context(mppi_group* group, int32_t member, mppi_ctx** out);
 int mppi_group_shard(mppi_group* group, int32_t member, int64_t* begin, int64_t* count);
 int mppi_group_step(mppi_group* group, int32_t proj, uint64_t step, mppi_outputs* out);
-/* Group facts, up to 5 values: info[0] = members, [1] = distinct devices, [2] = 1 if the records
+/* Group facts, up to 7 values: info[0] = members, [1] = distinct devices, [2] = 1 if the records
  * travel by RCCL (else device copies), [3] = ranks of the RCCL communicator (ncclCommCount; 0
- * without RCCL), [4] = 1 if members 1..n-1 run on group threads. */
+ * without RCCL), [4] = 1 if members 1..n-1 run on group threads, [5] = microseconds a member
+ * thread spins for the next step before it sleeps (0 when the members outnumber the granted
+ * CPUs), [6] = CPUs this process is granted (affinity, bounded by the cgroup quota). */
 int mppi_group_info(mppi_group* group, int64_t* info, int32_t n);
+/* Host-only test of the group's member threads (no device work, no GPU needed): n members whose
+ * steps take ~20 us of host time, member fail_member's fail (fail_member >= n: none), `steps` group
+ * steps.  Every step must return (no member thread left waiting), with the failing member named in
+ * mppi_last_error.  info[5]: steps returned, steps failed, failures naming the member, worker
+ * threads, spin microseconds. */
+int mppi_group_selftest(int32_t n, int32_t fail_member, int32_t steps, int64_t* info);
 
 /* ---- introspection (self.costs_wp / self.trajectories .numpy(), MPPI_isaac.py:466-470) ---- */
 /* costs of the last step's trajectories of this context [n <= K] */
@@ -285,7 +293,9 @@ int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
  *                        resident it holds one workgroup slot and ~154 KB of LDS on every CU:
  *                        other kernels on the device get the rest of each CU.  Results are
  *                        bitwise those of the separate launches (0).
- *   "resident_idle_us"   the server's idle limit, microseconds (default 2000, [100, 1e6]).
+ *   "resident_idle_us"   the server's idle limit, microseconds (default 200, [100, 1e6]): back-
+ *                        to-back steps keep it resident; at a simulator's frame cadence it leaves
+ *                        soon after each step and relaunches on the next.
  *   "finish_wait_ticks"  bound, in ticks of the 100 MHz s_memrealtime clock, on how long a
  *                        finish workgroup of the server waits for the step's rollout records
  *                        (default 2e8 = 2 s).  A finish that gives up publishes the failure:
@@ -294,8 +304,6 @@ int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
  *                        hook).
  *   "record_tree_finish" 1: the record-tree finish (mppi_finish_kernel) at every record count
  *                        (default 0: the column-split finish wherever its shape fits).
- *   "tail_streams"       the server's deferred optimal rollouts on the tail stream (1) or
- *                        alternating over the tail and the noise stream (2, default).
  *   "server_exit_after"  test hook: the next server launch leaves at its poll after serving this
  *                        many steps, whether or not the next step was posted (0: off, default);
  *                        that step is served by a relaunch. */

@@ -11,12 +11,8 @@ from mppi_amd import _lib, scene  # noqa: E402
 
 Z, hw, cm = scene.scene_c3()
 H = int(sys.argv[1]) if len(sys.argv) > 1 else 100
-for async_tail, ts in ((True, 1), (True, 2), (False, 1)):
+for async_tail in (True, False):
     eng = _lib.Engine(_lib.make_params(65536, H), 0)
-    if os.environ.get("MPPI_RESIDENT", "1") != "0":
-        eng.set_option("tail_streams", ts)
-    elif ts == 2:
-        continue
     eng.set_dem(Z, hw)
     eng.set_costmap(cm, hw)
     eng.set_state(_lib.make_state(-60.0, -5.0, (1.0, 0.0, 0.0), goal_x=65.0, goal_y=10.0))
@@ -59,13 +55,6 @@ for async_tail, ts in ((True, 1), (True, 2), (False, 1)):
             cmd, tick - cmd, done - tick, (nz - done) if nz else float("nan"), (nxt - done) if nxt else float("nan"),
             (pol - done) if pol else float("nan"), (w0n - done) if w0n else float("nan"),
             (tg - done) if tg else float("nan"), (te - tg) if te else float("nan")))
-    w = [v[330 + k] for k in range(33)]
-    if any(w[:32]):
-        seqw = int(w[32])
-        r_last = [r for r in range(8) if st[r, 2]][-1]
-        d = st[r_last, 2]
-        print("  wg0 per-wave (us from the last ring step's done): noise ends " + " ".join("%+.1f" % (x - d) for x in w[:16]))
-        print("                                                    end arrivals " + " ".join("%+.1f" % (x - d) for x in w[16:32]))
     eng.close()
-    print(f"async_tail={async_tail} tail_streams={ts}: " + "  ".join(f"[{i} step {a:.0f} out {b:.0f} L{l}]" for i, a, b, l in rows))
+    print(f"async_tail={async_tail}: " + "  ".join(f"[{i} step {a:.0f} out {b:.0f} L{l}]" for i, a, b, l in rows))
     print(f"  {n} back-to-back steps: {dt:.1f} us/step, launches {info['server_launches']}, steps {info['server_steps']}")

@@ -13,7 +13,12 @@ Tolerances (north_star: "<= 1e-5 relative on the emitted control vector"):
   ordering (``rel_err``: |a-b| / max(|ref|, 1e-3) per element);
 * at raised temperatures (many trajectories share the weight, the regime where summation
   order matters): the engine's u_opt is the exact weighted mean of the reference's own float32
-  weights to < 1e-7, and max|a-b| / max(|ref|, 1e-3) <= 1e-5 against every ordering at C1/C2.
+  weights to < 1e-7, and max|a-b| / max(|ref|, 1e-3) <= 1e-5 against every ordering at C1/C2
+  (whole-vector metric).  Per element the reference's orderings themselves spread up to 5e-5
+  (an element much smaller than the vector's largest), so the per-element bound is stated against
+  their envelope: each element of the engine lies within ENVELOPE_TOL = 2e-5 (relative, same
+  scale) of [min, max] over the 9 orderings (measured worst 1.2e-5, C2 at T = 300; <= 2e-6 in
+  the other cases).  Every tolerance and metric is the TOLS table below.
   At C3 with T = 1e5 (~15 500 effective samples) the reference's float32 recursive sums drift
   2e-5 from the exact mean: that is the reference's own rounding, measured in
   tests/test_gpu_headline.py and DESIGN.md §5.
@@ -26,7 +31,11 @@ from oracle import dmath
 from oracle import mppi_ref as R
 
 F32 = np.float32
-TOL = 1e-5
+TOLS = {"T=0.3, per element vs every ordering": 1e-5,
+        "raised T, whole vector vs every ordering": 1e-5,
+        "raised T, per element outside the orderings' envelope": 2e-5}
+TOL = TOLS["T=0.3, per element vs every ordering"]
+ENVELOPE_TOL = TOLS["raised T, per element outside the orderings' envelope"]
 KEYS = (("u1_opt", "u1_opt"), ("u2_opt", "u2_opt"), ("lin_vel", "v_opt"), ("ang_vel", "w_opt"))
 
 
@@ -101,4 +110,15 @@ def test_emitted_controls_vs_reference_f32_raised_temperature(K, H, T):
     outs = R.reference_emitted_f32(p, st, part["cost"], part["u1"], part["u2"])
     for o in outs:
         for _, b in KEYS:
-            assert glob_err(ref[b], o[b]) <= TOL, (b, glob_err(ref[b], o[b]))
+            assert glob_err(ref[b], o[b]) <= TOLS["raised T, whole vector vs every ordering"], (b, glob_err(ref[b], o[b]))
+    for _, b in KEYS:  # per element: inside the envelope of the reference's own orderings
+        assert outside_envelope(ref[b], [o[b] for o in outs]) <= ENVELOPE_TOL, (b, T)
+
+
+def outside_envelope(e, outs, floor=1e-3):
+    """Per element, how far e lies outside [min, max] over the orderings, relative to
+    max(max |ordering|, floor) of that element."""
+    O = np.stack([np.asarray(o, np.float64) for o in outs])
+    e = np.asarray(e, np.float64)
+    out = np.maximum(np.maximum(O.min(0) - e, e - O.max(0)), 0.0)
+    return float((out / np.maximum(np.abs(O).max(0), floor)).max())
