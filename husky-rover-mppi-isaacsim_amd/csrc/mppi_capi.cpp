@@ -1911,7 +1911,8 @@ int mppi_sync(mppi_ctx* c) {
 int mppi_selftest(mppi_ctx* c, int32_t what, int64_t n, uint64_t seed, int64_t* mismatches) {
   if (!c || !mismatches) return fail(MPPI_EINVAL, "null argument");
   quiesce(c);
-  if (what < 0 || what > 4 || n < 0) return fail(MPPI_EINVAL, "bad selftest arguments");
+  if (what < 0 || what > 5 || n < 0 || (what == 5 && n > 2 + 0x4C000000LL))  // 5: finite floats only
+    return fail(MPPI_EINVAL, "bad selftest arguments");
   HIP_TRY(hipSetDevice(c->device));
   unsigned long long* d = nullptr;
   HIP_TRY(hipMalloc(&d, sizeof(*d)));

@@ -148,6 +148,15 @@ struct U4 {
   uint32_t x, y, z, w;
 };
 
+// a ^ b ^ c: one v_bitop3_b32 (truth table 0x96) on gfx950, which the compiler does not form itself
+MPPI_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 MPPI_HD U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -155,7 +164,7 @@ MPPI_HD U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    c = U4{xor3(hi1, c.y, k0), lo1, xor3(hi0, c.w, k1), lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
@@ -215,12 +224,9 @@ MPPI_HD mf2 dm_logf2(mf2 x) {
 MPPI_HD void dm_sincosf2_pos(mf2 x, mf2* s_out, mf2* c_out) {
   const mf2 t = x * 1.27323954473516f;
   int j0 = (int)t.x, j1 = (int)t.y;
-  const mf2 y0 = mf2{(float)j0, (float)j1};
-  const mf2 y1 = y0 + 1.0f;
-  const bool o0 = (j0 & 1) != 0, o1 = (j1 & 1) != 0;
-  j0 = (o0 ? j0 + 1 : j0) & 7;
-  j1 = (o1 ? j1 + 1 : j1) & 7;
-  const mf2 y = mf2{o0 ? y1.x : y0.x, o1 ? y1.y : y0.y};
+  j0 += j0 & 1;  // odd j up, and y = (float)j exactly as dm_sincosf's y + 1 (j < 2^24)
+  j1 += j1 & 1;
+  const mf2 y = mf2{(float)j0, (float)j1};
   mf2 r = x - y * 0.78515625f;
   r = r - y * 2.4187564849853515625e-4f;
   r = r - y * 3.77489497744594108e-8f;
@@ -240,14 +246,14 @@ MPPI_HD void dm_sincosf2_pos(mf2 x, mf2* s_out, mf2* c_out) {
   pc = pc * z;
   pc = pc - 0.5f * z;
   pc = pc + 1.0f;
+  // the sign flips as sign-bit xors (IEEE negation): bit 2 of j for sin; for cos (j >> 1 ^ j >> 2) & 1,
+  // which for even j is bit 2 of j + 2
   auto quad = [](int j, float ps_, float pc_, float* so, float* co) {
     const bool swap = (j & 2) != 0;
     const float s0 = swap ? pc_ : ps_;
     const float c0 = swap ? ps_ : pc_;
-    const bool sneg = (j & 4) != 0;
-    const bool cneg = ((j >> 1) ^ (j >> 2)) & 1;
-    *so = sneg ? -s0 : s0;
-    *co = cneg ? -c0 : c0;
+    *so = bits_f(f_bits(s0) ^ (((uint32_t)j << 29) & 0x80000000u));
+    *co = bits_f(f_bits(c0) ^ (((uint32_t)j + 2u) << 29 & 0x80000000u));
   };
   float sa, ca, sb, cb;
   quad(j0, ps.x, pc.x, &sa, &ca);
@@ -256,13 +262,29 @@ MPPI_HD void dm_sincosf2_pos(mf2 x, mf2* s_out, mf2* c_out) {
   *c_out = mf2{ca, cb};
 }
 
+// sqrtf of the Box-Muller radius argument -2 log(u), in {-0, +0} U [2^-24, 34]: on the device
+// v_sqrt_f32 (within 1 ulp) and the neighbour residual test, correctly rounded there without
+// hipcc's denormal scaling and class tests (-0: the down-neighbour is a NaN, whose compare is
+// false, so -0 stays -0 as IEEE sqrt gives it)
+MPPI_HD float sqrt_bm(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const uint32_t si = f_bits(s);
+  const float sdn = bits_f(si - 1u), sup = bits_f(si + 1u);
+  const float out = (__builtin_fmaf(-sdn, s, x) <= 0.0f) ? sdn : s;
+  return (__builtin_fmaf(-sup, s, x) > 0.0f) ? sup : out;
+#else
+  return sqrtf(x);
+#endif
+}
+
 MPPI_HD void noise_block_pk(uint64_t seed, uint64_t n, uint64_t k, float* a1, float* a2, float* b1, float* b2) {
   const U4 r = philox4x32_10(U4{(uint32_t)n, (uint32_t)(n >> 32), (uint32_t)k, (uint32_t)(k >> 32)},
                              (uint32_t)seed, (uint32_t)(seed >> 32));
   const mf2 u = (mf2{(float)(r.x >> 8), (float)(r.z >> 8)} + 1.0f) * 5.9604644775390625e-8f;
   const mf2 v = mf2{(float)(r.y >> 8), (float)(r.w >> 8)} * 5.9604644775390625e-8f;
   const mf2 l = -2.0f * dm_logf2(u);
-  const mf2 rad = mf2{sqrtf(l.x), sqrtf(l.y)};
+  const mf2 rad = mf2{sqrt_bm(l.x), sqrt_bm(l.y)};
   mf2 s, c;
   dm_sincosf2_pos(6.2831853071795864769f * v, &s, &c);
   const mf2 zc = rad * c, zs = rad * s;

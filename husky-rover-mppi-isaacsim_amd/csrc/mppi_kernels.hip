@@ -3428,6 +3428,14 @@ __global__ __launch_bounds__(256) void mppi_selftest_kernel(int what, int64_t n,
     if (local) atomicAdd(bad_count, local);
     return;
   }
+  if (what == 5) {  // the noise radius' sqrt_bm against sqrtf: -0, +0, then every float from 2^-24 on
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      const float x = i < 2 ? (i == 0 ? -0.0f : 0.0f) : bits_f(0x33800000u + (uint32_t)(i - 2));
+      if (f_bits(sqrt_bm(x)) != f_bits(sqrtf(x))) ++local;
+    }
+    if (local) atomicAdd(bad_count, local);
+    return;
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const U4 r = philox4x32_10(U4{(uint32_t)i, (uint32_t)(i >> 32), 0x5e1fu, 0x7e57u}, (uint32_t)seed,
                                (uint32_t)(seed >> 32));

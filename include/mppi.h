@@ -383,7 +383,8 @@ int mppi_rollout_python25d(mppi_ctx* ctx, int64_t n, int32_t H, const double* x0
  * component) against IEEE sqrtf and a/b, on n random operands; what = 4 the
  * chain's quotient (refined reciprocal, one residual correction) against a/b
  * for every significand of a and n / 2^23 divisor significands ((seed + 8191 k)
- * mod 2^23); *mismatches receives the count of in-range results that differ in
+ * mod 2^23); what = 5 the noise radius' square root (sqrt_bm) against sqrtf
+ * for -0, +0 and the n - 2 floats from 2^-24 up (n <= 2 + 0x4C000000); *mismatches receives the count of in-range results that differ in
  * any bit (0 expected). */
 int mppi_selftest(mppi_ctx* ctx, int32_t what, int64_t n, uint64_t seed, int64_t* mismatches);
 

@@ -35,7 +35,7 @@ for st in "$@"; do
         for lib in ${libs//,/ }; do
           if [ "$lib" = "-" ]; then unset MPPI_LIB_PATH; else export MPPI_LIB_PATH=$R/$lib; fi
           timeout -k 10 300 python bench.py --steps $steps $BA > $O/ab_$TAG.json 2>$O/ab_$TAG.err || { tail -5 $O/ab_$TAG.err; exit 1; }
-          python3 -c "import json; d=json.load(open('$O/ab_$TAG.json')); c=d['config']; ch=c['chain']; print('$lib', 'value', d['value'], 'sync', c['sync_steps_per_s'], 'roll', d['roofline']['kernel_avg_ms'], 'leaf', ch['wg0_leaf_us'], 'cyc', ch['cycles_per_step'], 'srv_roll', c.get('server_rollout_us'), 'srv_step', c.get('server_step_us'), 'spread', ch['wg_end_spread_us'])"
+          python3 -c "import json; d=json.load(open('$O/ab_$TAG.json')); c=d['config']; ch=c['chain']; print('$lib', 'value', d['value'], 'sync', c['sync_steps_per_s'], 'roll', d['roofline']['kernel_avg_ms'], 'leaf', ch['wg0_leaf_us'], 'cyc', ch['cycles_per_step'], 'srv_roll', c.get('server_rollout_us'), 'srv_step', c.get('server_step_us'), 'spread', ch['wg_end_spread_us'], 'tail', c.get('tail_kernel_avg_ms'), 'fin', c.get('finish_kernel_avg_ms'))"
         done
       done
       unset MPPI_LIB_PATH ;;
