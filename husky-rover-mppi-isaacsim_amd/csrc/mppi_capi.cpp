@@ -534,8 +534,6 @@ int sync_tail(mppi_ctx* c) {
   return MPPI_OK;
 }
 
-
-
 // Stop the resident server (it finishes the step it runs, sees cmd->stop and exits): every call on
 // the context but mppi_step / set_state / get_outputs / get_timing starts with this.
 void quiesce(mppi_ctx* c) {
@@ -922,7 +920,6 @@ int enqueue_finish(mppi_ctx* c, const Plan& pl, const mppi_state& st, const doub
   return MPPI_OK;
 }
 
-
 void fill_outputs(const float* o, int H, mppi_outputs* out) {
   if (out->u1_opt) std::memcpy(out->u1_opt, o, H * sizeof(float));
   if (out->u2_opt) std::memcpy(out->u2_opt, o + H, H * sizeof(float));
@@ -1172,7 +1169,6 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   }
   return rc;
 }
-
 
 // ---- obstacle costmap builder (mppi_build_costmap / mppi_costmap_builder_*) ----
 
@@ -1911,8 +1907,7 @@ int mppi_sync(mppi_ctx* c) {
 int mppi_selftest(mppi_ctx* c, int32_t what, int64_t n, uint64_t seed, int64_t* mismatches) {
   if (!c || !mismatches) return fail(MPPI_EINVAL, "null argument");
   quiesce(c);
-  if (what < 0 || what > 5 || n < 0 || (what == 5 && n > 2 + 0x4C000000LL))  // 5: finite floats only
-    return fail(MPPI_EINVAL, "bad selftest arguments");
+  if (what < 0 || what > 5 || n < 0 || (what == 5 && n > 2 + 0x4C000000LL)) return fail(MPPI_EINVAL, "bad selftest arguments");
   HIP_TRY(hipSetDevice(c->device));
   unsigned long long* d = nullptr;
   HIP_TRY(hipMalloc(&d, sizeof(*d)));
