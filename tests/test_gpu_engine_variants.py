@@ -262,10 +262,12 @@ def test_server_leaving_as_step_is_posted_relaunches(trace):
     others follow its relayed stop, so nothing of the step ran.  The host sees the launch retire
     without a completion word and relaunches the server with the same command: the step completes,
     counted in launch_info["server_relaunches"], the server stays the schedule, and every output
-    equals the separate launches.  The same with MPPI_HOST_TRACE (the diagnostic path)."""
+    equals the separate launches.  The same with MPPI_HOST_TRACE (the diagnostic path).  The idle
+    limit is raised so that the host's own liveness check (a server idle for half its limit is
+    stopped before posting) cannot pre-empt the relaunch on a slow host step."""
     ref = _run(65536, 24, opts={"resident": 0}, steps=4, async_tail=True, states=True)
     env = {"MPPI_HOST_TRACE": "1"} if trace else {}
-    eng = _engine(65536, 24, env=env, opts={"server_exit_after": 1}, async_tail=True)
+    eng = _engine(65536, 24, env=env, opts={"server_exit_after": 1, "resident_idle_us": 100000}, async_tail=True)
     outs = []
     try:
         for i in range(4):
