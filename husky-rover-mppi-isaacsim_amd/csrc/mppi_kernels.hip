@@ -2056,12 +2056,13 @@ __device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem& dem
 // the rollout chain's.  Writes x, y (0, 1), n (6..8) and the new heading (9..11) of each step into
 // chain[12 t ..] (lane 0).
 constexpr int TAIL_WIN = 8, TAIL_WIN_LO = 3;  // neighbourhood cells [c - 3, c + 4] per axis
-// Every lane computes the same values, so the cell of a position is taken wave-uniform (readfirstlane):
-// the neighbourhood test, the source lane and the table offset are scalar, the test is a scalar
-// branch (no exec-mask divergence), and the rest of the step is the rollout chain's (orient_step,
-// then advance_step<true, false> of the next position, both redone with IEEE operators if the guards
-// fail).  Each step's v / sin / cos are read one step ahead.  Every lane stores the step's record
-// (same values, same LDS words).
+// Every lane computes the same values, so the lane holding a step's cell is found by comparing each
+// lane's table offset with the cell's (one compare, a ballot, the first set bit): the control flow is
+// uniform (a scalar branch on the ballot), and a lane whose clamped neighbour repeats another's holds
+// the same entry (the offset ti - tjj (grid + 1) is one-to-one on the clamped cells).  The rest of the
+// step is the rollout chain's (orient_step, then advance_step<true, false> of the next position, both
+// redone with IEEE operators if the guards fail).  Each step's v / sin / cos are read one step ahead.
+// Every lane stores the step's record (same values, same LDS words).
 __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& dem, const float* vb,
                                               const float* snb, const float* csb, float* chain, int H, int lane,
                                               const float* qpre) {
@@ -2070,7 +2071,7 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& de
   const float4* ntab0 = dem.N + (f.grid + 2);  // entry (jj, ii) = (1 - tjj, ti + 1): offset ti - tjj * (grid + 1)
   const int nrow = f.grid + 1;
   const int ldx = (lane % TAIL_WIN) - TAIL_WIN_LO, ldy = (lane / TAIL_WIN) - TAIL_WIN_LO;
-  // (ti, tjj) of the cell holding pos: min(i, grid - 1), -min(j, rows - 1) (Dem::cell), wave-uniform
+  // (ti, tjj) of the cell holding pos: min(i, grid - 1), -min(j, rows - 1) (Dem::cell)
   auto cell_of = [&](f2 pos, int& ti, int& tjj) __attribute__((always_inline)) {
     f2 q;
     if (dem.cdiv) {
@@ -2081,8 +2082,8 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& de
     } else {
       q = f2{(pos.x - f.x_min) / f.res, (pos.y + f.y_min) / f.res};
     }
-    ti = __builtin_amdgcn_readfirstlane((int)__builtin_amdgcn_fmed3f(q.x, -1.0f, fi_hi));
-    tjj = __builtin_amdgcn_readfirstlane((int)__builtin_amdgcn_fmed3f(q.y, fj_lo, 1.0f));
+    ti = (int)__builtin_amdgcn_fmed3f(q.x, -1.0f, fi_hi);
+    tjj = (int)__builtin_amdgcn_fmed3f(q.y, fj_lo, 1.0f);
   };
   // this lane's cell of the neighbourhood centred on (ti, tjj): its table offset, load issued
   // (|tjj|, nrow < 2^23 and the table < 4 GiB: 24-bit multiplies, as the rollout chain)
@@ -2092,21 +2093,18 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& de
     lo = ci - __mul24(cj, nrow);
     w = ntab0[lo];
   };
-  // the normal of (ti, tjj) from the neighbourhood centred on (cti, ctjj) (all scalar but the loads)
-  auto pick = [&](int ti, int tjj, int cti, int ctjj, int lo, const float4& w) __attribute__((always_inline)) {
+  // the normal of (ti, tjj): from the lane holding it, else loaded
+  auto pick = [&](int ti, int tjj, int lo, const float4& w) __attribute__((always_inline)) {
     const int to = ti - __mul24(tjj, nrow);
-    const int dx = ti - cti + TAIL_WIN_LO, dy = tjj - ctjj + TAIL_WIN_LO;
-    const int src = (dy * TAIL_WIN + dx) & 63;
+    const uint64_t hit = __builtin_amdgcn_ballot_w64(lo == to);
     float3 n;
-    if (((unsigned)dx < (unsigned)TAIL_WIN) & ((unsigned)dy < (unsigned)TAIL_WIN) &&
-        __builtin_amdgcn_readlane(lo, src) == to) {
+    if (hit) {
+      const int src = __builtin_ctzll(hit);
       n.x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w.x), src));
       n.y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w.y), src));
       n.z = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w.z), src));
-    } else {  // outside the neighbourhood: a vector load of the entry (the offset through a VGPR)
-      int tv = to;
-      asm volatile("v_mov_b32 %0, %1" : "=v"(tv) : "s"(to));
-      const float4 d = ntab0[tv];
+    } else {  // outside the neighbourhood: a load of the entry
+      const float4 d = ntab0[to];
       n = make_float3(d.x, d.y, d.z);
     }
     return n;
@@ -2123,15 +2121,15 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& de
   }
   int ti, tjj;
   cell_of(pos, ti, tjj);
-  int tiA = ti, tjjA = tjj, tiB = ti, tjjB = tjj, loA, loB;  // neighbourhoods of steps 0 and 1: around step 0
+  int loA, loB;  // neighbourhoods of steps 0 and 1: around step 0
   float4 wA, wB;
-  issue(tiA, tjjA, loA, wA);
+  issue(ti, tjj, loA, wA);
   loB = loA;
   wB = wA;
   float vn = H > 1 ? vb[1] : 0.f, snn = snb[0], csn = csb[0];
   // step t (position known, its cell (ti, tjj)): normal from neighbourhood X (centred two steps
   // back), refill X around this cell for step t + 2, orientation, record, next position and cell
-  auto step = [&](auto more_tag, int t, int& ctiX, int& ctjjX, int& loX, float4& wX) __attribute__((always_inline)) {
+  auto step = [&](auto more_tag, int t, int& loX, float4& wX) __attribute__((always_inline)) {
     constexpr bool more = decltype(more_tag)::value;
     const float v1 = vn, sn = snn, cs = csn;
     if constexpr (more) {  // the next step's inputs, one step ahead
@@ -2140,9 +2138,7 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& de
       snn = snb[t + 1];
       csn = csb[t + 1];
     }
-    const float3 n = pick(ti, tjj, ctiX, ctjjX, loX, wX);
-    ctiX = ti;
-    ctjjX = tjj;
+    const float3 n = pick(ti, tjj, loX, wX);
     issue(ti, tjj, loX, wX);
     const float omc = 1.0f - cs;
     const f2 nxy = f2{n.x, n.y};
@@ -2169,14 +2165,14 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& de
   using F_ = std::false_type;
   int t = 0;
   for (; t + 2 < H; t += 2) {
-    step(T_{}, t, tiA, tjjA, loA, wA);
-    step(T_{}, t + 1, tiB, tjjB, loB, wB);
+    step(T_{}, t, loA, wA);
+    step(T_{}, t + 1, loB, wB);
   }
   if (t + 1 < H) {
-    step(T_{}, t, tiA, tjjA, loA, wA);
-    step(F_{}, t + 1, tiB, tjjB, loB, wB);
+    step(T_{}, t, loA, wA);
+    step(F_{}, t + 1, loB, wB);
   } else {
-    step(F_{}, t, tiA, tjjA, loA, wA);
+    step(F_{}, t, loA, wA);
   }
 }
 
@@ -2214,6 +2210,9 @@ __device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem& 
                                                 const float* qpre = nullptr) {
   if (tid < 64) tail_chain_3d(f, dem, vb, snb, csb, chain, nsteps, tid, qpre);  // the serial chain, wave 0
   __syncthreads();
+#ifdef MPPI_STAMPS
+  FIN_STAMP(21);
+#endif
   for (int t = tid; t < nsteps; t += nthreads) {  // heights + wheel contacts, all lanes
     const float* ch = chain + 12 * t;
     float q[4] = {ch[2], ch[3], ch[4], ch[5]};

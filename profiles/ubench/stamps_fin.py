@@ -48,6 +48,8 @@ def main():
     print(f"  u_opt read {us(13, 1):.2f}  phase2 setup {us(1, 2):.2f}  filter {us(2, 12):.2f}  "
           f"v/w/sincos {us(12, 3):.2f}  outputs {us(3, 4):.2f}  signal {us(4, 5):.2f}")
     print(f"  total start -> signal {us(0, 5):.2f}")
+    if fs[21] > fs[3]:
+        print(f"  optimal rollout: chain {us(3, 21):.2f}  heights / wheels + output stores {us(21, 4):.2f}")
     cyc = lambda a, b: fs[32 + b] - fs[32 + a]  # noqa: E731
     print(f"  shader clock over start -> signal {cyc(0, 5) / us(0, 5):.0f} MHz; filter {cyc(2, 12):.0f} cycles "
           f"({cyc(2, 12) / us(2, 12):.0f} MHz), register levels {cyc(11, 15):.0f} cycles")
