@@ -302,11 +302,11 @@ Plan make_plan(const mppi_ctx* c) {
     // floats, 16-byte aligned after the scratch), so the leaf reduction re-reads only the
     // other steps' normals from HBM (all workgroups reduce at once: a bandwidth burst)
     // room is left for the deferred optimal rollout of the previous step (mppi_tail_kernel,
-    // 15H floats), which runs beside a rollout workgroup on one CU
+    // 12H + 4 floats), which runs beside a rollout workgroup on one CU
     const size_t base = (pl.lds_bytes + 15) / 16 * 16;
     const size_t row2 = (size_t)2 * (TB + 4) * sizeof(float);  // UCACHE_ROW: one float4 of bank skew
     // (1 KiB more: the server kernel's static command / ticket words and LDS allocation granularity)
-    const size_t budget = kLdsBytes - ((size_t)15 * H * sizeof(float) + 2047) / 1024 * 1024 - 1024;
+    const size_t budget = kLdsBytes - ((size_t)(12 * H + 4) * sizeof(float) + 2047) / 1024 * 1024 - 1024;
     pl.ucache_steps = base < budget ? (int)std::min<size_t>((size_t)H, (budget - base) / row2) : 0;
     if (pl.ucache_steps > 0) pl.lds_bytes = base + (size_t)pl.ucache_steps * row2;
   }

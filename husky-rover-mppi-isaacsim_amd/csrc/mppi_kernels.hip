@@ -2053,8 +2053,9 @@ __device__ __forceinline__ Traj initial_pose(const FinishArgs& f, const Dem& dem
 // while those two steps run, and is read from the lane holding it (v_readlane); a position more
 // than 3 cells from that centre loads its entry directly.  Arithmetic as the rollout chain
 // (advance_step / orient_step, correctly rounded, IEEE redo out of range), so every value is
-// the rollout chain's.  Writes x, y (0, 1), n (6..8) and the new heading (9..11) of each step into
-// chain[12 t ..] (lane 0).
+// the rollout chain's.  Inputs: in4[t] = (v[t + 1], sin, cos, 1 - cos of step t) (v[H - 1] in the last
+// row) and in4[H].x = v[0], one LDS read per step.  Writes x, y, n, the new heading of each step into
+// chain[8 t ..].
 constexpr int TAIL_WIN = 8, TAIL_WIN_LO = 3;  // neighbourhood cells [c - 3, c + 4] per axis
 // Every lane computes the same values, so the lane holding a step's cell is found by comparing each
 // lane's table offset with the cell's (one compare, a ballot, the first set bit): the control flow is
@@ -2063,9 +2064,8 @@ constexpr int TAIL_WIN = 8, TAIL_WIN_LO = 3;  // neighbourhood cells [c - 3, c +
 // step is the rollout chain's (orient_step, then advance_step<true, false> of the next position, both
 // redone with IEEE operators if the guards fail).  Each step's v / sin / cos are read one step ahead.
 // Every lane stores the step's record (same values, same LDS words).
-__device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& dem, const float* vb,
-                                              const float* snb, const float* csb, float* chain, int H, int lane,
-                                              const float* qpre) {
+__device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& dem, const float4* in4, float* chain,
+                                              int H, int lane, const float* qpre) {
   const f2 cell_off = f2{-f.x_min, f.y_min};
   const float fi_hi = (float)(f.grid - 1), fj_lo = (float)(1 - f.rows);
   const float4* ntab0 = dem.N + (f.grid + 2);  // entry (jj, ii) = (1 - tjj, ti + 1): offset ti - tjj * (grid + 1)
@@ -2115,8 +2115,9 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& de
   {  // step 0's position (guarded: the heading comes from the IEEE initial pose)
     Lean la;
     lean_init(la);
-    f2 p = advance_step<true>(hd, vb[0], f.dt, pos, la);
-    if (__builtin_expect(lean_bad(la), 0)) p = advance_step<false>(hd, vb[0], f.dt, pos, la);
+    const float v0 = in4[H].x;
+    f2 p = advance_step<true>(hd, v0, f.dt, pos, la);
+    if (__builtin_expect(lean_bad(la), 0)) p = advance_step<false>(hd, v0, f.dt, pos, la);
     pos = p;
   }
   int ti, tjj;
@@ -2126,21 +2127,15 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& de
   issue(ti, tjj, loA, wA);
   loB = loA;
   wB = wA;
-  float vn = H > 1 ? vb[1] : 0.f, snn = snb[0], csn = csb[0];
+  float4 inn = in4[0];
   // step t (position known, its cell (ti, tjj)): normal from neighbourhood X (centred two steps
   // back), refill X around this cell for step t + 2, orientation, record, next position and cell
   auto step = [&](auto more_tag, int t, int& loX, float4& wX) __attribute__((always_inline)) {
     constexpr bool more = decltype(more_tag)::value;
-    const float v1 = vn, sn = snn, cs = csn;
-    if constexpr (more) {  // the next step's inputs, one step ahead
-      const int t2 = min(t + 2, H - 1);
-      vn = vb[t2];
-      snn = snb[t + 1];
-      csn = csb[t + 1];
-    }
+    const float v1 = inn.x, sn = inn.y, cs = inn.z, omc = inn.w;
+    if constexpr (more) inn = in4[t + 1];  // the next step's inputs, one step ahead
     const float3 n = pick(ti, tjj, loX, wX);
     issue(ti, tjj, loX, wX);
-    const float omc = 1.0f - cs;
     const f2 nxy = f2{n.x, n.y};
     Lean l;
     lean_init(l);
@@ -2151,10 +2146,10 @@ __device__ __forceinline__ void tail_chain_3d(const FinishArgs& f, const Dem& de
       ho = orient_step<false>(nxy, n.z, hd, sn, cs, omc, l);
       if constexpr (more) p1 = advance_step<false>(ho, v1, f.dt, pos, l);
     }
-    float* ch = chain + 12 * t;
+    float* ch = chain + 8 * t;
     ch[0] = pos.x; ch[1] = pos.y;
-    ch[6] = n.x; ch[7] = n.y; ch[8] = n.z;
-    ch[9] = ho.xy.x; ch[10] = ho.xy.y; ch[11] = ho.z;
+    ch[2] = n.x; ch[3] = n.y; ch[4] = n.z;
+    ch[5] = ho.xy.x; ch[6] = ho.xy.y; ch[7] = ho.z;
     hd = ho;
     if constexpr (more) {
       pos = p1;
@@ -2201,36 +2196,36 @@ __device__ __forceinline__ void first_step(const FinishArgs& f, const Dem& dem, 
 }
 
 // The 3D rollout of the optimal sequence for `nsteps` steps from the robot pose
-// (projection_warp.py:306-348 on one trajectory): the serial chain on wave 0 (12 floats per step
-// into LDS `chain`), then heights and wheel contacts on all lanes.  Writes traj[3n] | hv[3n] |
-// lw[3n] | rw[3n] at `out`.
-__device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem& dem, const float* vb,
-                                                const float* snb, const float* csb, float* chain,
+// (projection_warp.py:306-348 on one trajectory): the serial chain on wave 0 (8 floats per step
+// into LDS `chain`, 16-byte aligned), then heights and wheel contacts on all lanes.  Writes
+// traj[3n] | hv[3n] | lw[3n] | rw[3n] at `out`.
+__device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem& dem, const float4* in4, float* chain,
                                                 int nsteps, float* out, int tid, int nthreads,
                                                 const float* qpre = nullptr) {
-  if (tid < 64) tail_chain_3d(f, dem, vb, snb, csb, chain, nsteps, tid, qpre);  // the serial chain, wave 0
+  if (tid < 64) tail_chain_3d(f, dem, in4, chain, nsteps, tid, qpre);  // the serial chain, wave 0
   __syncthreads();
 #ifdef MPPI_STAMPS
   FIN_STAMP(21);
 #endif
   for (int t = tid; t < nsteps; t += nthreads) {  // heights + wheel contacts, all lanes
-    const float* ch = chain + 12 * t;
-    float q[4] = {ch[2], ch[3], ch[4], ch[5]};
+    const float4 ca = reinterpret_cast<const float4*>(chain)[2 * t], cb = reinterpret_cast<const float4*>(chain)[2 * t + 1];
+    const float ch[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};  // x, y, n, heading
+    float q[4];
     {  // the chain read the normal table: corners here
       bool unused = false;
       dem.template corners<false>(ch[0], ch[1], q, unused);
     }
     StepOut o;
     bool bad = false;
-    wheels3d<kFastMath>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
+    wheels3d<kFastMath>(dem, f.off, ch[0], ch[1], q, ch[2], ch[3], ch[4], ch[5], ch[6], ch[7], o, bad);
     if (kFastMath && bad)
-      wheels3d<false>(dem, f.off, ch[0], ch[1], q, ch[6], ch[7], ch[8], ch[9], ch[10], ch[11], o, bad);
+      wheels3d<false>(dem, f.off, ch[0], ch[1], q, ch[2], ch[3], ch[4], ch[5], ch[6], ch[7], o, bad);
     float* o_traj = out + 3 * t;
     float* o_hv = out + 3 * nsteps + 3 * t;
     float* o_lw = out + 6 * nsteps + 3 * t;
     float* o_rw = out + 9 * nsteps + 3 * t;
     o_traj[0] = ch[0]; o_traj[1] = ch[1]; o_traj[2] = o.z;
-    o_hv[0] = ch[9]; o_hv[1] = ch[10]; o_hv[2] = ch[11];
+    o_hv[0] = ch[5]; o_hv[1] = ch[6]; o_hv[2] = ch[7];
     o_lw[0] = o.lx; o_lw[1] = o.ly; o_lw[2] = o.lz;
     o_rw[0] = o.rx; o_rw[1] = o.ry; o_rw[2] = o.rz;
   }
@@ -2255,7 +2250,7 @@ __device__ __forceinline__ void signal_done(const FinishArgs& f) {
 // (V/S of the root record); the optimal-sequence filter, the outputs, and the
 // optimal rollout (whole, or step 0 with the rest deferred, f.mode 2), then the
 // completion word.  Called by all `nthreads` threads of one workgroup; smem holds
-// uo[2][PS] v[H] w[H] sn[H] cs[H] chain[12H] out[16H] lr[2][PS] floats (fin_phase2_floats).
+// uo[2][PS] in4[4(H + 1)] chain[8H] out[16H] lr[2][PS] floats (<= fin_phase2_floats).
 // qpre: the DEM corners of the robot's cell, loaded at the start of the finish by waves 0 and
 // nthreads / 64 - 1 (the waves that use them here), or nullptr.
 __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, unsigned char* smem, int tid,
@@ -2263,14 +2258,11 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
   const int H = f.H;
   const int PS = fin_plane_stride(H);
   float* uo = reinterpret_cast<float*>(smem);  // [2][PS]: the L inputs, then the R inputs
-  float* vb = uo + 2 * PS;
-  float* wb = vb + H;
-  float* snb = wb + H;
-  float* csb = snb + H;
-  float* chain = csb + H;  // [H][12]: x, y, q00, q01, q10, q11, nx, ny, nz, hx, hy, hz
+  float4* in4 = reinterpret_cast<float4*>(uo + 2 * PS);  // [H + 1]: the optimal rollout's inputs
+  float* chain = reinterpret_cast<float*>(in4 + H + 1);  // [H][8]: x, y, nx, ny, nz, hx, hy, hz
   // outputs are staged here and stored to f.out (pinned host memory) in one burst at the
   // end: a workgroup barrier after host stores would wait for their PCIe round trip
-  float* ostage = chain + 12 * H;  // [16H]
+  float* ostage = chain + 8 * H;  // [16H]
   float* lrp = ostage + 16 * H;    // [2][PS]: the filtered L, then R (16-byte aligned)
   const int nout = f.mode == 2 ? 4 * H + 12 : 16 * H;
   const float one_m_a = 1.0f - f.oa;
@@ -2373,10 +2365,11 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
     const float w = clampf(((-L) + R) / f.rwheel, f.wmin, f.wmax);
     float sn, cs;
     dm_sincosf(w * f.dt, &sn, &cs);
-    vb[t] = v;
-    wb[t] = w;
-    snb[t] = sn;
-    csb[t] = cs;
+    in4[t].y = sn;
+    in4[t].z = cs;
+    in4[t].w = 1.0f - cs;
+    in4[t > 0 ? t - 1 : H].x = v;  // v of step t in the row before (v[0]: row H)
+    if (t == H - 1) in4[t].x = v;
     ostage[2 * H + t] = v;
     ostage[3 * H + t] = w;
     if (f.mode == 2) {  // inputs of the deferred optimal rollout (mppi_tail_kernel), written through
@@ -2391,7 +2384,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
 #endif
   // mode 1: the whole optimal rollout; mode 2: its first step only (the pose the
   // closed loop needs now), the rest runs in mppi_tail_kernel on a side stream
-  if (f.mode != 2) optimal_rollout(f, dem, vb, snb, csb, chain, H, ostage + 4 * H, tid, nthreads, qpre);
+  if (f.mode != 2) optimal_rollout(f, dem, in4, chain, H, ostage + 4 * H, tid, nthreads, qpre);
   __syncthreads();
   for (int i = tid; i < nout; i += nthreads) store_out(f.out + i, ostage[i]);
 #ifdef MPPI_STAMPS
@@ -2912,19 +2905,24 @@ __global__ __launch_bounds__(TAIL_THREADS) void mppi_tail_kernel(const FinishArg
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int tid = threadIdx.x;
   const int H = f.H;
-  float* vb = reinterpret_cast<float*>(smem_raw);
-  float* snb = vb + H;
-  float* csb = snb + H;
-  float* chain = csb + H;
+  float4* in4 = reinterpret_cast<float4*>(smem_raw);  // [H + 1] (finish_phase2's layout)
+  float* chain = reinterpret_cast<float*>(in4 + H + 1);
   if (tid == 0 && f.clk) f.clk[kClkServer + 8 * (f.seq & 7) + 4] = __builtin_amdgcn_s_memrealtime();
   // (agent-scope loads: written through by the finish; an L1 line of an earlier tail could be stale)
-  for (int i = tid; i < 3 * H; i += TAIL_THREADS)
-    vb[i] = __hip_atomic_load(f.tail_in + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  auto ld = [&](int i) { return __hip_atomic_load(f.tail_in + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  for (int t = tid; t <= H; t += TAIL_THREADS) {
+    if (t == H) {
+      in4[H] = make_float4(ld(0), 0.f, 0.f, 0.f);
+    } else {
+      const float cs = ld(2 * H + t);
+      in4[t] = make_float4(ld(min(t + 1, H - 1)), ld(H + t), cs, 1.0f - cs);
+    }
+  }
   __syncthreads();
   Dem dem;
   dem.init(f.Z, f.rows, f.grid, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
   dem.N = f.ntab;
-  optimal_rollout(f, dem, vb, snb, csb, chain, H, f.tail_out, tid, TAIL_THREADS);
+  optimal_rollout(f, dem, in4, chain, H, f.tail_out, tid, TAIL_THREADS);
   if (tid == 0 && f.clk) f.clk[kClkServer + 8 * (f.seq & 7) + 5] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -3553,7 +3551,7 @@ hipError_t launch_colfin(const FinishArgs& f, size_t lds, hipStream_t st, int P,
 }
 
 hipError_t launch_tail(const FinishArgs& f, hipStream_t st) {
-  const size_t lds = (size_t)15 * f.H * sizeof(float);
+  const size_t lds = (size_t)(12 * f.H + 4) * sizeof(float);  // in4[H + 1], chain[8H]
   hipLaunchKernelGGL(mppi_tail_kernel, dim3(1), dim3(TAIL_THREADS), lds, st, f);
   return hipGetLastError();
 }
