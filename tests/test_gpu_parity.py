@@ -125,10 +125,12 @@ def test_collision_costs_and_nonzero_nominal():
     _assert_step(ref, out, eng)
 
 
-def test_map_edge_clamping():
-    # robot at the map corner: cells outside the DEM/costmap are clamped (DEFINED semantics)
+@pytest.mark.parametrize("corner", [1.0, -1.0], ids=["upper", "lower"])
+def test_map_edge_clamping(corner):
+    # robot at a map corner heading out: cells outside the DEM/costmap are clamped (DEFINED
+    # semantics); the optimal rollout's neighbourhood then holds repeated border cells
     Z, hw, cm = hp.c3_scene()
-    st = hp.oracle_state(x=hw - 0.35, y=hw - 0.25, heading=(1.0, 1.0, 0.0))
+    st = hp.oracle_state(x=corner * (hw - 0.35), y=corner * (hw - 0.25), heading=(corner, corner, 0.0))
     ref, out, eng = _run_both(512, 40, 2, st)
     _assert_step(ref, out, eng)
 
