@@ -2647,18 +2647,7 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
   const int E = 2 * H + 2;
   const int n = f.n_recs;
   const double* recs = f.recs;
-  // the robot cell's DEM corners for phase 2's initial pose, loaded now by the two waves that use
-  // them there (only the last workgroup does), so that load is off phase 2's serial path
   float qpre[4] = {0.f, 0.f, 0.f, 0.f};
-  {
-    const int w = tid >> 6;
-    if (f.mode != 0 && (w == 0 || w == FIN_THREADS / 64 - 1)) {
-      Dem d0;
-      d0.init(f.Z, f.rows, f.grid, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
-      bool unused = false;
-      d0.template corners<false>(f.x0, f.y0, qpre, unused);
-    }
-  }
   PairScale* lps = reinterpret_cast<PairScale*>(smem_raw);
   float* mlev = reinterpret_cast<float*>(lps + (P - 1));  // node minima, level l at 2P - (2P >> l)
   double* part = reinterpret_cast<double*>(mlev + 2 * P);  // [ncol + 1][P / 16], 8-byte aligned (P >= 16)
@@ -2709,6 +2698,18 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
     }
   }
   ml = L == 1 ? 0 : (L == 2 ? 1 : 2);
+  // the robot cell's DEM corners for phase 2's initial pose, loaded now by the two waves that use
+  // them there (only the last workgroup does), so that load is off phase 2's serial path; after the
+  // minima (a wave's loads complete in order: wave 0's minima no longer wait behind them)
+  {
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (f.mode != 0 && (w == 0 || w == FIN_THREADS / 64 - 1)) {
+      Dem d0;
+      d0.init(f.Z, f.rows, f.grid, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
+      bool unused = false;
+      d0.template corners<false>(f.x0, f.y0, qpre, unused);
+    }
+  }
   // the items on the LAST waves (a column's groups in consecutive lanes), clear of the waves
   // that load the minima where they fit: a wave's loads complete in order, and behind a branch
   // the compiler waits for all of them (vmcnt(0)) before using the minima
