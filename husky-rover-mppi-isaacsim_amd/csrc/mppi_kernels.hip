@@ -1083,7 +1083,10 @@ __device__ __forceinline__ void lds_wait_ge(const int* f, int target, int& seen,
   const uint64_t t0 = dbg_stamp();
 #endif
   int v;
-  while ((v = lds_load_acquire(f)) < target) __builtin_amdgcn_s_sleep(1);
+  // (the chain waves: no s_sleep between reads, a woken chain lost up to ~64 cycles per wait; C3
+  // +0.7 % at 200 steps, chain waits 131 -> 120 cycles per step)
+  while ((v = lds_load_acquire(f)) < target) {
+  }
   seen = v;
 #ifdef MPPI_STAMPS
   ws.wait += dbg_stamp() - t0;
