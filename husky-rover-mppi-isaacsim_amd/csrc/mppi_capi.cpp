@@ -192,6 +192,7 @@ struct mppi_ctx {
   hipEvent_t ev_tail[kTailSlots] = {};  // per slot: tail done
   bool tail_pending = false;       // the latest tail's outputs are not merged into out_host yet
   bool tail_inflight[kTailSlots] = {};  // the tail of that slot may still run
+  hipStream_t tail_ts[kTailSlots] = {};  // the stream that slot's tail was launched on
   int tail_par = 0;                // slot of the latest tail
   float* tail_in[kTailSlots] = {};    // device [3H] per slot
   float* tail_host[kTailSlots] = {};  // pinned [12H] per slot (written by the kernel)
@@ -522,6 +523,19 @@ int sync_tail(mppi_ctx* c) {
   bool any = c->tail_pending;
   for (int i = 0; i < kTailSlots; ++i) any |= c->tail_inflight[i];
   if (!any) return MPPI_OK;
+  // The tails' streams are drained, not only their events, the latest tail's last: a stream's first
+  // synchronize after a kernel costs ~8-15 us of runtime work even when the kernel is long done
+  // (profiles/ubench/devsync.hip), which the caller's next device synchronize would pay otherwise;
+  // the older tails' stream is drained while the latest tail runs.
+  hipStream_t last = c->tail_pending ? c->tail_ts[c->tail_par] : nullptr;
+  for (int i = 0; i < kTailSlots; ++i)
+    if (c->tail_inflight[i] && c->tail_ts[i] && c->tail_ts[i] != last) {
+      const hipStream_t ts = c->tail_ts[i];
+      HIP_TRY(hipStreamSynchronize(ts));
+      for (int j = 0; j < kTailSlots; ++j)
+        if (c->tail_ts[j] == ts) c->tail_inflight[j] = false;
+    }
+  if (last) HIP_TRY(hipStreamSynchronize(last));
   for (int i = 0; i < kTailSlots; ++i)
     if (c->tail_inflight[i] || (c->tail_pending && i == c->tail_par)) HIP_TRY(hipEventSynchronize(c->ev_tail[i]));
   collect_tail_timing(c);
@@ -857,6 +871,7 @@ int enqueue_tail(mppi_ctx* c, const FinishArgs& f, int par) {
     c->ev_tail_pending = true;
   }
   HIP_TRY(hipEventRecord(c->ev_tail[par], ts));
+  c->tail_ts[par] = ts;
   c->tail_inflight[par] = true;
   c->tail_par = par;
   c->tail_pending = true;
