@@ -391,6 +391,26 @@ class Runner:
             self.eng.close()
 
 
+def group_parity(cfg, devices, proj, steps=3):
+    """The C-ABI group's outputs (member 0) against one context over the whole K, synchronous mode, a
+    few chained steps: bitwise equal when every member holds a power-of-two number of 256-trajectory
+    leaves (the member roots are then subtrees of the one-context record tree)."""
+    g = Runner(cfg, devices[0], 1, devices=devices)
+    one = Runner(cfg, devices[0], 1, solo=True)
+    try:
+        g.set_async_tail(False)
+        one.set_async_tail(False)
+        same = True
+        for i in range(steps):
+            a = g.group.step(proj, 500 + i, copy=True)
+            b = one.eng.step(proj, 500 + i, copy=True)
+            same &= all(np.array_equal(a[k], b[k]) for k in a)
+    finally:
+        g.close()
+        one.close()
+    return bool(same)
+
+
 def timed_run(torch, dist, run, proj, warmup, steps, step0, async_tail, kernel_timing=False):
     """`warmup` untimed + `steps` timed MPPI steps, barrier + synchronize on both sides; returns
     the max-over-ranks wall time of the timed steps.  Kernel timing (if any) on the first
@@ -479,9 +499,13 @@ def cadence_bench(torch, device, proj, frames=40):
     one MPPI step (latency = call -> controls in host memory), then a stand-in for the simulator's
     frame on a stream of its own: a 1 GiB device copy (HBM-bound) and a bf16 4096^3 GEMM (LDS-tiled
     library kernel), each timed with events, then the host waits out the rest of the frame gap.  Gaps
-    of 2 ms and 16 ms; schedules: the resident step server with the default idle limit (2 ms), with a
-    200 us idle limit, and separate launches.  `slowdown` = the stand-in kernels' time beside the
-    schedule / alone.  C3 (the headline K) and K=1000 (config.yaml's number_of_trajectories)."""
+    of 2 ms and 16 ms; schedules ("resident" option): "default" (1: the server for back-to-back calls
+    only, so at a frame cadence every step runs as separate launches), "server_always" (2, idle limit
+    200 us: the server relaunched for every frame, round 5's default), "server_idle2000" (2, idle limit
+    2 ms: round 4's default, whose idle server holds every CU's LDS past the step) and "separate" (0).
+    `slowdown` = the stand-in kernels' time beside the schedule / alone.  C3 (the headline K) and
+    K=1000 (config.yaml's number_of_trajectories).  Rows with "sim_first" launch the frame's stand-in
+    BEFORE the step (the simulator's kernels still in flight when the controller is called)."""
     from mppi_amd import _lib
     dev = torch.device("cuda", device)
     src = torch.ones(1 << 28, dtype=torch.float32, device=dev)
@@ -491,28 +515,37 @@ def cadence_bench(torch, device, proj, frames=40):
     sim = torch.cuda.Stream(device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
 
-    def world_step():
+    def world_launch():
         with torch.cuda.stream(sim):
             ev[0].record(sim)
             dst.copy_(src)
             ev[1].record(sim)
             torch.matmul(A, B)
             ev[2].record(sim)
+
+    def world_wait():
         ev[2].synchronize()
         return ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+
+    def world_step():
+        world_launch()
+        return world_wait()
 
     for _ in range(5):
         world_step()
     alone = np.median(np.array([world_step() for _ in range(20)]), axis=0)
-    out = {"workload": "MPPI_step (3d, deferred optimal rollout) then a simulator frame stand-in on its own "
+    out = {"workload": "MPPI_step (3d, deferred optimal rollout) and a simulator frame stand-in on its own "
                        "stream (1 GiB copy + bf16 4096^3 GEMM), host waits out the frame gap",
            "alone_copy_ms": round(float(alone[0]), 4), "alone_gemm_ms": round(float(alone[1]), 4), "rows": []}
     Z, hw, cm = get_scene("scene_c3")
     start, goal = CONFIGS["c3"][3], CONFIGS["c3"][4]
     state = _lib.make_state(start[0], start[1], (1.0, 0.0, 0.0), goal_x=goal[0], goal_y=goal[1])
+    scheds = (("default", {}, False), ("server_always", {"resident": 2}, False),
+              ("server_idle2000", {"resident": 2, "resident_idle_us": 2000}, False),
+              ("separate", {"resident": 0}, False),
+              ("default", {}, True), ("separate", {"resident": 0}, True))
     for K in (65536, 1000):
-        for sched, opts in (("server", {"resident": 1}), ("server_idle200", {"resident": 1, "resident_idle_us": 200}),
-                            ("separate", {"resident": 0})):
+        for sched, opts, sim_first in scheds:
             eng = _lib.Engine(_lib.make_params(K, 100), device)
             for k, v in opts.items():
                 eng.set_option(k, v)
@@ -523,30 +556,32 @@ def cadence_bench(torch, device, proj, frames=40):
             for i in range(10):
                 eng.step(proj, i, copy=False)
             step = 10
-            for gap_ms in (2.0, 16.0):
+            for gap_ms in ((2.0,) if sim_first else (2.0, 16.0)):
                 lat, wk = [], []
                 i0 = eng.launch_info()
                 for _ in range(frames):
+                    if sim_first:
+                        world_launch()
                     t0 = time.perf_counter()
                     eng.step(proj, step, copy=False)
                     t1 = time.perf_counter()
                     step += 1
                     lat.append((t1 - t0) * 1e3)
-                    wk.append(world_step())
+                    wk.append(world_wait() if sim_first else world_step())
                     while (time.perf_counter() - t1) * 1e3 < gap_ms:
                         time.sleep(0.0002)
                 i1 = eng.launch_info()
                 wk = np.median(np.array(wk), axis=0)
                 lat = np.array(lat)
                 out["rows"].append({
-                    "K": K, "schedule": sched, "gap_ms": gap_ms, "frames": frames,
+                    "K": K, "schedule": sched, "sim_first": sim_first, "gap_ms": gap_ms, "frames": frames,
                     "latency_ms_p50": round(float(np.median(lat)), 4),
                     "latency_ms_p90": round(float(np.percentile(lat, 90)), 4),
                     "copy_ms": round(float(wk[0]), 4), "gemm_ms": round(float(wk[1]), 4),
                     "copy_slowdown": round(float(wk[0] / alone[0]), 3),
                     "gemm_slowdown": round(float(wk[1] / alone[1]), 3),
-                    "server_launches": i1["server_launches"] - i0["server_launches"],
-                    "server_relaunches": i1["server_relaunches"] - i0["server_relaunches"]})
+                    **{k: i1[k] - i0[k] for k in ("server_launches", "server_relaunches", "server_steps",
+                                                  "cadence_steps", "server_fallbacks")}})
             eng.close()
     return out
 
@@ -675,6 +710,7 @@ def main():
         dist.barrier()
     elif members > 1:
         speedup = (args.steps / el) / solo_rate(args.config, args.steps)
+    parity = group_parity(args.config, devices, args.proj) if devices is not None and members > 1 else None
 
     c4 = None
     if not args.no_c4 and args.config != "c4":
@@ -750,6 +786,7 @@ def main():
                                else (group_info or {}).get("rccl_ranks", 0)),
                 "record_bytes_per_rank": record_bytes,
                 "speedup_vs_1": round(speedup, 3) if speedup is not None else None,
+                "group_parity_bitwise": parity,
                 "rollout_kernel": info,
                 "pipelined_tail": not args.sync,
                 "prewarm": {"ms": args.prewarm_ms, "steps": prewarm_steps},

@@ -127,13 +127,21 @@ struct mppi_ctx {
   int roles = -1;     // rollout kernel: -1 auto (role split at <= 1 workgroup per CU), 0 pair, 1 roles (MPPI_ROLES)
   // Resident step server (mppi_step_server_kernel): sampled steps of the role-split plan run on one
   // resident launch that polls the command block `cmd` (pinned) instead of one launch per step
-  // (mppi_set_option "resident", env MPPI_RESIDENT; default on).  It exits after srv_idle_us without a
-  // command, on cmd->stop (every other call on the context stops it first: quiesce) or on a failed
-  // step; the host relaunches it when the last command is older than half the idle limit.
+  // (mppi_set_option "resident", env MPPI_RESIDENT).  It exits after srv_idle_us without a command, on
+  // cmd->stop == its launch id (every other call on the context stops it first: quiesce) or on a
+  // failed step.  resident 1 (default): only back-to-back calls (within half the idle limit of the
+  // last step's return) keep or start it, a step after a longer gap runs as separate launches (the
+  // caller's frame cadence: a launch of the server per frame costs more than the launches it saves);
+  // 2: every step whose plan fits; 0: never.
   int resident = 1;
   ServerCmd* cmd = nullptr;   // pinned
   unsigned* relay = nullptr;  // device [64]: workgroup 0's relay of the command (ServerArgs::relay)
   bool srv_running = false;
+  bool srv_exiting = false;   // a stop was posted and the launch may not have retired yet
+  unsigned srv_launch_id = 0;  // the running (or last) launch's id: its stop word
+  double last_return_us = 0;  // host time the last step returned (0: none yet)
+  int64_t srv_fallbacks = 0;  // server steps whose finish gave up, rerun as separate launches
+  int64_t cadence_steps = 0;  // steps the server's plan fits that ran as separate launches (resident 1)
   int srv_proj = 0;
   double srv_last_us = 0;     // host time the server last became idle (its last step completed, or launch)
   uint64_t srv_idle_us = 200;  // (bench.py cadence leg: at 2000 a simulator kernel needing LDS waited
@@ -150,7 +158,12 @@ struct mppi_ctx {
   size_t srv_lds = 0;
   unsigned srv_exit_after = 0;  // test hook mppi_set_option("server_exit_after"): the next launch's head
                                 // leaves after serving this many commands (0: off)
-  uint64_t fin_wait_ticks = 200000000ull;  // a finish's record wait bound (2 s at 100 MHz; mppi_set_option)
+  // a finish's record wait bound (100 MHz ticks; mppi_set_option): 1 ms, many step periods.  Every
+  // workgroup of a running server is resident, so its records arrive within the rollouts' end spread
+  // (~4 us at C3); a fresh launch whose workgroups cannot all get CUs (another stream's kernels hold
+  // some) would wait for them, while the workgroups it has hold theirs: past the bound the step is
+  // rerun as separate launches, which need no co-residency (step_impl)
+  uint64_t fin_wait_ticks = 100000ull;
   // the server's tail of the last step, launched once its completion word was seen (at the next
   // step's command, or when its outputs are wanted): no kernel waits on the GPU for its inputs
   bool tail_deferred = false;
@@ -548,15 +561,36 @@ int sync_tail(mppi_ctx* c) {
   return MPPI_OK;
 }
 
-// Stop the resident server (it finishes the step it runs, sees cmd->stop and exits): every call on
-// the context but mppi_step / set_state / get_outputs / get_timing starts with this.
-void quiesce(mppi_ctx* c) {
-  if (!c || !c->srv_running) return;
-  __atomic_store_n(&c->cmd->stop, 1u, __ATOMIC_RELEASE);
-  hipSetDevice(c->device);
-  if (hipStreamSynchronize(c->stream) != hipSuccess) (void)hipGetLastError();
-  __atomic_store_n(&c->cmd->stop, 0u, __ATOMIC_RELEASE);
+// Tell the running server to leave (it finishes the step it runs, reads its launch id in cmd->stop
+// and exits) without waiting: launches enqueued after it on the context stream run once it retired.
+void post_stop(mppi_ctx* c) {
+  if (!c->srv_running) return;
+  __atomic_store_n(&c->cmd->stop, c->srv_launch_id, __ATOMIC_RELEASE);
   c->srv_running = false;
+  c->srv_exiting = true;
+}
+
+// Stop the resident server and wait until it has retired: every call on the context but mppi_step /
+// set_state / get_outputs / get_timing starts with this.  Bounded (10 s: its workgroups must get CUs
+// to leave, which another process's kernels can hold): MPPI_EHIP if it did not retire.
+int quiesce(mppi_ctx* c) {
+  if (!c) return MPPI_OK;
+  post_stop(c);
+  if (!c->srv_exiting) return MPPI_OK;
+  hipSetDevice(c->device);
+  const double t0 = now_us();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(c->stream);
+    if (e == hipSuccess) break;
+    if (e != hipErrorNotReady) {
+      c->srv_exiting = false;
+      return fail(MPPI_EHIP, std::string("step server: ") + hipGetErrorString(e));
+    }
+    if (now_us() - t0 > 10e6) return fail(MPPI_EHIP, "the step server did not retire within 10 s of its stop");
+    std::this_thread::yield();
+  }
+  c->srv_exiting = false;
+  return MPPI_OK;
 }
 
 // Zero the finish handoff counter (level1_cnt[0]) and the server's record counter ([16]) after a
@@ -566,8 +600,9 @@ void rearm_counters(mppi_ctx* c) {
 }
 
 // Launch the resident server for the posted command `seq` (its first), with the plan of the last
-// server_step (c->srv_pl ...).  The relay needs no reset: its seq word is older than this command,
-// and its stop word holds the first seq of the launch that wrote it, never this one's.
+// server_step (c->srv_pl ...).  Neither the relay nor cmd->stop needs a reset: the relay's seq word is
+// older than this command, and the stop words hold an earlier launch's id, never this one's (a
+// relaunch for the same command included).
 int launch_server(mppi_ctx* c, unsigned seq) {
   const Plan& pl = c->srv_pl;
   RolloutArgs a;
@@ -580,6 +615,7 @@ int launch_server(mppi_ctx* c, unsigned seq) {
   z.f.n_recs = pl.blocks;
   z.f.level1 = c->level1;
   z.f.level1_cnt = c->level1_cnt;
+  z.f.abort = c->level1_cnt + 24;  // (re-armed with the counters after a failed step)
   z.f.done = c->done;
   z.nroll = pl.blocks;
   z.fin_P = c->srv_P;
@@ -597,6 +633,8 @@ int launch_server(mppi_ctx* c, unsigned seq) {
     z.tail_out[i] = c->tail_host[i];
   }
   z.first_seq = seq;
+  if (++c->srv_launch_id == 0) c->srv_launch_id = 1;
+  z.launch_id = c->srv_launch_id;
   z.wait_ticks = c->fin_wait_ticks;
   z.idle_ticks = c->srv_idle_us * 100;
   z.exit_after = c->srv_exit_after;
@@ -670,7 +708,13 @@ int wait_done(mppi_ctx* c) {
   }
   c->srv_cmd_live = false;
   ++c->srv_failed;
-  quiesce(c);
+  // (a server whose workgroups cannot all get CUs retires once they do: until then nothing may be
+  // re-armed or rerun, and a server that never retires fails the call here)
+  const std::string saved = why;
+  if (quiesce(c)) {
+    c->fail_kind = 3;
+    return fail(MPPI_EHIP, saved + "; " + g_err);
+  }
   rearm_counters(c);
   // the normals the failed step's server was to generate may be incomplete: regenerate them
   if (c->last_resident && c->srv_cmd_noise >= 0) c->eps_step[c->srv_cmd_noise] = -1;
@@ -766,14 +810,14 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
   int rc = ensure_nodes(c, pl.blocks);
   if (rc) return rc;
-  if (mode == 1) {  // injected controls: the leaf reads them back from here
+  if (mode == 1 || MPPI_NOISE_REG) {  // injected / sampled controls the leaf reads back from HBM
     rc = grow(c->ustore, c->ustore_cap, (size_t)pl.blocks * pl.traj_per_block * 2 * H_of(c) * sizeof(float), c->stream);
     if (rc) return rc;
   }
   RolloutArgs a;
   fill_rollout(c, pl, st, step, unom, a);
   int eps_slot = -1;
-  if (mode == 0 && pl.blocks > 0) {
+  if (mode == 0 && pl.blocks > 0 && !MPPI_NOISE_REG) {
     rc = eps_for_step(c, pl, step, c->stream, false, &eps_slot);
     if (rc) return rc;
     a.eps = c->eps[eps_slot];
@@ -1003,7 +1047,7 @@ void remember(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
 // MPPI_HOST_TRACE marks of a step: 0 entry, 1 normals ready, 2 tail slot free (server), 3 command
 // posted / launches enqueued, 4 side launches done (the previous tail), 5 completion seen + copies
 void trace_mark(mppi_ctx* c, int k) {
-  if (c->trace) c->tr_m[k] = now_us();
+  if (c && c->trace) c->tr_m[k] = now_us();
 }
 
 bool server_shape(const mppi_ctx* c, const Plan& pl, int mode, int* P, int* ncol, int* groups, size_t* lds) {
@@ -1020,31 +1064,34 @@ bool server_shape(const mppi_ctx* c, const Plan& pl, int mode, int* P, int* ncol
 
 int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int ncol, int groups, size_t lds) {
   if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
-  if (c->srv_running && proj != c->srv_proj) quiesce(c);
+  if (c->srv_running && proj != c->srv_proj) post_stop(c);  // (the next launch queues behind it)
   // (first step: the buffers are allocated before the server holds pointers to them)
-  if (c->srv_running && (c->nodes_cap < (size_t)pl.blocks * E_of(c) || c->eps_cap < (size_t)pl.blocks * 2 * H_of(c) * 256))
-    quiesce(c);
-  int rc = ensure_nodes(c, pl.blocks);
+  int rc = MPPI_OK;
+  const size_t rows = (size_t)pl.blocks * 2 * H_of(c) * 256;
+  if (c->nodes_cap < (size_t)pl.blocks * E_of(c) || (MPPI_NOISE_REG ? c->ustore_cap < rows * sizeof(float) : c->eps_cap < rows))
+    rc = quiesce(c);
+  if (!rc) rc = ensure_nodes(c, pl.blocks);
+  if (!rc && MPPI_NOISE_REG) rc = grow(c->ustore, c->ustore_cap, rows * sizeof(float), c->stream);
   if (rc) return rc;
+  int slot = 0, noise_slot = -1;
+  const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);  // Philox blocks per trajectory and step
+#if !MPPI_NOISE_REG
   // a step whose normals no slot holds (first step, a jump of the step counter): the server may still
   // be writing normals of a later step in its last noise phase, so it is stopped before any slot is
   // regenerated
   bool have = false;
   for (int i = 0; i < kEpsSlots; ++i) have |= c->eps_step[i] == (int64_t)step;
-  if (!have) quiesce(c);
-  int slot = -1;
+  if (!have && (rc = quiesce(c))) return rc;
   rc = eps_for_step(c, pl, step, c->noise_stream, true, &slot);
   if (rc) return rc;
   trace_mark(c, 1);
   // normals of step + 1 (normally generated by the previous step's noise phase; else now, on the
   // noise stream beside this step) and of step + 2 (by this step's noise phase, in the server)
-  const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);
   // the server's noise phase runs mostly in the workgroups outside the finish: with fewer than a
   // quarter of them, or fewer than two (few records: every rollout workgroup may hold a finish
   // column) the noise kernel does it
   const bool srv_noise = pl.blocks - groups >= 2 &&
                          (int64_t)(pl.blocks - groups) * 4 >= (int64_t)pl.blocks;
-  int noise_slot = -1;
   for (int d = 1; d <= 2; ++d) {
     const uint64_t target = step + (uint64_t)d;
     bool got = false;
@@ -1065,6 +1112,7 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
     }
     c->eps_step[v] = (int64_t)target;
   }
+#endif
   const int par = ((c->tail_deferred ? c->tail_def_par : c->tail_par) + 1) % kTailSlots;
   if (c->async_tail && c->tail_inflight[par]) {  // the tail of kTailSlots steps ago: long done
     HIP_TRY(hipEventSynchronize(c->ev_tail[par]));
@@ -1084,13 +1132,15 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   d.mode = c->async_tail ? 2 : 1;
   d.noise_slot = noise_slot;
   c->srv_cmd_noise = noise_slot;
-  d.noise_n_base_lo = (unsigned)((step + 2) * nb);
-  d.noise_n_base_hi = (unsigned)(((step + 2) * nb) >> 32);
+  // (MPPI_NOISE_REG: the Philox base of this step's normals, which the producer waves generate)
+  const uint64_t nbase = (MPPI_NOISE_REG ? step : step + 2) * nb;
+  d.noise_n_base_lo = (unsigned)nbase;
+  d.noise_n_base_hi = (unsigned)(nbase >> 32);
   // a server idle for more than half its limit (since its last step completed) may be leaving: stop
-  // it and start a fresh one.  This is checked after the host's waits above, right before the command
-  // is posted; a head that leaves anyway (a slower host) never relays the command, and wait_done
-  // relaunches the server with it
-  if (c->srv_running && now_us() - c->srv_last_us > 0.5 * (double)c->srv_idle_us) quiesce(c);
+  // it and start a fresh one behind it.  This is checked after the host's waits above, right before
+  // the command is posted; a head that leaves anyway (a slower host) never relays the command, and
+  // wait_done relaunches the server with it
+  if (c->srv_running && now_us() - c->srv_last_us > 0.5 * (double)c->srv_idle_us) post_stop(c);
   unsigned* cw = reinterpret_cast<unsigned*>(cmd);
   const unsigned* dw = reinterpret_cast<const unsigned*>(&d);
   for (int i = 2; i < kCmdWords; ++i) __atomic_store_n(cw + i, dw[i], __ATOMIC_RELAXED);
@@ -1140,14 +1190,26 @@ int enqueue_step(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl)
 
 int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out) {
   int rc = check_ready(c);
-  trace_mark(c, 0);
   if (rc) return rc;
+  trace_mark(c, 0);
   const Plan pl = make_plan(c);
   int sP = 0, scol = 0, sgroups = 0;
   size_t slds = 0;
-  const bool resident = server_shape(c, pl, mode, &sP, &scol, &sgroups, &slds);
+  bool resident = server_shape(c, pl, mode, &sP, &scol, &sgroups, &slds);
+  if (resident && c->resident == 1) {
+    // the caller's cadence: a call more than half the idle limit after the last step returned (a
+    // simulator frame) runs as separate launches, and a server that has been idle that long is told
+    // to leave (the launches queue behind it); back-to-back calls keep or start the server
+    const double now = now_us(), half = 0.5 * (double)c->srv_idle_us;
+    const bool back_to_back = c->last_return_us > 0 && now - c->last_return_us <= half;
+    if (c->srv_running ? now - c->srv_last_us > half : !back_to_back) {
+      post_stop(c);
+      resident = false;
+      ++c->cadence_steps;
+    }
+  }
   if (!resident) {
-    quiesce(c);
+    post_stop(c);  // (stream order: these launches run after it retired)
     rc = flush_tail(c);
     if (rc) return rc;
   }
@@ -1157,20 +1219,28 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   remember(c, proj, step, mode, pl);
   trace_mark(c, 4);
   rc = copy_outputs(c, out);
-  // a freshly launched server that retired without serving its first command (it cannot hold all
-  // its workgroups on the device at once): separate launches from now on, this step again (it
-  // published nothing and changed no state).  A server that left on its idle limit as the command
-  // was posted is not this case: wait_done relaunched it.
-  if (resident && rc == MPPI_EHIP && c->fail_kind == 2) {
-    if (!c->srv_warned)
-      std::fprintf(stderr, "mppi: the resident step server could not run here; using separate launches\n");
-    c->srv_warned = true;
-    c->resident = false;
+  // A server step that did not complete published nothing and changed no state (wait_done stopped
+  // the server, waited for it to retire and re-armed its counters): this step again as separate
+  // launches.  Its finish gave up (1: the rollout workgroups could not all get CUs within the wait
+  // bound, e.g. beside another process's kernels): counted, the server stays the schedule.  A fresh
+  // launch retired without serving its first command (2): it cannot run here, separate launches from
+  // now on.  (A server that left on its idle limit as the command was posted is neither: wait_done
+  // relaunched it.)
+  if (resident && rc == MPPI_EHIP && (c->fail_kind == 1 || c->fail_kind == 2)) {
+    if (c->fail_kind == 2) {
+      if (!c->srv_warned)
+        std::fprintf(stderr, "mppi: the resident step server could not run here; using separate launches\n");
+      c->srv_warned = true;
+      c->resident = 0;
+    } else {
+      ++c->srv_fallbacks;
+    }
     c->last_resident = false;
     rc = enqueue_step(c, proj, step, mode, pl);
     if (rc) return rc;
     rc = copy_outputs(c, out);
   }
+  c->last_return_us = now_us();
   if (c->trace) {  // marks a schedule does not set (separate launches: 1, 2) take the one before
     c->tr_m[5] = now_us();
     for (int k = 1; k < 6; ++k) c->tr_m[k] = std::max(c->tr_m[k], c->tr_m[k - 1]);
@@ -1305,7 +1375,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
   // MPPI_GROUP_RCCL for groups)
   if (const char* e = std::getenv("MPPI_HOST_TRACE")) c->trace = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPPI_ROLES")) c->roles = std::atoi(e) != 0;
-  if (const char* e = std::getenv("MPPI_RESIDENT")) c->resident = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MPPI_RESIDENT")) c->resident = std::min(std::max(std::atoi(e), 0), 2);
   const int H = p.num_iterations;
   auto cleanup = [&](int rc) {
     mppi_destroy(c);
@@ -1366,7 +1436,7 @@ int mppi_create(const mppi_params* params, int32_t device, mppi_ctx** out) {
 
 void mppi_destroy(mppi_ctx* c) {
   if (!c) return;
-  quiesce(c);
+  (void)quiesce(c);
   if (c->trace && c->tr_n > 0) {
     static const char* ph[6] = {"caller", "normals wait", "tail slot wait", "command / launches", "side launches",
                                 "completion + copies"};
@@ -1438,7 +1508,7 @@ void mppi_destroy(mppi_ctx* c) {
 
 int mppi_set_stream(mppi_ctx* c, void* s) {
   if (!c) return fail(MPPI_EINVAL, "null context");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   int rc = sync_tail(c);
@@ -1479,7 +1549,7 @@ static int build_normal_table(mppi_ctx* c) {
 int mppi_set_dem(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float x_min, float y_min,
                  float resolution) {
   if (!c || !z) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   int rc = check_grid(rows, cols, resolution);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
@@ -1509,7 +1579,7 @@ int mppi_set_dem(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float 
 int mppi_set_dem_device(mppi_ctx* c, const float* z, int32_t rows, int32_t cols, float x_min,
                         float y_min, float resolution) {
   if (!c || !z) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   int rc = check_grid(rows, cols, resolution);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
@@ -1532,7 +1602,7 @@ int mppi_set_dem_device(mppi_ctx* c, const float* z, int32_t rows, int32_t cols,
 
 int mppi_dem_updated(mppi_ctx* c) {
   if (!c) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   if (!c->Z || c->rows <= 0) return fail(MPPI_EINVAL, "no DEM bound");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());  // the in-place write may be on any stream of the device
@@ -1543,7 +1613,7 @@ int mppi_dem_updated(mppi_ctx* c) {
 
 int mppi_set_costmap(mppi_ctx* c, const float* cm, int32_t size, float half_width, float resolution) {
   if (!c || !cm) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   if (size < 1) return fail(MPPI_EINVAL, "costmap size must be >= 1");
   if (!(resolution > 0.0f)) return fail(MPPI_EINVAL, "costmap resolution must be > 0");
   HIP_TRY(hipSetDevice(c->device));
@@ -1567,7 +1637,7 @@ int mppi_set_state(mppi_ctx* c, const mppi_state* s) {
 
 int mppi_set_nominal(mppi_ctx* c, const float* u1, const float* u2) {
   if (!c || !u1 || !u2) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   HIP_TRY(hipSetDevice(c->device));
   const int H = H_of(c);
   HIP_TRY(hipMemcpyAsync(c->u_nom[c->cur], u1, H * sizeof(float), hipMemcpyHostToDevice, c->stream));
@@ -1578,7 +1648,7 @@ int mppi_set_nominal(mppi_ctx* c, const float* u1, const float* u2) {
 
 int mppi_get_nominal(mppi_ctx* c, float* u1, float* u2) {
   if (!c || !u1 || !u2) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   HIP_TRY(hipSetDevice(c->device));
   const int H = H_of(c);
   HIP_TRY(hipMemcpyAsync(u1, c->u_nom[c->cur], H * sizeof(float), hipMemcpyDeviceToHost, c->stream));
@@ -1594,7 +1664,7 @@ int mppi_step(mppi_ctx* c, int32_t proj, uint64_t step, mppi_outputs* out) {
 int mppi_step_injected(mppi_ctx* c, int32_t proj, const float* u1, const float* u2,
                        mppi_outputs* out) {
   if (!c || !u1 || !u2) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   HIP_TRY(hipSetDevice(c->device));
   const size_t n = (size_t)std::max<int64_t>(c->p.num_trajectories, 1) * H_of(c);
   if (!c->inj1) {
@@ -1611,7 +1681,7 @@ int64_t mppi_record_len(mppi_ctx* c) { return c ? E_of(c) : -1; }
 
 int mppi_step_partial(mppi_ctx* c, int32_t proj, uint64_t step, double* record_dev) {
   if (!c) return fail(MPPI_EINVAL, "null context");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   int rc = check_ready(c);
   if (rc) return rc;
   if (!record_dev) return fail(MPPI_EINVAL, "null record buffer");
@@ -1625,7 +1695,7 @@ int mppi_step_partial(mppi_ctx* c, int32_t proj, uint64_t step, double* record_d
 
 int mppi_step_finish(mppi_ctx* c, const double* records_dev, int32_t n, mppi_outputs* out) {
   if (!c) return fail(MPPI_EINVAL, "null context");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   int rc = check_ready(c);
   if (rc) return rc;
   if (!records_dev || n < 1) return fail(MPPI_EINVAL, "records required");
@@ -1637,7 +1707,7 @@ int mppi_step_finish(mppi_ctx* c, const double* records_dev, int32_t n, mppi_out
 
 int mppi_get_costs(mppi_ctx* c, float* costs, int64_t n) {
   if (!c || !costs) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   if (n < 0 || n > c->p.num_trajectories) return fail(MPPI_EINVAL, "n out of range");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipMemcpyAsync(costs, c->cost, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
@@ -1648,7 +1718,7 @@ int mppi_get_costs(mppi_ctx* c, float* costs, int64_t n) {
 int mppi_dump_rollouts(mppi_ctx* c, float* traj, float* hv, float* lw, float* rw, float* v, float* w,
                        float* u1, float* u2) {
   if (!c) return fail(MPPI_EINVAL, "null context");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   int rc = check_ready(c);
   if (rc) return rc;
   if (!c->have_last) return fail(MPPI_ESTATE, "no step to dump");
@@ -1689,10 +1759,11 @@ int mppi_dump_rollouts(mppi_ctx* c, float* traj, float* hv, float* lw, float* rw
 
 int mppi_set_option(mppi_ctx* c, const char* name, int64_t value) {
   if (!c || !name) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   const std::string n(name);
-  if (n == "resident") {  // the resident step server on (1, default) / off (0: one launch per kernel)
-    c->resident = value != 0;
+  if (n == "resident") {  // the resident step server: 1 for back-to-back calls (default), 2 always, 0 never
+    if (value < 0 || value > 2) return fail(MPPI_EINVAL, "resident must be 0, 1 or 2");
+    c->resident = (int)value;
     return MPPI_OK;
   }
   if (n == "resident_idle_us") {  // how long an idle server stays resident
@@ -1719,7 +1790,7 @@ int mppi_set_option(mppi_ctx* c, const char* name, int64_t value) {
 
 int mppi_set_timing(mppi_ctx* c, int32_t enable) {
   if (!c) return fail(MPPI_EINVAL, "null context");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   int rc = sync_tail(c);
   if (rc) return rc;
   if (enable < 0 || enable > 2) return fail(MPPI_EINVAL, "timing mode must be 0, 1 or 2");
@@ -1741,7 +1812,7 @@ int mppi_get_tail_timing(mppi_ctx* c, double* tail_ms, int64_t* n) {
 
 int mppi_set_async_tail(mppi_ctx* c, int32_t enable) {
   if (!c) return fail(MPPI_EINVAL, "null context");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   HIP_TRY(hipSetDevice(c->device));
   int rc = sync_tail(c);
   if (rc) return rc;
@@ -1781,7 +1852,7 @@ int mppi_get_server_time(mppi_ctx* c, double* roll_us, double* step_us, int64_t*
 
 int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
   if (!c || !out) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   std::vector<uint64_t> all((size_t)kClkWords, 0);
@@ -1831,16 +1902,17 @@ int mppi_get_chain_clock(mppi_ctx* c, double* out, int32_t n) {
 int mppi_get_launch_info(mppi_ctx* c, int64_t* info, int32_t n) {
   if (!c || !info) return fail(MPPI_EINVAL, "null argument");
   const Plan& pl = c->last_plan;
-  const int64_t v[16] = {0, pl.block, pl.blocks, pl.W, pl.Wr, (int64_t)pl.lds_bytes, c->fin_kind,
+  const int64_t v[18] = {0, pl.block, pl.blocks, pl.W, pl.Wr, (int64_t)pl.lds_bytes, c->fin_kind,
                          c->fin_P, c->fin_ncol, c->fin_groups, pl.ucache_steps, c->last_resident ? 1 : 0,
-                         c->srv_launches, c->srv_steps, c->srv_failed, c->srv_relaunches};
-  for (int i = 0; i < n && i < 16; ++i) info[i] = v[i];
+                         c->srv_launches, c->srv_steps, c->srv_failed, c->srv_relaunches, c->srv_fallbacks,
+                         c->cadence_steps};
+  for (int i = 0; i < n && i < 18; ++i) info[i] = v[i];
   return MPPI_OK;
 }
 
 int mppi_bilinear_query(mppi_ctx* c, const float* x, const float* y, float* h, int64_t n) {
   if (!c || !x || !y || !h) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   if (!c->Z) return fail(MPPI_ESTATE, "no DEM");
   if (n < 0) return fail(MPPI_EINVAL, "n < 0");
   HIP_TRY(hipSetDevice(c->device));
@@ -1860,7 +1932,7 @@ int mppi_bilinear_tiles(mppi_ctx* c, int32_t* ntiles) {
 int mppi_bin_queries(mppi_ctx* c, const float* x, const float* y, int64_t n, float* xs_out, float* ys_out,
                      int32_t* perm, int32_t* tile_off) {
   if (!c || !x || !y || !xs_out || !ys_out || !perm || !tile_off) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   if (!c->Z) return fail(MPPI_ESTATE, "no DEM");
   if (n < 0 || n > INT32_MAX) return fail(MPPI_EINVAL, "n out of range [0, 2^31)");
   HIP_TRY(hipSetDevice(c->device));
@@ -1903,7 +1975,7 @@ int mppi_bin_queries(mppi_ctx* c, const float* x, const float* y, int64_t n, flo
 
 int mppi_bilinear_tiled(mppi_ctx* c, const float* xs, const float* ys, const int32_t* tile_off, float* h) {
   if (!c || !xs || !ys || !tile_off || !h) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   if (!c->Z) return fail(MPPI_ESTATE, "no DEM");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(launch_bilinear_tiled(c->Z, c->rows, c->cols, c->x_min, c->y_min, c->res, c->rinv_res,
@@ -1913,15 +1985,24 @@ int mppi_bilinear_tiled(mppi_ctx* c, const float* xs, const float* ys, const int
 
 int mppi_sync(mppi_ctx* c) {
   if (!c) return fail(MPPI_EINVAL, "null context");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return MPPI_OK;
 }
 
+int mppi_debug_hold(int32_t device, void* stream, int32_t groups, int32_t lds_bytes, int32_t microseconds) {
+  if (groups < 1 || groups > 65536 || lds_bytes < 64 || (size_t)lds_bytes > kLdsBytes || microseconds < 0 ||
+      microseconds > 1000000)
+    return fail(MPPI_EINVAL, "debug_hold: groups in [1, 65536], lds_bytes in [64, 160 KiB], microseconds <= 1e6");
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(launch_hold(groups, (size_t)lds_bytes, (uint64_t)microseconds * 100, (hipStream_t)stream));
+  return MPPI_OK;
+}
+
 int mppi_selftest(mppi_ctx* c, int32_t what, int64_t n, uint64_t seed, int64_t* mismatches) {
   if (!c || !mismatches) return fail(MPPI_EINVAL, "null argument");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   if (what < 0 || what > 5 || n < 0 || (what == 5 && n > 2 + 0x4C000000LL)) return fail(MPPI_EINVAL, "bad selftest arguments");
   HIP_TRY(hipSetDevice(c->device));
   unsigned long long* d = nullptr;
@@ -1941,7 +2022,7 @@ int mppi_build_costmap(mppi_ctx* c, const double* obstacles, int32_t n, int32_t 
                        double origin_x, double origin_y, double r_robot, int32_t power, float* out_host,
                        int32_t metric) {
   if (!c) return fail(MPPI_EINVAL, "null context");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   int rc = costmap_check(obstacles, n, size, power, metric);
   if (rc) return rc;
   const float res = (float)(2 * half_width / size);  // Surface.costmap_resolution (MPPI_isaac.py:272)
@@ -2026,7 +2107,7 @@ int mppi_rollout_python25d(mppi_ctx* c, int64_t n, int32_t H, const double* x0, 
                            const double* heading, const double* lin_vel, const double* ang_vel, double dt,
                            double half_width, double resolution, double bound, double* traj, int32_t* valid) {
   if (!c) return fail(MPPI_EINVAL, "null context");
-  quiesce(c);
+  if (int rc_q = quiesce(c)) return rc_q;
   if (n < 0 || H < 1) return fail(MPPI_EINVAL, "python25d: need n >= 0 and H >= 1");
   if (n == 0) return MPPI_OK;
   if (!x0 || !y0 || !heading || !lin_vel || !ang_vel || !traj || !valid)
@@ -2390,7 +2471,12 @@ int mppi_group_selftest(int32_t n, int32_t fail_member, int32_t steps, int64_t* 
   g->selftest = true;
   g->fail_member = fail_member;
   g->dev.assign(n, 0);
-  start_workers(g);
+  try {  // (std::thread can throw: the exception must not cross the C ABI)
+    start_workers(g);
+  } catch (const std::exception& ex) {
+    mppi_group_destroy(g);
+    return fail(MPPI_EHIP, std::string("group selftest: worker threads: ") + ex.what());
+  }
   int64_t done = 0, failed = 0, named = 0;
   for (int k = 0; k < steps; ++k) {
     const int rc = group_step_threaded(g, 3, (uint64_t)k, nullptr);

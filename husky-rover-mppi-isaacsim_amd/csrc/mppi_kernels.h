@@ -4,14 +4,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// MPPI_NOISE_REG 1: the rollout's producer generates each step's sampling normals in registers
+// (Philox, sampling_warp.py:73-90) and keeps the sampled controls the LDS cache cannot hold in
+// ustore for the leaf; 0: the normals precomputed by mppi_noise_kernel into HBM rows (round 1-5)
+#ifndef MPPI_NOISE_REG
+#define MPPI_NOISE_REG 1
+#endif
+
 namespace mppi {
 
 // The resident step server's command block (mppi_capi.cpp "resident step server"): pinned host
 // memory the host fills for every step (every field, then seq with release order); the server's
-// workgroups poll seq and read the rest with system-scope loads.  stop != 0 ends the server.
+// workgroups poll seq and read the rest with system-scope loads.  stop == the launch's launch_id
+// ends that launch (a later launch has another id: the host never clears the word).
 struct ServerCmd {
   unsigned seq;    // the step's completion sequence number (written last)
-  unsigned stop;   // (same 8-byte word as seq: one poll reads both)
+  unsigned stop;   // (same 8-byte word as seq: one poll reads both; checked before seq)
   int eps_slot;    // normals slot of the step
   int cur;         // nominal buffer the step reads (the finish writes the other one)
   int tail_slot;   // deferred optimal rollout slot (mode 2)
@@ -58,6 +66,9 @@ struct FinishArgs {
   // memory, system scope, release) so the host can spin on it instead of a stream sync
   unsigned* done;
   unsigned seq;
+  // resident server: a finish workgroup that gave up stores the step's seq here, and the last finish
+  // workgroup's u_opt poll stops on it (null: separate launches)
+  unsigned* abort;
   uint64_t* clk;  // optional: the deferred tail's stamps (kClkServer ring)
   // multi-workgroup first tree level (launch_finish with groups > 1)
   double* level1;         // [groups][2H+2]
@@ -166,8 +177,9 @@ struct ServerArgs {
   int nroll, fin_P, fin_ncol, fin_groups;
   unsigned* rec_cnt;          // [0] records counted; zeroed, re-armed by the finish
   const ServerCmd* cmd;       // pinned host memory (polled by workgroup 0 only)
-  unsigned* relay;            // device: [0] seq, [1] stop (the first_seq of the launch that stopped) as relayed
-                              // by workgroup 0, [16, 16 + kCmdWords) the command words
+  unsigned* relay;            // device: [0] seq, [1] stop (the launch_id of the launch that stopped) as relayed
+                              // by the head, [16, 16 + kCmdWords) the command words
+  unsigned launch_id;         // unique per launch of the context (never 0): the stop word that ends it
   float* eps[3];              // the normals slots
   float* u_nom[2];            // the nominal double buffer, [2H] each
   float* tail_in[kTailSlots];   // deferred optimal rollout inputs per slot (device)
@@ -194,6 +206,8 @@ hipError_t launch_tail(const FinishArgs& f, hipStream_t st);
 // per-cell surface normals of the DEM, [(rows+1) x (grid+1)] float4 (x, y, z, 0)
 hipError_t launch_normal_table(const float* Z, int rows, int grid, float res, float4* out, hipStream_t st);
 hipError_t launch_selftest(int what, int64_t n, uint64_t seed, unsigned long long* bad, hipStream_t st);
+// test hook: `groups` workgroups each holding `lds` bytes of LDS for `ticks` (100 MHz)
+hipError_t launch_hold(int groups, size_t lds, uint64_t ticks, hipStream_t st);
 // counts the significands a in [1, 2) for which cdiv_f(a, b, y) != a / b (IEEE)
 hipError_t launch_cdiv_verify(float b, float y, unsigned* bad, hipStream_t st);
 // The sampling normals of one step (Philox block n_base + t/2 of global trajectory k_offset + k),

@@ -863,8 +863,8 @@ constexpr int UCACHE_ROW = 256 + 4;
 template <int TB, int NT, bool EPS = false, bool WT = false>
 __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
                                              unsigned char* scratch, const float* ub_block,
-                                             const float* unom = nullptr, const float* ucache = nullptr,
-                                             int uc_steps = 0, int blk = -1);
+                                             const float* unom, const float* ucache, int uc_steps,
+                                             int blk = -1);
 
 // =====================================================================  leaf records (shared)
 // Softmax leaf records (DEFINED replacement of critics_warp.py:338-376) for the
@@ -940,20 +940,20 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
       const int tr0 = 256 * leaf + 128 * half + 32 * line;  // first trajectory of the line
       w4r[q] = reinterpret_cast<const float4*>(wbuf + tr0);
       const float4* u4 = reinterpret_cast<const float4*>(ub_block + (size_t)(j >= 2 ? j - 2 : 0) * TB + tr0);
-      bool cached = false;  // the sampled controls of this row are in LDS (no normals re-read)
+      bool cached = false;  // the sampled controls of this row are in LDS (no HBM row read)
       float nom = 0.f, sg = 0.f, lo = 0.f, hi = 0.f;
+      const int c = (j - 2) >= H ? 1 : 0;
+      const int t = max(j - 2, 0) - c * H;
       if constexpr (EPS) {  // rows hold the normals: u = clamp(u_nom[t+1] + sigma*eps) as sampled
-        const int c = (j - 2) >= H ? 1 : 0;
-        const int t = max(j - 2, 0) - c * H;
         const int ti = min(t + 1, H - 1);
         nom = unom[c * H + ti];
         sg = c ? a.s2 : a.s1;
         lo = c ? a.min_u2 : a.min_u1;
         hi = c ? a.max_u2 : a.max_u1;
-        if (j >= 2 && t < uc_steps) {
-          cached = true;
-          u4 = reinterpret_cast<const float4*>(ucache + (size_t)(c * uc_steps + t) * UCACHE_ROW + tr0);
-        }
+      }
+      if (j >= 2 && t < uc_steps) {
+        cached = true;
+        u4 = reinterpret_cast<const float4*>(ucache + (size_t)(c * uc_steps + t) * UCACHE_ROW + tr0);
       }
       cached_r[q] = cached;
       nom_r[q] = nom;
@@ -1304,15 +1304,17 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   // ---------------- per-role state
   Traj s;                       // chain
   float L = a.wl, R = a.wr;     // side: filter
+  float en1 = 0.f, en2 = 0.f;
+#if !MPPI_NOISE_REG
   // side, MODE 0: this trajectory's normals, rows [2][H] of 256 (mppi_noise_kernel)
   const float* eps_row = (MODE == 0) ? a.eps + (size_t)blockIdx.x * (2 * H) * TB + tj : nullptr;
-  float en1 = 0.f, en2 = 0.f;
   if constexpr (MODE == 0) {
     if (side) {
       en1 = eps_row[0];
       en2 = eps_row[(size_t)H * TB];
     }
   }
+#endif
   float pf_sum = 0.f, sw = 0.f, sp = 0.f, ob = 0.f, last_x = a.x0, last_y = a.y0;
   float lwx = 0.f, lwy = 0.f, lwz = 0.f, rwx = 0.f, rwy = 0.f, rwz = 0.f;
   float* ust = a.ustore + (size_t)blockIdx.x * (2 * H) * TB + tj;
@@ -1410,11 +1412,15 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
     //    DUMP), used one half later.
     int seen_chain = 0;                                 // last acquired value of f_chain
     float eA1 = en1, eA2 = en2, eB1 = 0.f, eB2 = 0.f;  // normals of the even / odd step
+#if MPPI_NOISE_REG
+    const uint64_t kg = (uint64_t)(a.k_offset + (int64_t)blockIdx.x * TB + tj);
+#else
     if constexpr (MODE == 0) {
       const int t1 = min(1, H - 1);
       eB1 = eps_row[(size_t)t1 * TB];
       eB2 = eps_row[(size_t)(H + t1) * TB];
     }
+#endif
     float cmA = 0.f, cmB = 0.f;                        // costmap value of the even / odd step
     float elx = 0.f, ely = 0.f, elz = 0.f, erx = 0.f, ery = 0.f, erz = 0.f;  // even step's contacts
     // PROD / CONS: the half produces step p / consumes step sc = p - PAIR_LAG for sure
@@ -1428,12 +1434,19 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
       if (PROD || (GUARD && p < H)) {  // sampling, filter (sampling_warp.py:54-138); normals precomputed
         float u1, u2;
         if constexpr (MODE == 0) {
+#if MPPI_NOISE_REG
+          // Philox block n_base + p / 2: the normals of steps p and p + 1 (the even half)
+          if constexpr (!ODD) noise_block_pk(a.seed, a.n_base + (uint64_t)(p >> 1), kg, &eA1, &eA2, &eB1, &eB2);
+#endif
           const int ti = min(p + 1, H - 1);
           u1 = clampf(unom_lds[ti] + a.s1 * e1r, a.min_u1, a.max_u1);
           u2 = clampf(unom_lds[H + ti] + a.s2 * e2r, a.min_u2, a.max_u2);
           if (p < a.ucache_steps) {  // kept for the leaf reduction (uniform branch)
             ucache[(size_t)p * UCACHE_ROW + tj] = u1;
             ucache[(size_t)(a.ucache_steps + p) * UCACHE_ROW + tj] = u2;
+          } else if (MPPI_NOISE_REG) {  // the rest in HBM (the leaf reads them back)
+            ust[(size_t)p * TB] = u1;
+            ust[(size_t)(H + p) * TB] = u2;
           }
         } else {
           const size_t o = (size_t)(valid ? kl : 0) * H + p;
@@ -1525,11 +1538,13 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
         }
         lds_store_release(f_cons, sc + 1);
       }
+#if !MPPI_NOISE_REG
       if constexpr (MODE == 0) {  // prefetch the normals of step p + 2 into the registers just freed
         const int tn = min(p + 2, H - 1);
         e1r = eps_row[(size_t)tn * TB];
         e2r = eps_row[(size_t)(H + tn) * TB];
       }
+#endif
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
@@ -1574,11 +1589,12 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   }
 #endif
   __syncthreads();
-  if constexpr (MODE == 0)  // rows hold the normals; the leaf recomputes the sampled controls
-    leaf_records<TB, NT, true>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB, unom_lds, ucache,
-                               a.ucache_steps);
+  if constexpr (MODE == 0)  // (as the role-split kernel's)
+    leaf_records<TB, NT, !MPPI_NOISE_REG>(a, cost_lds, scratch,
+                                          (MPPI_NOISE_REG ? a.ustore : a.eps) + (size_t)blockIdx.x * (2 * H) * TB,
+                                          unom_lds, ucache, a.ucache_steps);
   else
-    leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
+    leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB, unom_lds, ucache, 0);
 #ifdef MPPI_STAMPS
   const uint64_t k_t2 = dbg_stamp(), k_r2 = __builtin_amdgcn_s_memrealtime();
   if ((tid & 63) == 0 && blockIdx.x < 64) {
@@ -1762,11 +1778,18 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
   else if (role == ROLE_PROD) {
     // ---------------- sampling + wheel filter + sin/cos, normals prefetched two steps ahead
     // (even / odd steps in their own registers: no loop-carried copy of a load in flight)
-    const float* eps_row = (MODE == 0) ? a.eps + (size_t)blk * (2 * H) * TB + tj : nullptr;
     float* ust = a.ustore + (size_t)blk * (2 * H) * TB + tj;
     float L = a.wl, R = a.wr;
     int seen_cost = 0;
     float eA1 = 0.f, eA2 = 0.f, eB1 = 0.f, eB2 = 0.f;
+#if MPPI_NOISE_REG
+    // Philox block n_base + p / 2 of this global trajectory: the normals of steps p and p + 1
+    const uint64_t kg = (uint64_t)(a.k_offset + (int64_t)blk * TB + tj);
+    auto gen = [&](int p) __attribute__((always_inline)) {
+      if constexpr (MODE == 0) noise_block_pk(a.seed, a.n_base + (uint64_t)(p >> 1), kg, &eA1, &eA2, &eB1, &eB2);
+    };
+#else
+    const float* eps_row = (MODE == 0) ? a.eps + (size_t)blk * (2 * H) * TB + tj : nullptr;
     if constexpr (MODE == 0) {
       eA1 = eps_row[0];
       eA2 = eps_row[(size_t)H * TB];
@@ -1774,6 +1797,8 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       eB1 = eps_row[(size_t)t1 * TB];
       eB2 = eps_row[(size_t)(H + t1) * TB];
     }
+    auto gen = [&](int) {};
+#endif
     auto prod = [&](int p, float& e1r, float& e2r) __attribute__((always_inline)) {
       float u1, u2;
       if constexpr (MODE == 0) {
@@ -1783,6 +1808,9 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
         if (p < a.ucache_steps) {  // kept for the leaf reduction (uniform branch)
           ucache[(size_t)p * UCACHE_ROW + tj] = u1;
           ucache[(size_t)(a.ucache_steps + p) * UCACHE_ROW + tj] = u2;
+        } else if (MPPI_NOISE_REG) {  // the rest in HBM (the leaf reads them back)
+          ust[(size_t)p * TB] = u1;
+          ust[(size_t)(H + p) * TB] = u2;
         }
       } else {
         const size_t o = (size_t)(valid ? kl : 0) * H + p;
@@ -1813,18 +1841,24 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
         }
       }
       lds_store_release(f_prod, p + 1);
+#if !MPPI_NOISE_REG
       if constexpr (MODE == 0) {  // the normals of step p + 2 into the registers just freed
         const int tn = min(p + 2, H - 1);
         e1r = eps_row[(size_t)tn * TB];
         e2r = eps_row[(size_t)(H + tn) * TB];
       }
+#endif
     };
     int p = 0;
     for (; p + 1 < H; p += 2) {
+      gen(p);
       prod(p, eA1, eA2);
       prod(p + 1, eB1, eB2);
     }
-    if (p < H) prod(p, eA1, eA2);
+    if (p < H) {
+      gen(p);
+      prod(p, eA1, eA2);
+    }
   } else if (role == ROLE_WHEEL) {
     // ---------------- wheel contacts of the even steps (the slope critic reads lw / rw at i,
     // i + 2 for even i, critics_warp.py:220-267) and the slope critic.  Contact sets A / B
@@ -1967,11 +2001,13 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
     cost_lds[tj] = valid ? cost : INFINITY;
   }
   __syncthreads();
-  if constexpr (MODE == 0)  // rows hold the normals; the leaf recomputes the sampled controls
-    leaf_records<TB, NT, true, FUSED>(a, cost_lds, scratch, a.eps + (size_t)blk * (2 * H) * TB, unom_lds,
-                                      ucache, a.ucache_steps, blk);
+  if constexpr (MODE == 0)  // the first steps' sampled controls in LDS, the rest in HBM rows (the
+                            // sampled controls, or the normals: the leaf recomputes the controls)
+    leaf_records<TB, NT, !MPPI_NOISE_REG, FUSED>(a, cost_lds, scratch,
+                                                 (MPPI_NOISE_REG ? a.ustore : a.eps) + (size_t)blk * (2 * H) * TB,
+                                                 unom_lds, ucache, a.ucache_steps, blk);
   else
-    leaf_records<TB, NT, false, FUSED>(a, cost_lds, scratch, a.ustore + (size_t)blk * (2 * H) * TB, nullptr, nullptr,
+    leaf_records<TB, NT, false, FUSED>(a, cost_lds, scratch, a.ustore + (size_t)blk * (2 * H) * TB, unom_lds, ucache,
                                        0, blk);
   if (clk_wg) a.clk[6] = __builtin_amdgcn_s_memrealtime();  // workgroup 0's leaf record written
   if (clk_any) a.clk[kClkBase + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -2869,8 +2905,9 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       unsigned long long w = __hip_atomic_load(f.uopt + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       while ((unsigned)(w >> 32) != f.seq) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 >= kColfinPollTicks) {
-          late = 1;
+        if (__builtin_amdgcn_s_memrealtime() - t0 >= kColfinPollTicks ||
+            (f.abort && __hip_atomic_load(f.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == f.seq)) {
+          late = 1;  // (or another finish workgroup of the server gave up: its slice never comes)
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -3647,31 +3684,42 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
     if (tid < 64) {
       // the head polls the pinned command (seq and stop in one 8-byte read) and relays it: the
       // command words to relay[16..], then (after they completed) seq / stop to relay[0..1]; the
-      // others poll relay[0..1] in device memory.  An idle head relays a stop.  The relay's stop
-      // word is this launch's first seq (a stale one from an earlier launch never matches), so the
-      // host launches without resetting the relay.
+      // others poll relay[0..1] in device memory.  An idle head relays a stop.  Stop words are this
+      // launch's launch_id (a stale one from an earlier launch never matches), so the host launches
+      // without resetting the relay or the command's stop word.
       const unsigned long long* src = head ? reinterpret_cast<const unsigned long long*>(z.cmd)
                                            : reinterpret_cast<const unsigned long long*>(z.relay);
       // Only the head leaves on its own (idle limit, or the exit_after test hook); the others leave
       // on the stop it relays.  So an exit is all-or-nothing: either every workgroup serves a command
       // or none does, and a command the head never relayed leaves no trace of the step (the host sees
       // the launch retire without a completion word and relaunches the server with that command).
+      // The host's stop is read before seq (a stop posted before a later launch's command ends this
+      // launch first), and the others also read it themselves every ~100 us: after a finish that gave
+      // up no workgroup holds the last ticket, so there is no head to relay it.
       unsigned ok = 0;
       if (tid == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint64_t t_stop = t0;
         if (head && z.clk) z.clk[kClkServer + 8 * (expect & 7) + 6] = t0;
         const bool forced = head && z.exit_after != 0 && expect - z.first_seq >= z.exit_after;
         while (!forced) {
           const unsigned long long w = head ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                             : __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(w >> 32) == z.launch_id) break;
           if ((int)((unsigned)w - expect) >= 0) {
             ok = 1;
             break;
           }
-          if (head ? ((w >> 32) != 0 || __builtin_amdgcn_s_memrealtime() - t0 >= z.idle_ticks)
-                   : (unsigned)(w >> 32) == z.first_seq)
-            break;
-          if (!head) __builtin_amdgcn_s_sleep(2);  // (~0.06 us; 8: server rollout +0.4 us, its start spread)
+          const uint64_t now = __builtin_amdgcn_s_memrealtime();
+          if (head) {
+            if (now - t0 >= z.idle_ticks) break;
+          } else {
+            if (now - t_stop >= 10000) {
+              t_stop = now;
+              if (__hip_atomic_load(&z.cmd->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == z.launch_id) break;
+            }
+            __builtin_amdgcn_s_sleep(2);  // (~0.06 us; 8: server rollout +0.4 us, its start spread)
+          }
         }
       }
       ok = __builtin_amdgcn_readfirstlane(ok);
@@ -3693,7 +3741,7 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
           if (ok)
             __hip_atomic_store(z.relay, cmd_lds[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           else
-            __hip_atomic_store(z.relay + 1, z.first_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(z.relay + 1, z.launch_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       if (tid == 0) cmd_lds[31] = ok;
@@ -3733,6 +3781,7 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
     const int nslot = __builtin_amdgcn_readfirstlane(c.noise_slot);
     const uint64_t nbase = ((uint64_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_hi) << 32) |
                            (uint32_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_lo);
+    if (MPPI_NOISE_REG) a.n_base = nbase;  // (this step's normals, generated by the producer waves)
     // the normals of step + 2 (when commanded): W wave-units (one Philox block of 64 trajectories
     // each) in S static shares, two per workgroup outside the finish (ticket t: shares 2t, 2t + 1,
     // from its record on) and one per finish workgroup but the last (blk: share 2 nn + blk, after
@@ -3763,12 +3812,17 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         int late = z.wait_ticks == 0;  // 0: give up at once (the test hook of mppi_set_option)
         while (!late && __hip_atomic_load(z.rec_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)z.nroll) {
-          if (__builtin_amdgcn_s_memrealtime() - t0 >= z.wait_ticks) {
+          // (another finish workgroup gave up on this step: the step has failed, stop waiting)
+          if (__builtin_amdgcn_s_memrealtime() - t0 >= z.wait_ticks ||
+              __hip_atomic_load(z.f.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == seq) {
             late = 1;
             break;
           }
           __builtin_amdgcn_s_sleep(2);
         }
+        // the step fails: the last finish workgroup's u_opt poll and the other finish workgroups still
+        // waiting stop on this word instead of their own bounds
+        if (late) __hip_atomic_store(z.f.abort, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sh[1] = late;
       }
       __syncthreads();
@@ -3848,6 +3902,20 @@ __global__ __launch_bounds__(256) void mppi_cdiv_verify_kernel(float b, float y,
   const float q = cdiv_f(a, b, y);
   const float ref = a / b;
   if (__builtin_bit_cast(unsigned, q) != __builtin_bit_cast(unsigned, ref)) atomicAdd(bad, 1u);
+}
+
+// Test hook (mppi_debug_hold): workgroups that each hold `lds` bytes of a CU's LDS for `ticks` of the
+// 100 MHz clock, i.e. another stream's kernels occupying CUs when a step is posted.  Time-bounded.
+__global__ __launch_bounds__(64) void mppi_hold_kernel(uint64_t ticks) {
+  extern __shared__ unsigned char hold_lds[];
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  hold_lds[threadIdx.x] = 0;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(64);
+}
+
+hipError_t launch_hold(int groups, size_t lds, uint64_t ticks, hipStream_t st) {
+  hipLaunchKernelGGL(mppi_hold_kernel, dim3((unsigned)groups), dim3(64), lds, st, ticks);
+  return hipGetLastError();
 }
 
 hipError_t launch_cdiv_verify(float b, float y, unsigned* bad, hipStream_t st) {

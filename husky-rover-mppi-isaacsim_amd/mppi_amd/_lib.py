@@ -102,6 +102,7 @@ _PROTOS = {
                                    C.c_void_p, C.c_void_p]),
     "mppi_bilinear_tiled": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mppi_sync": (C.c_int, [C.c_void_p]),
+    "mppi_debug_hold": (C.c_int, [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
     "mppi_build_costmap": (C.c_int, [C.c_void_p, _DP, C.c_int32, C.c_int32, C.c_double, C.c_double,
                                      C.c_double, C.c_double, C.c_int32, _FP, C.c_int32]),
     "mppi_costmap_builder_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
@@ -469,11 +470,12 @@ class Engine:
         return t.value, n.value
 
     def launch_info(self):
-        info = (C.c_int64 * 16)()
-        self._c(self.lib.mppi_get_launch_info(self.ctx, info, 16), "mppi_get_launch_info")
+        info = (C.c_int64 * 18)()
+        self._c(self.lib.mppi_get_launch_info(self.ctx, info, 18), "mppi_get_launch_info")
         keys = ("reserved", "block", "blocks", "window_cols", "window_rows", "lds_bytes", "finish_kind",
                 "finish_records", "finish_ncol", "finish_groups", "ucache_steps", "resident",
-                "server_launches", "server_steps", "server_failed_steps", "server_relaunches")
+                "server_launches", "server_steps", "server_failed_steps", "server_relaunches",
+                "server_fallbacks", "cadence_steps")
         return dict(zip(keys, [int(v) for v in info]))
 
     def server_time(self):
@@ -517,6 +519,14 @@ class Engine:
     def bilinear_query(self, x_ptr, y_ptr, h_ptr, n):
         self._c(self.lib.mppi_bilinear_query(self.ctx, C.c_void_p(int(x_ptr)), C.c_void_p(int(y_ptr)),
                                              C.c_void_p(int(h_ptr)), int(n)), "mppi_bilinear_query")
+
+
+def debug_hold(device, stream_handle, groups, lds_bytes, microseconds):
+    """mppi_debug_hold (test hook): `groups` workgroups holding lds_bytes of LDS each for `microseconds`
+    on the given stream (another stream's kernels occupying CUs when a step is posted)."""
+    lib = load_library()
+    _check(lib, lib.mppi_debug_hold(int(device), C.c_void_p(stream_handle or None), int(groups), int(lds_bytes),
+                                    int(microseconds)), "mppi_debug_hold")
 
 
 class Group:

@@ -281,27 +281,32 @@ int mppi_dump_rollouts(mppi_ctx* ctx, float* traj, float* heading, float* left_w
 int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
 
 /* Per-context options and test hooks, by name (MPPI_EINVAL for an unknown name):
- *   "resident"           1 (default; env MPPI_RESIDENT=0 turns it off) / 0: sampled steps of
- *                        the role-split plan (K <= 256 x CUs, records that fit the in-kernel
- *                        finish: C1-C3) run on the resident step server, one launch that stays
- *                        on the GPU across steps and polls a command block in pinned memory
- *                        (mppi_step_server_kernel): no launch and no kernel boundary on a
- *                        step's path.  It leaves after "resident_idle_us" without a step (a
- *                        step posted as it leaves is served by a relaunch, launch_info[15]), and
- *                        every call on the context other than mppi_step / mppi_set_state /
- *                        mppi_get_outputs / mppi_get_timing stops it first.  While it is
- *                        resident it holds one workgroup slot and ~154 KB of LDS on every CU:
- *                        other kernels on the device get the rest of each CU.  Results are
- *                        bitwise those of the separate launches (0).
- *   "resident_idle_us"   the server's idle limit, microseconds (default 200, [100, 1e6]): back-
- *                        to-back steps keep it resident; at a simulator's frame cadence it leaves
- *                        soon after each step and relaunches on the next.
+ *   "resident"           sampled steps of the role-split plan (K <= 256 x CUs, records that fit
+ *                        the in-kernel finish: C1-C3) on the resident step server, one launch that
+ *                        stays on the GPU across steps and polls a command block in pinned memory
+ *                        (mppi_step_server_kernel): no launch and no kernel boundary on a step's
+ *                        path.  1 (default): for back-to-back calls only, i.e. a call within half
+ *                        "resident_idle_us" of the last step's return keeps or starts it, and a
+ *                        call after a longer gap (a simulator's frame: VERDICT r05 item 3, the
+ *                        server's launch per frame cost more than the launches it saves) runs as
+ *                        separate launches (launch_info[17]) and lets a running server go; 2: every
+ *                        step whose plan fits; 0: never (env MPPI_RESIDENT=0/1/2 sets the default).
+ *                        The server leaves after "resident_idle_us" without a step (a step posted
+ *                        as it leaves is served by a relaunch, launch_info[15]), and every call on
+ *                        the context other than mppi_step / mppi_set_state / mppi_get_outputs /
+ *                        mppi_get_timing stops it first.  While it is resident it holds one
+ *                        workgroup slot and ~154 KB of LDS on every CU: other kernels on the device
+ *                        get the rest of each CU.  Results are bitwise those of separate launches.
+ *   "resident_idle_us"   the server's idle limit, microseconds (default 200, [100, 1e6]).
  *   "finish_wait_ticks"  bound, in ticks of the 100 MHz s_memrealtime clock, on how long a
  *                        finish workgroup of the server waits for the step's rollout records
- *                        (default 2e8 = 2 s).  A finish that gives up publishes the failure:
- *                        the step returns MPPI_EHIP, the server is stopped and the counters
- *                        re-armed, so the next step is correct (0: give up at once, the test
- *                        hook).
+ *                        (default 1e5 = 1 ms: a running server's records arrive within microseconds
+ *                        of each other; a fresh launch beside another stream's kernels that hold some
+ *                        CUs has workgroups that cannot start).  A finish that gives up publishes
+ *                        the failure; the host stops the server, waits for it to retire, re-arms
+ *                        its counters and runs the step again as separate launches (same
+ *                        results, launch_info[16]; 0: give up at once, the test hook).  A server
+ *                        that does not retire within 10 s of its stop fails the call (MPPI_EHIP).
  *   "record_tree_finish" 1: the record-tree finish (mppi_finish_kernel) at every record count
  *                        (default 0: the column-split finish wherever its shape fits).
  *   "server_exit_after"  test hook: the next server launch leaves at its poll after serving this
@@ -312,7 +317,7 @@ int mppi_get_timing(mppi_ctx* ctx, double* rollout_ms, double* finish_ms, int64_
 /* HIP-event time of the deferred optimal-rollout kernels (side stream). */
 int mppi_get_tail_timing(mppi_ctx* ctx, double* tail_ms, int64_t* launches);
 
-/* Layout/launch facts for the last step (for tests and the bench), up to 16 values:
+/* Layout/launch facts for the last step (for tests and the bench):
  * info[0]=0 (reserved), [1]=rollout block threads, [2]=rollout blocks, [3]/[4]=cols/rows of
  * the DEM window the step's lanes can touch, [5]=rollout LDS bytes, [6]=finish kind (1 =
  * column-split mppi_colfin_kernel, 0 = record tree mppi_finish_kernel), [7]=records padded
@@ -320,7 +325,9 @@ int mppi_get_tail_timing(mppi_ctx* ctx, double* tail_ms, int64_t* launches);
  * [10]=steps whose sampled controls the rollout keeps in LDS, [11]=1 if the step ran on the
  * resident step server (mppi_step_server_kernel), else 0; [12]/[13]/[14] = server launches /
  * steps served / failed steps so far (mppi_set_option "resident"); [15] = commands posted to a
- * server that was leaving on its idle limit and served by a relaunch (included in [12]). */
+ * server that was leaving on its idle limit and served by a relaunch (included in [12]); [16] =
+ * failed server steps rerun as separate launches; [17] = steps the server could have run that ran as
+ * separate launches because the call was not back-to-back ("resident" 1).  Up to 18 values. */
 int mppi_get_launch_info(mppi_ctx* ctx, int64_t* info, int32_t n);
 
 /* Shader clock of the last sampled 3D rollout, from the chain wave of trajectories 0..63
@@ -360,6 +367,12 @@ int mppi_bilinear_tiled(mppi_ctx* ctx, const float* xs_dev, const float* ys_dev,
                         const int32_t* tile_off_dev, float* h_dev);
 /* Wait for all work enqueued on the context stream. */
 int mppi_sync(mppi_ctx* ctx);
+
+/* Test hook: enqueue on `stream` (a hipStream_t of `device`; NULL = its null stream) `groups`
+ * workgroups that each hold lds_bytes (<= 160 KiB) of a CU's LDS for `microseconds` (<= 1 s) and do
+ * nothing else: another stream's kernels occupying CUs when a step is posted (the simulator's, in
+ * the reference's loop, visual_terrain_stack_full_terrain.py:466-541).  Asynchronous. */
+int mppi_debug_hold(int32_t device, void* stream, int32_t groups, int32_t lds_bytes, int32_t microseconds);
 
 /* ---- reference-integrator mode "python25d"  ----
  * generate_trajectory_25D of thesis_master/python_mppi_projection/debug.py:312-364,

@@ -38,7 +38,9 @@ def _engine(K, H, env=None, opts=None, async_tail=False):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-    for k, v in (opts or {}).items():
+    # (the server tests run it on every step, "resident" 2: with the default 1 a host gap between
+    # steps longer than half the idle limit runs a step as separate launches, test_cadence_policy)
+    for k, v in dict({"resident": 2}, **(opts or {})).items():
         eng.set_option(k, v)
     Z, hw, cm = scene.scene_c3()
     eng.set_dem(Z, hw)
@@ -112,7 +114,8 @@ def test_server_closed_loop_states(async_tail):
     optimal rollout: the server equals the separate launches in every output, incl. the *_sim rows."""
     i_got = {}
     ref = _run(65536, 24, opts={"resident": 0}, steps=5, async_tail=async_tail, states=True)
-    got = _run(65536, 24, steps=5, async_tail=async_tail, states=True, info=i_got)
+    # (an idle limit far above this loop's host work between steps: one launch serves all five)
+    got = _run(65536, 24, opts={"resident_idle_us": 5000}, steps=5, async_tail=async_tail, states=True, info=i_got)
     _same(got, ref, f"closed loop async={async_tail}")
     assert i_got["resident"] == 1 and i_got["server_launches"] == 1 and i_got["server_steps"] == 5, i_got
 
@@ -192,7 +195,7 @@ def test_column_split_finish_at_4096_records(K, H):
     _same(got, ref, "4096 records")
 
 
-@pytest.mark.parametrize("resident", [0, 1], ids=["separate", "server"])
+@pytest.mark.parametrize("resident", [0, 1, 2], ids=["separate", "cadence", "server"])
 def test_step_counter_jumps(resident):
     """Step counters that skip and repeat (normals generated out of order, slots reused) give the
     same results on the server and on separate launches of either rollout kernel."""
@@ -227,31 +230,112 @@ def test_timing_modes():
         eng.close()
 
 
-def test_server_finish_gives_up_then_recovers():
+def test_server_finish_gives_up_then_falls_back():
     """A server finish that stops waiting for the records (mppi_set_option("finish_wait_ticks", 0):
-    give up at once) publishes the failure: the step raises, the host stops the server and re-arms
-    the record and handoff counters, and the next steps are bitwise equal to a fresh context's (the
-    nominal controls were not touched by the failed step)."""
-    eng, ref = _engine(65536, 24, async_tail=True), _engine(65536, 24, async_tail=True)
+    give up at once) publishes the failure: the host stops the server, waits for it to retire,
+    re-arms the record and handoff counters and runs the step again as separate launches, so the
+    call returns the same outputs as a fresh context (counted in launch_info["server_fallbacks"]);
+    with the bound restored the next steps run on the server again, still bitwise equal."""
+    eng, ref = _engine(65536, 24, async_tail=True), _engine(65536, 24, opts={"resident": 0}, async_tail=True)
     try:
         eng.set_option("finish_wait_ticks", 0)
-        with pytest.raises(RuntimeError, match="gave up"):
-            eng.step("3d", 0)
-        info = eng.launch_info()
-        assert info["resident"] == 1 and info["server_failed_steps"] == 1, info
-        eng.set_option("finish_wait_ticks", 200000000)
-        for i in (1, 2):
+        for i in range(4):
+            if i == 2:
+                eng.set_option("finish_wait_ticks", 200000000)
             eng.step("3d", i, copy=False)
             ref.step("3d", i, copy=False)
             a, b = eng.outputs(), ref.outputs()
             for k in ALL:
                 np.testing.assert_array_equal(a[k], b[k], err_msg=f"step {i} {k}")
+            info = eng.launch_info()
+            assert info["resident"] == (1 if i >= 2 else 0), (i, info)
+        assert info["server_failed_steps"] == 2 and info["server_fallbacks"] == 2, info
+        assert info["server_steps"] == 4, info
         np.testing.assert_array_equal(eng.costs(), ref.costs())
         with pytest.raises(RuntimeError, match="unknown option"):
             eng.set_option("no_such_option", 1)
+        with pytest.raises(RuntimeError, match="resident must be"):
+            eng.set_option("resident", 3)
     finally:
         eng.close()
         ref.close()
+
+
+def test_cadence_policy():
+    """"resident" 1 (the default): back-to-back calls run on the server, a call more than half the idle
+    limit after the last step returned (a simulator frame) runs as separate launches and lets the server
+    go (launch_info["cadence_steps"]).  Every step equals the separate launches."""
+    ref = _run(65536, 24, opts={"resident": 0}, steps=8, async_tail=True, states=True)
+    # (an idle limit of 1 ms: half of it leaves room for this loop's host work between calls)
+    eng = _engine(65536, 24, opts={"resident": 1, "resident_idle_us": 1000}, async_tail=True)
+    outs, sched = [], []
+    try:
+        for i in range(8):
+            if i in (3, 6):
+                time.sleep(0.005)  # a frame gap (10x half the idle limit)
+            eng.set_state(_state(i))
+            eng.step("3d", i, copy=False)
+            sched.append(eng.launch_info()["resident"])
+            o = eng.outputs()
+            outs.append({k: o[k].copy() for k in ALL})
+        info = eng.launch_info()
+        costs = eng.costs()
+    finally:
+        eng.close()
+    _same((outs, costs), ref, "cadence policy")
+    # step 0 has no previous return; 3 and 6 follow a frame gap; the others are back to back
+    assert sched == [0, 1, 1, 0, 1, 1, 0, 1], sched
+    assert info["cadence_steps"] == 8 - sum(sched) and info["server_failed_steps"] == 0, info
+
+
+def _hold(groups, lds, us):
+    """Another stream's kernels holding CUs: `groups` workgroups with `lds` bytes of LDS each for `us`."""
+    import torch
+    from mppi_amd import _lib
+    s = torch.cuda.Stream()
+    _lib.debug_hold(0, s.cuda_stream, groups, lds, us)
+    return s
+
+
+def test_step_posted_under_cu_contention():
+    """a step posted while another stream's kernels hold CUs.  (a) Every CU holds a
+    96 KiB workgroup for 10 ms when the server is launched: none of its workgroups fits until they
+    leave (nothing of the server runs, so nothing waits), and the step completes late on the server,
+    bitwise equal.  (b) 16 CUs are held for 10 ms and the finish waits at most 0.5 ms for the records:
+    16 of the server's workgroups cannot start (the others hold their CUs, polling for the next step),
+    its finish gives up, the host stops the server (the late workgroups then run on the CUs the others
+    left and it retires) and reruns the step as separate launches: no exception, bitwise equal, counted
+    in launch_info["server_fallbacks"], in about the wait bound instead of the 10 ms hold."""
+    import torch
+    ref = _run(65536, 100, opts={"resident": 0}, steps=4, async_tail=True, states=True)
+    eng = _engine(65536, 100, opts={"finish_wait_ticks": 50000}, async_tail=True)   # 0.5 ms
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    outs, lat = [], []
+    try:
+        for i in range(4):
+            eng.set_state(_state(i))
+            if i in (1, 3):
+                eng.sync()  # the server leaves: the next step launches one beside the holders
+                _hold(cus if i == 1 else 16, 96 * 1024, 10000)
+                time.sleep(0.001)  # the holders are resident before the server's launch
+            t0 = time.perf_counter()
+            eng.step("3d", i, copy=False)
+            lat.append(time.perf_counter() - t0)
+            o = eng.outputs()
+            outs.append({k: o[k].copy() for k in ALL})
+            if i == 1:
+                info1 = eng.launch_info()
+        info = eng.launch_info()
+        costs = eng.costs()
+        torch.cuda.synchronize()
+    finally:
+        eng.close()
+    _same((outs, costs), ref, "contention")
+    print(f"step latency ms: {[round(x * 1e3, 3) for x in lat]}; {info}")
+    assert info1["resident"] == 1 and info1["server_fallbacks"] == 0, info1   # (a) late, on the server
+    assert info["server_fallbacks"] == 1 and info["server_failed_steps"] == 1, info   # (b)
+    assert lat[1] > 0.004, lat                      # (a) waited for the held CUs
+    assert 0.0005 < lat[3] < 0.005, lat             # (b) the wait bound, the server's exit, the rerun
 
 
 @pytest.mark.parametrize("trace", [False, True], ids=["plain", "host-trace"])

@@ -63,18 +63,33 @@ def run_schedule(n, H, opts, gaps, read):
     return outs, info
 
 
-def test_server_mixed_cadence_equals_separate_launches():
+@pytest.fixture(scope="module")
+def soak_ref():
+    n, H = 1500, 24
+    gaps, read = _schedule(n)
+    ref, rinfo = run_schedule(n, H, {"resident": 0}, gaps, read)
+    assert rinfo["server_steps"] == 0, rinfo
+    return n, H, gaps, read, ref
+
+
+@pytest.mark.parametrize("resident", [2, 1], ids=["server-always", "cadence"])
+def test_server_mixed_cadence_equals_separate_launches(resident, soak_ref):
+    """resident 2: every step on the server (relaunched after gaps past the idle limit); 1 (default):
+    the steps after gaps longer than half the idle limit as separate launches, the others on the
+    server, switching both ways hundreds of times."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
-    n, H = 1500, 24
-    gaps, read = _schedule(n)
-    got, info = run_schedule(n, H, {}, gaps, read)
-    ref, rinfo = run_schedule(n, H, {"resident": 0}, gaps, read)
-    assert rinfo["server_steps"] == 0, rinfo
+    n, H, gaps, read, ref = soak_ref
+    got, info = run_schedule(n, H, {"resident": resident}, gaps, read)
     for i, (a, b) in enumerate(zip(got, ref)):
         for k in a:
             np.testing.assert_array_equal(a[k], b[k], err_msg=f"step {i} {k}")
-    assert info["server_failed_steps"] == 0 and info["server_steps"] == n, info
+    assert info["server_failed_steps"] == 0 and info["server_fallbacks"] == 0, info
     # gaps past the idle limit end the server; the next step relaunches it
     assert info["server_launches"] > 1, info
+    if resident == 2:
+        assert info["server_steps"] == n and info["cadence_steps"] == 0, info
+    else:
+        assert info["server_steps"] + info["cadence_steps"] == n, info
+        assert info["server_steps"] > n // 4 and info["cadence_steps"] > n // 4, info

@@ -76,3 +76,21 @@ def test_missing_library_fails_loudly(tmp_path):
     from mppi_amd import _lib
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _lib.load_library(str(tmp_path / "libmppi_hip.so"))
+
+
+def test_null_context_calls_are_refused(libpath):
+    """Entry points called with a null context or out-of-range arguments return MPPI_EINVAL (-1) before
+    touching any device (round-5 advisor: mppi_step(NULL) used to dereference the context)."""
+    from mppi_amd import _lib
+    lib = _lib.load_library(libpath)
+    out = _lib.MppiOutputs()
+    assert lib.mppi_step(None, 3, 0, ctypes.byref(out)) != 0
+    assert b"null" in lib.mppi_last_error()
+    u = (ctypes.c_float * 4)()
+    assert lib.mppi_step_injected(None, 3, u, u, ctypes.byref(out)) != 0
+    assert lib.mppi_set_option(None, b"resident", 1) != 0
+    assert lib.mppi_group_step(None, 3, 0, ctypes.byref(out)) != 0
+    assert lib.mppi_sync(None) != 0
+    assert lib.mppi_debug_hold(0, None, 0, 1024, 10) != 0        # no workgroups
+    assert lib.mppi_debug_hold(0, None, 1, 1 << 20, 10) != 0     # more LDS than a CU has
+    assert lib.mppi_debug_hold(0, None, 1, 1024, 2_000_000) != 0  # longer than 1 s
