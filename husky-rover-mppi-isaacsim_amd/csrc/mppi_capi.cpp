@@ -810,14 +810,14 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
   if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
   int rc = ensure_nodes(c, pl.blocks);
   if (rc) return rc;
-  if (mode == 1 || MPPI_NOISE_REG) {  // injected / sampled controls the leaf reads back from HBM
+  if (mode == 1) {  // injected controls: the leaf reads them back from here
     rc = grow(c->ustore, c->ustore_cap, (size_t)pl.blocks * pl.traj_per_block * 2 * H_of(c) * sizeof(float), c->stream);
     if (rc) return rc;
   }
   RolloutArgs a;
   fill_rollout(c, pl, st, step, unom, a);
   int eps_slot = -1;
-  if (mode == 0 && pl.blocks > 0 && !MPPI_NOISE_REG) {
+  if (mode == 0 && pl.blocks > 0) {
     rc = eps_for_step(c, pl, step, c->stream, false, &eps_slot);
     if (rc) return rc;
     a.eps = c->eps[eps_slot];
@@ -1067,15 +1067,12 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   if (c->srv_running && proj != c->srv_proj) post_stop(c);  // (the next launch queues behind it)
   // (first step: the buffers are allocated before the server holds pointers to them)
   int rc = MPPI_OK;
-  const size_t rows = (size_t)pl.blocks * 2 * H_of(c) * 256;
-  if (c->nodes_cap < (size_t)pl.blocks * E_of(c) || (MPPI_NOISE_REG ? c->ustore_cap < rows * sizeof(float) : c->eps_cap < rows))
+  if (c->nodes_cap < (size_t)pl.blocks * E_of(c) || c->eps_cap < (size_t)pl.blocks * 2 * H_of(c) * 256)
     rc = quiesce(c);
   if (!rc) rc = ensure_nodes(c, pl.blocks);
-  if (!rc && MPPI_NOISE_REG) rc = grow(c->ustore, c->ustore_cap, rows * sizeof(float), c->stream);
   if (rc) return rc;
   int slot = 0, noise_slot = -1;
   const uint64_t nb = (uint64_t)((H_of(c) + 1) / 2);  // Philox blocks per trajectory and step
-#if !MPPI_NOISE_REG
   // a step whose normals no slot holds (first step, a jump of the step counter): the server may still
   // be writing normals of a later step in its last noise phase, so it is stopped before any slot is
   // regenerated
@@ -1112,7 +1109,6 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
     }
     c->eps_step[v] = (int64_t)target;
   }
-#endif
   const int par = ((c->tail_deferred ? c->tail_def_par : c->tail_par) + 1) % kTailSlots;
   if (c->async_tail && c->tail_inflight[par]) {  // the tail of kTailSlots steps ago: long done
     HIP_TRY(hipEventSynchronize(c->ev_tail[par]));
@@ -1132,8 +1128,7 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
   d.mode = c->async_tail ? 2 : 1;
   d.noise_slot = noise_slot;
   c->srv_cmd_noise = noise_slot;
-  // (MPPI_NOISE_REG: the Philox base of this step's normals, which the producer waves generate)
-  const uint64_t nbase = (MPPI_NOISE_REG ? step : step + 2) * nb;
+  const uint64_t nbase = (step + 2) * nb;
   d.noise_n_base_lo = (unsigned)nbase;
   d.noise_n_base_hi = (unsigned)(nbase >> 32);
   // a server idle for more than half its limit (since its last step completed) may be leaving: stop

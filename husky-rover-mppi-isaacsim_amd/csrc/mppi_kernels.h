@@ -4,13 +4,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// MPPI_NOISE_REG 1: the rollout's producer generates each step's sampling normals in registers
-// (Philox, sampling_warp.py:73-90) and keeps the sampled controls the LDS cache cannot hold in
-// ustore for the leaf; 0: the normals precomputed by mppi_noise_kernel into HBM rows (round 1-5)
-#ifndef MPPI_NOISE_REG
-#define MPPI_NOISE_REG 1
-#endif
-
 namespace mppi {
 
 // The resident step server's command block (mppi_capi.cpp "resident step server"): pinned host

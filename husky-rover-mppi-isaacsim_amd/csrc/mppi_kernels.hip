@@ -863,8 +863,8 @@ constexpr int UCACHE_ROW = 256 + 4;
 template <int TB, int NT, bool EPS = false, bool WT = false>
 __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* cost_lds,
                                              unsigned char* scratch, const float* ub_block,
-                                             const float* unom, const float* ucache, int uc_steps,
-                                             int blk = -1);
+                                             const float* unom = nullptr, const float* ucache = nullptr,
+                                             int uc_steps = 0, int blk = -1);
 
 // =====================================================================  leaf records (shared)
 // Softmax leaf records (DEFINED replacement of critics_warp.py:338-376) for the
@@ -940,20 +940,20 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
       const int tr0 = 256 * leaf + 128 * half + 32 * line;  // first trajectory of the line
       w4r[q] = reinterpret_cast<const float4*>(wbuf + tr0);
       const float4* u4 = reinterpret_cast<const float4*>(ub_block + (size_t)(j >= 2 ? j - 2 : 0) * TB + tr0);
-      bool cached = false;  // the sampled controls of this row are in LDS (no HBM row read)
+      bool cached = false;  // the sampled controls of this row are in LDS (no normals re-read)
       float nom = 0.f, sg = 0.f, lo = 0.f, hi = 0.f;
-      const int c = (j - 2) >= H ? 1 : 0;
-      const int t = max(j - 2, 0) - c * H;
       if constexpr (EPS) {  // rows hold the normals: u = clamp(u_nom[t+1] + sigma*eps) as sampled
+        const int c = (j - 2) >= H ? 1 : 0;
+        const int t = max(j - 2, 0) - c * H;
         const int ti = min(t + 1, H - 1);
         nom = unom[c * H + ti];
         sg = c ? a.s2 : a.s1;
         lo = c ? a.min_u2 : a.min_u1;
         hi = c ? a.max_u2 : a.max_u1;
-      }
-      if (j >= 2 && t < uc_steps) {
-        cached = true;
-        u4 = reinterpret_cast<const float4*>(ucache + (size_t)(c * uc_steps + t) * UCACHE_ROW + tr0);
+        if (j >= 2 && t < uc_steps) {
+          cached = true;
+          u4 = reinterpret_cast<const float4*>(ucache + (size_t)(c * uc_steps + t) * UCACHE_ROW + tr0);
+        }
       }
       cached_r[q] = cached;
       nom_r[q] = nom;
@@ -1304,17 +1304,15 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   // ---------------- per-role state
   Traj s;                       // chain
   float L = a.wl, R = a.wr;     // side: filter
-  float en1 = 0.f, en2 = 0.f;
-#if !MPPI_NOISE_REG
   // side, MODE 0: this trajectory's normals, rows [2][H] of 256 (mppi_noise_kernel)
   const float* eps_row = (MODE == 0) ? a.eps + (size_t)blockIdx.x * (2 * H) * TB + tj : nullptr;
+  float en1 = 0.f, en2 = 0.f;
   if constexpr (MODE == 0) {
     if (side) {
       en1 = eps_row[0];
       en2 = eps_row[(size_t)H * TB];
     }
   }
-#endif
   float pf_sum = 0.f, sw = 0.f, sp = 0.f, ob = 0.f, last_x = a.x0, last_y = a.y0;
   float lwx = 0.f, lwy = 0.f, lwz = 0.f, rwx = 0.f, rwy = 0.f, rwz = 0.f;
   float* ust = a.ustore + (size_t)blockIdx.x * (2 * H) * TB + tj;
@@ -1412,15 +1410,11 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
     //    DUMP), used one half later.
     int seen_chain = 0;                                 // last acquired value of f_chain
     float eA1 = en1, eA2 = en2, eB1 = 0.f, eB2 = 0.f;  // normals of the even / odd step
-#if MPPI_NOISE_REG
-    const uint64_t kg = (uint64_t)(a.k_offset + (int64_t)blockIdx.x * TB + tj);
-#else
     if constexpr (MODE == 0) {
       const int t1 = min(1, H - 1);
       eB1 = eps_row[(size_t)t1 * TB];
       eB2 = eps_row[(size_t)(H + t1) * TB];
     }
-#endif
     float cmA = 0.f, cmB = 0.f;                        // costmap value of the even / odd step
     float elx = 0.f, ely = 0.f, elz = 0.f, erx = 0.f, ery = 0.f, erz = 0.f;  // even step's contacts
     // PROD / CONS: the half produces step p / consumes step sc = p - PAIR_LAG for sure
@@ -1434,19 +1428,12 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
       if (PROD || (GUARD && p < H)) {  // sampling, filter (sampling_warp.py:54-138); normals precomputed
         float u1, u2;
         if constexpr (MODE == 0) {
-#if MPPI_NOISE_REG
-          // Philox block n_base + p / 2: the normals of steps p and p + 1 (the even half)
-          if constexpr (!ODD) noise_block_pk(a.seed, a.n_base + (uint64_t)(p >> 1), kg, &eA1, &eA2, &eB1, &eB2);
-#endif
           const int ti = min(p + 1, H - 1);
           u1 = clampf(unom_lds[ti] + a.s1 * e1r, a.min_u1, a.max_u1);
           u2 = clampf(unom_lds[H + ti] + a.s2 * e2r, a.min_u2, a.max_u2);
           if (p < a.ucache_steps) {  // kept for the leaf reduction (uniform branch)
             ucache[(size_t)p * UCACHE_ROW + tj] = u1;
             ucache[(size_t)(a.ucache_steps + p) * UCACHE_ROW + tj] = u2;
-          } else if (MPPI_NOISE_REG) {  // the rest in HBM (the leaf reads them back)
-            ust[(size_t)p * TB] = u1;
-            ust[(size_t)(H + p) * TB] = u2;
           }
         } else {
           const size_t o = (size_t)(valid ? kl : 0) * H + p;
@@ -1538,13 +1525,11 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
         }
         lds_store_release(f_cons, sc + 1);
       }
-#if !MPPI_NOISE_REG
       if constexpr (MODE == 0) {  // prefetch the normals of step p + 2 into the registers just freed
         const int tn = min(p + 2, H - 1);
         e1r = eps_row[(size_t)tn * TB];
         e2r = eps_row[(size_t)(H + tn) * TB];
       }
-#endif
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
@@ -1589,12 +1574,11 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   }
 #endif
   __syncthreads();
-  if constexpr (MODE == 0)  // (as the role-split kernel's)
-    leaf_records<TB, NT, !MPPI_NOISE_REG>(a, cost_lds, scratch,
-                                          (MPPI_NOISE_REG ? a.ustore : a.eps) + (size_t)blockIdx.x * (2 * H) * TB,
-                                          unom_lds, ucache, a.ucache_steps);
+  if constexpr (MODE == 0)  // rows hold the normals; the leaf recomputes the sampled controls
+    leaf_records<TB, NT, true>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB, unom_lds, ucache,
+                               a.ucache_steps);
   else
-    leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB, unom_lds, ucache, 0);
+    leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
 #ifdef MPPI_STAMPS
   const uint64_t k_t2 = dbg_stamp(), k_r2 = __builtin_amdgcn_s_memrealtime();
   if ((tid & 63) == 0 && blockIdx.x < 64) {
@@ -1778,18 +1762,11 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
   else if (role == ROLE_PROD) {
     // ---------------- sampling + wheel filter + sin/cos, normals prefetched two steps ahead
     // (even / odd steps in their own registers: no loop-carried copy of a load in flight)
+    const float* eps_row = (MODE == 0) ? a.eps + (size_t)blk * (2 * H) * TB + tj : nullptr;
     float* ust = a.ustore + (size_t)blk * (2 * H) * TB + tj;
     float L = a.wl, R = a.wr;
     int seen_cost = 0;
     float eA1 = 0.f, eA2 = 0.f, eB1 = 0.f, eB2 = 0.f;
-#if MPPI_NOISE_REG
-    // Philox block n_base + p / 2 of this global trajectory: the normals of steps p and p + 1
-    const uint64_t kg = (uint64_t)(a.k_offset + (int64_t)blk * TB + tj);
-    auto gen = [&](int p) __attribute__((always_inline)) {
-      if constexpr (MODE == 0) noise_block_pk(a.seed, a.n_base + (uint64_t)(p >> 1), kg, &eA1, &eA2, &eB1, &eB2);
-    };
-#else
-    const float* eps_row = (MODE == 0) ? a.eps + (size_t)blk * (2 * H) * TB + tj : nullptr;
     if constexpr (MODE == 0) {
       eA1 = eps_row[0];
       eA2 = eps_row[(size_t)H * TB];
@@ -1797,8 +1774,6 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       eB1 = eps_row[(size_t)t1 * TB];
       eB2 = eps_row[(size_t)(H + t1) * TB];
     }
-    auto gen = [&](int) {};
-#endif
     auto prod = [&](int p, float& e1r, float& e2r) __attribute__((always_inline)) {
       float u1, u2;
       if constexpr (MODE == 0) {
@@ -1808,9 +1783,6 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
         if (p < a.ucache_steps) {  // kept for the leaf reduction (uniform branch)
           ucache[(size_t)p * UCACHE_ROW + tj] = u1;
           ucache[(size_t)(a.ucache_steps + p) * UCACHE_ROW + tj] = u2;
-        } else if (MPPI_NOISE_REG) {  // the rest in HBM (the leaf reads them back)
-          ust[(size_t)p * TB] = u1;
-          ust[(size_t)(H + p) * TB] = u2;
         }
       } else {
         const size_t o = (size_t)(valid ? kl : 0) * H + p;
@@ -1841,24 +1813,18 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
         }
       }
       lds_store_release(f_prod, p + 1);
-#if !MPPI_NOISE_REG
       if constexpr (MODE == 0) {  // the normals of step p + 2 into the registers just freed
         const int tn = min(p + 2, H - 1);
         e1r = eps_row[(size_t)tn * TB];
         e2r = eps_row[(size_t)(H + tn) * TB];
       }
-#endif
     };
     int p = 0;
     for (; p + 1 < H; p += 2) {
-      gen(p);
       prod(p, eA1, eA2);
       prod(p + 1, eB1, eB2);
     }
-    if (p < H) {
-      gen(p);
-      prod(p, eA1, eA2);
-    }
+    if (p < H) prod(p, eA1, eA2);
   } else if (role == ROLE_WHEEL) {
     // ---------------- wheel contacts of the even steps (the slope critic reads lw / rw at i,
     // i + 2 for even i, critics_warp.py:220-267) and the slope critic.  Contact sets A / B
@@ -2001,13 +1967,11 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
     cost_lds[tj] = valid ? cost : INFINITY;
   }
   __syncthreads();
-  if constexpr (MODE == 0)  // the first steps' sampled controls in LDS, the rest in HBM rows (the
-                            // sampled controls, or the normals: the leaf recomputes the controls)
-    leaf_records<TB, NT, !MPPI_NOISE_REG, FUSED>(a, cost_lds, scratch,
-                                                 (MPPI_NOISE_REG ? a.ustore : a.eps) + (size_t)blk * (2 * H) * TB,
-                                                 unom_lds, ucache, a.ucache_steps, blk);
+  if constexpr (MODE == 0)  // rows hold the normals; the leaf recomputes the sampled controls
+    leaf_records<TB, NT, true, FUSED>(a, cost_lds, scratch, a.eps + (size_t)blk * (2 * H) * TB, unom_lds,
+                                      ucache, a.ucache_steps, blk);
   else
-    leaf_records<TB, NT, false, FUSED>(a, cost_lds, scratch, a.ustore + (size_t)blk * (2 * H) * TB, unom_lds, ucache,
+    leaf_records<TB, NT, false, FUSED>(a, cost_lds, scratch, a.ustore + (size_t)blk * (2 * H) * TB, nullptr, nullptr,
                                        0, blk);
   if (clk_wg) a.clk[6] = __builtin_amdgcn_s_memrealtime();  // workgroup 0's leaf record written
   if (clk_any) a.clk[kClkBase + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -3781,7 +3745,6 @@ __global__ __launch_bounds__(NROLES * TB) void mppi_step_server_kernel(const Ser
     const int nslot = __builtin_amdgcn_readfirstlane(c.noise_slot);
     const uint64_t nbase = ((uint64_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_hi) << 32) |
                            (uint32_t)__builtin_amdgcn_readfirstlane(c.noise_n_base_lo);
-    if (MPPI_NOISE_REG) a.n_base = nbase;  // (this step's normals, generated by the producer waves)
     // the normals of step + 2 (when commanded): W wave-units (one Philox block of 64 trajectories
     // each) in S static shares, two per workgroup outside the finish (ticket t: shares 2t, 2t + 1,
     // from its record on) and one per finish workgroup but the last (blk: share 2 nn + blk, after
