@@ -1146,7 +1146,12 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem& d
         const int ti = (int)__builtin_amdgcn_fmed3f(f.x, -1.0f, fi_hi);  // min(i, grid - 1)
         const int tjj = (int)__builtin_amdgcn_fmed3f(f.y, fj_lo, 1.0f);  // -min(j, rows - 1)
         const int idx = __mul24(tjj, -nrow) + (ti + ncol0);
+#if MPPI_DIAG_CHAIN >= 2  // (diagnostic: every gather hits one entry, i.e. L1; the address is still formed)
+        asm volatile("" ::"v"(idx));
+        nv = *reinterpret_cast<const float4*>(nbase + (uint32_t)(ncol0 << 4));
+#else
         nv = *reinterpret_cast<const float4*>(nbase + (uint32_t)(idx << 4));
+#endif
       };
       auto read_in = [&](int t, float& v, float& sn, float& cs, float& om, int need) __attribute__((always_inline)) {
         if (need) lds_wait_ge(f_prod, need, seen_prod, ws);
@@ -1611,7 +1616,9 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 // other three waves, whose own streams are then shorter than the chain's.
 // Progress counters per group (LDS), each wave caching the last value it acquired:
 //   CHAIN step s : produced > s, wheel > s - D, cost > s - D   (ring_out slot s % D free)
-//   PROD  step p : cost > p - D   (ring_in slot p % D read by CHAIN and COST; COST waited on CHAIN)
+//   PROD  step p : chained > p - D   (ring_in slot p % D is read by CHAIN only: the speed critic, the
+//                  one consumer of v, runs in PROD itself since round 6, so the producer runs up to D
+//                  steps ahead of the chain instead of the cost wave, which trails the chain)
 //   WHEEL / COST step s : chained > s
 // Deadlock-free: no wave waits on a later step of a wave that waits on it.
 // Issue priorities: the chain 3; the producer 1 (the chain waits on it each step: +1.3 % C3 steps/s
@@ -1695,7 +1702,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  float c_pf = 0.f, c_sp = 0.f, c_ob = 0.f;  // COST: the critic sums, kept across the barrier
+  float c_pf = 0.f, c_ob = 0.f;  // COST: the critic sums, kept across the barrier
 
   if (role == ROLE_CHAIN) {
     // ---------------- the serial projection, one step per iteration
@@ -1759,13 +1766,33 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       lds_store_release(f_chain, sc + 1);
     }
   }
+#if MPPI_DIAG_CHAIN == 1 || MPPI_DIAG_CHAIN == 2  // (diagnostic: the chain alone on its SIMD)
+  else if (role == ROLE_PROD) {
+    for (int p = 0; p < H; ++p) {
+      float* ri = ring_in + (p % D) * RI * TB + tj;
+      ri[0] = 0.9f;
+      ri[TB] = 0.01f;
+      ri[2 * TB] = 0.99995f;
+      ri[3 * TB] = 5e-5f;
+      lds_store_release(f_prod, p + 1);
+    }
+  } else if (role == ROLE_WHEEL) {
+    lds_store_release(f_wheel, H);
+    sw_lds[tj] = 0.f;
+  } else {
+    lds_store_release(f_cost, H);
+  }
+  if (true) {  // (the roles' normal work below is not run)
+  }
+#endif
   else if (role == ROLE_PROD) {
     // ---------------- sampling + wheel filter + sin/cos, normals prefetched two steps ahead
     // (even / odd steps in their own registers: no loop-carried copy of a load in flight)
     const float* eps_row = (MODE == 0) ? a.eps + (size_t)blk * (2 * H) * TB + tj : nullptr;
     float* ust = a.ustore + (size_t)blk * (2 * H) * TB + tj;
     float L = a.wl, R = a.wr;
-    int seen_cost = 0;
+    float sp = 0.f;  // _maximise_speed (critics_warp.py:281-300) over the v it produces
+    int seen_chain = 0;
     float eA1 = 0.f, eA2 = 0.f, eB1 = 0.f, eB2 = 0.f;
     if constexpr (MODE == 0) {
       eA1 = eps_row[0];
@@ -1798,7 +1825,11 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       float sn, cs;
       if (a.small_angle) dm_sincosf_small(wp * a.dt, &sn, &cs);
       else dm_sincosf(wp * a.dt, &sn, &cs);
-      wait_ge(f_cost, p - D + 1, seen_cost);
+      const float spt = sp + (a.vmax - vp) / (vp + 0.0001f);
+      sp = a.speed_on ? spt : sp;
+      // ring_in slot p % D held step p - D, which only the chain reads (at the latest by its
+      // iteration p - D, so chained >= p - D + 1 covers it; step 0 before its first iteration)
+      wait_ge(f_chain, p - D + 1, seen_chain);
       float* ri = ring_in + (p % D) * RI * TB + tj;
       ri[0] = vp;
       ri[TB] = sn;
@@ -1810,6 +1841,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
           if (a.d_u1) a.d_u1[o1] = u1;
           if (a.d_u2) a.d_u2[o1] = u2;
           if (a.d_w) a.d_w[o1] = wp;
+          if (a.d_v) a.d_v[o1] = vp;
         }
       }
       lds_store_release(f_prod, p + 1);
@@ -1825,6 +1857,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       prod(p + 1, eB1, eB2);
     }
     if (p < H) prod(p, eA1, eA2);
+    cost_lds[tj] = sp;  // (to the cost wave, which reads it after the barrier and then stores the cost)
   } else if (role == ROLE_WHEEL) {
     // ---------------- wheel contacts of the even steps (the slope critic reads lw / rw at i,
     // i + 2 for even i, critics_warp.py:220-267) and the slope critic.  Contact sets A / B
@@ -1903,7 +1936,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
   } else {
     // ---------------- costmap gather (used one step later), path-follow, speed, obstacle
     int seen_chain = 0;
-    float pf_sum = 0.f, sp = 0.f, ob = 0.f, last_x = a.x0, last_y = a.y0;
+    float pf_sum = 0.f, ob = 0.f, last_x = a.x0, last_y = a.y0;
     float cmA = 0.f, cmB = 0.f;  // costmap value of the even / odd step
     Recip rcm;
     rcm.b = a.res_c;
@@ -1911,19 +1944,15 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       wait_ge(f_chain, sc + 1, seen_chain);
       const float* ro = ring_out + (sc % D) * 4 * TB + tj;
       const float x = ro[0], y = ro[TB];
-      const float vq = ring_in[(sc % D) * RI * TB + tj];  // v of step sc (slot not reused yet)
       cm_mine = a.cm[costmap_index<false>(a.cm_size, a.hw, rcm, x, y, nobad, a.rinv_res_c, a.cdiv_res_c)];
       const float pft = pf_sum + 10.0f * (fabsf(x - a.gx) + fabsf(y - a.gy));
       pf_sum = (sc < H - 1) ? pft : pf_sum;  // _path_follow_critic sum over t < H-1
       last_x = x;
       last_y = y;
-      const float spt = sp + (a.vmax - vq) / (vq + 0.0001f);  // _maximise_speed
-      sp = a.speed_on ? spt : sp;
       // _avoid_obstacle: the costmap value gathered one step earlier (step sc - 1)
       const float ob1 = (cm_prev > a.thr) ? ob + a.pen : ob;
       ob = (sc > 0) ? ob1 + cm_prev : ob;
       if constexpr (DUMP) {
-        if (valid && a.d_v) a.d_v[(size_t)kl * H + sc] = vq;
       }
       lds_store_release(f_cost, sc + 1);
     };
@@ -1944,7 +1973,6 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       pf = pf_sum;
     }
     c_pf = pf;
-    c_sp = sp;
     c_ob = ob;
   }
 #ifdef MPPI_STAMPS
@@ -1961,7 +1989,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
   if (role == ROLE_COST) {  // critics_warp.py:325-329, this f32 add order
     float cost = a.w_path * c_pf;
     cost = cost + a.w_slope * sw_lds[tj];
-    cost = cost + a.w_speed * c_sp;
+    cost = cost + a.w_speed * cost_lds[tj];  // (the producer's speed critic sum)
     cost = cost + a.w_obs * c_ob;
     if (valid) a.cost_out[kl] = cost;
     cost_lds[tj] = valid ? cost : INFINITY;
