@@ -641,36 +641,6 @@ __device__ __forceinline__ int costmap_index(int size, float hw, const Recip& rr
   return ix + size * iy;
 }
 
-#ifdef MPPI_STAMPS
-// Diagnostic build only (profiles/ubench/stamps.sh): per-wave cycle stamps.
-__device__ uint64_t g_dbg_stamps[64 * 16 * 2 + 64 * 16 * 4 + 1024 * 2 + 64 * 8 + 64 + 128 * 4];
-#define FIN_STAMP(k)                                                                    \
-  do {                                                                                  \
-    if (threadIdx.x == 0) {                                                             \
-      g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-      g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + 32 + (k)] = __builtin_amdgcn_s_memtime(); \
-    }                                                                                   \
-  } while (0)
-// per finish workgroup b < 128: [.. + 64 + 4 b + k]
-#define FINWG_STAMP(b, k)                                                                \
-  do {                                                                                  \
-    if (threadIdx.x == 0 && (b) < 128)                                                  \
-      g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + 64 + 4 * (b) + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#define LEAF_STAMP(k)                                                                   \
-  do {                                                                                  \
-    if (threadIdx.x == 0 && blockIdx.x < 64)                                            \
-      g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + blockIdx.x * 8 + (k)] = dbg_stamp();        \
-  } while (0)
-__device__ __forceinline__ uint64_t dbg_stamp() {
-  uint64_t t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
-extern "C" int mppi_debug_stamps(uint64_t* host, int n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dbg_stamps), n * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
-}
-#endif
 
 // =====================================================================  reductions
 __device__ __forceinline__ float wave_min(float v) {
@@ -891,9 +861,6 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
   float* wbuf = reinterpret_cast<float*>(scratch);                           // [TB]
   float* wave_m = wbuf + TB;                                                 // [NWL]
   double* red = reinterpret_cast<double*>(scratch + ((TB + NWL) * 4 + 15) / 16 * 16);  // [NL][E]
-#ifdef MPPI_STAMPS
-  LEAF_STAMP(0);
-#endif
   if (wave < NWL) {
     const float wm = wave_min(cost_lds[tid]);
     if (lane == 0) wave_m[wave] = wm;
@@ -907,9 +874,6 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
     wbuf[j] = (c < INFINITY) ? dm_expf(-((c - m) / a.T)) : 0.0f;
   }
   __syncthreads();
-#ifdef MPPI_STAMPS
-  LEAF_STAMP(1);
-#endif
   // rows (leaf, j), j in [1, E): the pairwise tree over the leaf's 256 trajectories in index
   // order = (half 0) + (half 1), half = ((line 0 + line 1) + (line 2 + line 3)), line = 32
   // trajectories (8 float4 groups, a pairwise tree of its own).  One LINE per thread, the loads
@@ -998,9 +962,6 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
       }
     }
   }
-#ifdef MPPI_STAMPS
-  LEAF_STAMP(4);
-#endif
   __syncthreads();
   for (int j = tid; j < E; j += NT) {
     double val[NL];
@@ -1030,9 +991,6 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
         a.rec_m[blk] = lm[0];
     }
   }
-#ifdef MPPI_STAMPS
-  LEAF_STAMP(5);
-#endif
 }
 
 // =====================================================================  pair-synchronised rollout kernel
@@ -1074,32 +1032,21 @@ __device__ __forceinline__ void lds_store_release(int* f, int v) {
 // flight while step t's outputs are published.  Arithmetic: packed x / y FP32 (orient_step,
 // advance_step), every quotient and square root correctly rounded; an out-of-range lane redoes
 // its step with the IEEE operators.
-struct WaitStat {
-  uint64_t wait = 0, n = 0;  // MPPI_STAMPS builds: cycles spent in LDS waits, waits that read LDS
-};
-__device__ __forceinline__ void lds_wait_ge(const int* f, int target, int& seen, WaitStat& ws) {
+__device__ __forceinline__ void lds_wait_ge(const int* f, int target, int& seen) {
   if (seen >= target) return;
-#ifdef MPPI_STAMPS
-  const uint64_t t0 = dbg_stamp();
-#endif
   int v;
   // (the chain waves: no s_sleep between reads, a woken chain lost up to ~64 cycles per wait; C3
   // +0.7 % at 200 steps, chain waits 131 -> 120 cycles per step)
   while ((v = lds_load_acquire(f)) < target) {
   }
   seen = v;
-#ifdef MPPI_STAMPS
-  ws.wait += dbg_stamp() - t0;
-  ws.n += 1;
-#endif
-  (void)ws;
 }
 
 template <int TB, int NC, bool DUMP>
 __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem& dem, const Traj& s, int tj,
                                               bool valid, int64_t kl, const float* ring_in, float* ring_out,
                                               const int* f_prod, int* f_chain, const int* const (&f_cons)[NC],
-                                              int& seen_prod, int (&seen_cons)[NC], WaitStat& ws) {
+                                              int& seen_prod, int (&seen_cons)[NC]) {
   constexpr int D = PAIR_D;
   constexpr int RI = 4;
   using T_ = std::true_type;
@@ -1146,15 +1093,10 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem& d
         const int ti = (int)__builtin_amdgcn_fmed3f(f.x, -1.0f, fi_hi);  // min(i, grid - 1)
         const int tjj = (int)__builtin_amdgcn_fmed3f(f.y, fj_lo, 1.0f);  // -min(j, rows - 1)
         const int idx = __mul24(tjj, -nrow) + (ti + ncol0);
-#if MPPI_DIAG_CHAIN >= 2  // (diagnostic: every gather hits one entry, i.e. L1; the address is still formed)
-        asm volatile("" ::"v"(idx));
-        nv = *reinterpret_cast<const float4*>(nbase + (uint32_t)(ncol0 << 4));
-#else
         nv = *reinterpret_cast<const float4*>(nbase + (uint32_t)(idx << 4));
-#endif
       };
       auto read_in = [&](int t, float& v, float& sn, float& cs, float& om, int need) __attribute__((always_inline)) {
-        if (need) lds_wait_ge(f_prod, need, seen_prod, ws);
+        if (need) lds_wait_ge(f_prod, need, seen_prod);
         const float* ri = ring_in + (t % D) * RI * TB + tj;
         v = ri[0];
         sn = ri[TB];
@@ -1201,7 +1143,7 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem& d
         }
         if constexpr (EVEN) {
 #pragma unroll
-          for (int c = 0; c < NC; ++c) lds_wait_ge(f_cons[c], t - D + 2, seen_cons[c], ws);
+          for (int c = 0; c < NC; ++c) lds_wait_ge(f_cons[c], t - D + 2, seen_cons[c]);
         }
         float* ro = ring_out + (t % D) * 4 * TB + tj;
         ro[0] = pX.x;
@@ -1279,15 +1221,6 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   int* f_prod = flags + pair;
   int* f_chain = flags + NWC + pair;
   int* f_cons = flags + 2 * NWC + pair;
-#ifdef MPPI_STAMPS
-  const uint64_t k_t0 = dbg_stamp(), k_r0 = __builtin_amdgcn_s_memrealtime();
-  uint64_t st_wait = 0;
-  if (blockIdx.x == 0 && tid == 0) {  // previous finish's completion signal -> this kernel's start
-    uint64_t* fs = g_dbg_stamps + 64 * 16 * 6 + 1024 * 2 + 64 * 8;
-    fs[14] = fs[5];
-    fs[15] = k_r0;
-  }
-#endif
   const int64_t kl = (int64_t)blockIdx.x * TB + tj;
   const bool valid = kl < a.K;
   const int H = a.H;
@@ -1352,15 +1285,9 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
   // needs no LDS read and no fence (the partner usually runs several steps ahead).
   auto wait_ge = [&](const int* f, int target, int& seen) __attribute__((always_inline)) {
     if (seen >= target) return;
-#ifdef MPPI_STAMPS
-    const uint64_t t0 = dbg_stamp();
-#endif
     int v;
     while ((v = lds_load_acquire(f)) < target) __builtin_amdgcn_s_sleep(1);
     seen = v;
-#ifdef MPPI_STAMPS
-    st_wait += dbg_stamp() - t0;
-#endif
   };
 
   if (!side) {
@@ -1369,12 +1296,8 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
     if constexpr (PROJ == 3) {
       const int* cons[1] = {f_cons};
       int seen_c[1] = {0};
-      WaitStat ws;
       chain_wave_3d<TB, 1, DUMP>(a, dem, s, tj, valid, kl, ring_in, ring_out, f_prod, f_chain, cons, seen_prod,
-                                 seen_c, ws);
-#ifdef MPPI_STAMPS
-      st_wait += ws.wait;
-#endif
+                                 seen_c);
     } else
     for (int sc = 0; sc < H; ++sc) {  // 2D: the planar step (projection_warp.py:353-382)
       wait_ge(f_prod, sc + 1, seen_prod);
@@ -1571,34 +1494,12 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
     if (valid) a.cost_out[kl] = cost;
     cost_lds[tj] = valid ? cost : INFINITY;
   }
-#ifdef MPPI_STAMPS
-  const uint64_t k_t1 = dbg_stamp();
-  if ((tid & 63) == 0 && blockIdx.x < 64) {
-    g_dbg_stamps[(blockIdx.x * (NT / 64) + wave) * 2] = (k_t1 - k_t0) - st_wait;
-    g_dbg_stamps[(blockIdx.x * (NT / 64) + wave) * 2 + 1] = st_wait;
-  }
-#endif
   __syncthreads();
   if constexpr (MODE == 0)  // rows hold the normals; the leaf recomputes the sampled controls
     leaf_records<TB, NT, true>(a, cost_lds, scratch, a.eps + (size_t)blockIdx.x * (2 * H) * TB, unom_lds, ucache,
                                a.ucache_steps);
   else
     leaf_records<TB, NT>(a, cost_lds, scratch, a.ustore + (size_t)blockIdx.x * (2 * H) * TB);
-#ifdef MPPI_STAMPS
-  const uint64_t k_t2 = dbg_stamp(), k_r2 = __builtin_amdgcn_s_memrealtime();
-  if ((tid & 63) == 0 && blockIdx.x < 64) {
-    uint64_t* g = g_dbg_stamps + 64 * 16 * 2 + (blockIdx.x * (NT / 64) + wave) * 4;
-    g[0] = k_t1 - k_t0;
-    g[1] = k_t2 - k_t1;
-    g[2] = k_r2 - k_r0;
-    g[3] = k_t2 - k_t0;
-  }
-  if (tid == 0 && blockIdx.x < 1024) {
-    uint64_t* g = g_dbg_stamps + 64 * 16 * 6 + blockIdx.x * 2;
-    g[0] = k_r0;
-    g[1] = k_r2;
-  }
-#endif
 }
 
 // =====================================================================  role-split rollout kernel
@@ -1627,6 +1528,9 @@ __global__ __launch_bounds__(2 * TB) void mppi_rollout_pair_kernel(const Rollout
 // starved, ran ~105 us and into the next finish, and pipelined C3 steps alternated between ~98 and
 // ~120 us (profiles/r02_notes.md; 0: ~9900 against ~9200 steps/s).
 constexpr int kProdPrio = 1, kSidePrio = 0;
+// steps ahead the producer loads each step's normals (round 6: 4 and 8 measured within noise of 2 on
+// the server and in separate launches, profiles/r06_notes.md)
+constexpr int kProdPrefetch = 2;
 constexpr int ROLE_CHAIN = 0, ROLE_PROD = 1, ROLE_WHEEL = 2, ROLE_COST = 3, NROLES = 4;
 
 // FUSED: returns the workgroup's ticket (its rank among the workgroups that have completed their
@@ -1683,22 +1587,11 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
                                       __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();  // flags and nominal sequence initialised
 
-#ifdef MPPI_STAMPS
-  const uint64_t k_t0 = dbg_stamp();
-  uint64_t st_wait = 0, st_n = 0;
-#endif
   auto wait_ge = [&](const int* f, int target, int& seen) __attribute__((always_inline)) {
     if (seen >= target) return;
-#ifdef MPPI_STAMPS
-    const uint64_t t0 = dbg_stamp();
-#endif
     int v;
     while ((v = lds_load_acquire(f)) < target) __builtin_amdgcn_s_sleep(1);
     seen = v;
-#ifdef MPPI_STAMPS
-    st_wait += dbg_stamp() - t0;
-    st_n += 1;
-#endif
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
@@ -1733,13 +1626,8 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
     if constexpr (PROJ == 3) {
       const int* cons[2] = {f_wheel, f_cost};
       int seen_cons[2] = {0, 0};
-      WaitStat ws;
       chain_wave_3d<TB, 2, DUMP>(a, dem, s, tj, valid, kl, ring_in, ring_out, f_prod, f_chain, cons, seen_prod,
-                                 seen_cons, ws);
-#ifdef MPPI_STAMPS
-      st_wait += ws.wait;
-      st_n += ws.n;
-#endif
+                                 seen_cons);
     } else
     for (int sc = 0; sc < H; ++sc) {  // 2D (projection_warp.py:373-382): no normal, wheels zero
       wait_ge(f_prod, sc + 1, seen_prod);
@@ -1766,40 +1654,23 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
       lds_store_release(f_chain, sc + 1);
     }
   }
-#if MPPI_DIAG_CHAIN == 1 || MPPI_DIAG_CHAIN == 2  // (diagnostic: the chain alone on its SIMD)
   else if (role == ROLE_PROD) {
-    for (int p = 0; p < H; ++p) {
-      float* ri = ring_in + (p % D) * RI * TB + tj;
-      ri[0] = 0.9f;
-      ri[TB] = 0.01f;
-      ri[2 * TB] = 0.99995f;
-      ri[3 * TB] = 5e-5f;
-      lds_store_release(f_prod, p + 1);
-    }
-  } else if (role == ROLE_WHEEL) {
-    lds_store_release(f_wheel, H);
-    sw_lds[tj] = 0.f;
-  } else {
-    lds_store_release(f_cost, H);
-  }
-  if (true) {  // (the roles' normal work below is not run)
-  }
-#endif
-  else if (role == ROLE_PROD) {
-    // ---------------- sampling + wheel filter + sin/cos, normals prefetched two steps ahead
-    // (even / odd steps in their own registers: no loop-carried copy of a load in flight)
+    // ---------------- sampling + wheel filter + sin/cos, normals prefetched PF steps ahead (step p in
+    // register set p % PF: no loop-carried copy of a load in flight)
     const float* eps_row = (MODE == 0) ? a.eps + (size_t)blk * (2 * H) * TB + tj : nullptr;
     float* ust = a.ustore + (size_t)blk * (2 * H) * TB + tj;
     float L = a.wl, R = a.wr;
     float sp = 0.f;  // _maximise_speed (critics_warp.py:281-300) over the v it produces
     int seen_chain = 0;
-    float eA1 = 0.f, eA2 = 0.f, eB1 = 0.f, eB2 = 0.f;
+    constexpr int PF = kProdPrefetch;
+    float e[PF][2] = {};
     if constexpr (MODE == 0) {
-      eA1 = eps_row[0];
-      eA2 = eps_row[(size_t)H * TB];
-      const int t1 = min(1, H - 1);
-      eB1 = eps_row[(size_t)t1 * TB];
-      eB2 = eps_row[(size_t)(H + t1) * TB];
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int t = min(q, H - 1);
+        e[q][0] = eps_row[(size_t)t * TB];
+        e[q][1] = eps_row[(size_t)(H + t) * TB];
+      }
     }
     auto prod = [&](int p, float& e1r, float& e2r) __attribute__((always_inline)) {
       float u1, u2;
@@ -1845,18 +1716,20 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
         }
       }
       lds_store_release(f_prod, p + 1);
-      if constexpr (MODE == 0) {  // the normals of step p + 2 into the registers just freed
-        const int tn = min(p + 2, H - 1);
+      if constexpr (MODE == 0) {  // the normals of step p + PF into the registers just freed
+        const int tn = min(p + PF, H - 1);
         e1r = eps_row[(size_t)tn * TB];
         e2r = eps_row[(size_t)(H + tn) * TB];
       }
     };
     int p = 0;
-    for (; p + 1 < H; p += 2) {
-      prod(p, eA1, eA2);
-      prod(p + 1, eB1, eB2);
+    for (; p + PF <= H; p += PF) {
+#pragma unroll
+      for (int q = 0; q < PF; ++q) prod(p + q, e[q][0], e[q][1]);
     }
-    if (p < H) prod(p, eA1, eA2);
+#pragma unroll
+    for (int q = 0; q < PF - 1; ++q)
+      if (p + q < H) prod(p + q, e[q][0], e[q][1]);
     cost_lds[tj] = sp;  // (to the cost wave, which reads it after the barrier and then stores the cost)
   } else if (role == ROLE_WHEEL) {
     // ---------------- wheel contacts of the even steps (the slope critic reads lw / rw at i,
@@ -1975,15 +1848,6 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
     c_pf = pf;
     c_ob = ob;
   }
-#ifdef MPPI_STAMPS
-  // per wave of the first 64 workgroups: [work cycles, wait cycles, waits that read LDS]
-  if ((tid & 63) == 0 && blockIdx.x < 64) {
-    uint64_t* g = g_dbg_stamps + (blockIdx.x * 16 + wave) * 2;
-    g[0] = (dbg_stamp() - k_t0) - st_wait;
-    g[1] = st_wait;
-    g_dbg_stamps[64 * 16 * 2 + blockIdx.x * 16 + wave] = st_n;
-  }
-#endif
   __syncthreads();  // WHEEL's slope sums are in sw_lds
   if (clk_wg) a.clk[5] = __builtin_amdgcn_s_memrealtime();  // every role of workgroup 0 done
   if (role == ROLE_COST) {  // critics_warp.py:325-329, this f32 add order
@@ -2235,9 +2099,6 @@ __device__ __forceinline__ void optimal_rollout(const FinishArgs& f, const Dem& 
                                                 const float* qpre = nullptr) {
   if (tid < 64) tail_chain_3d(f, dem, in4, chain, nsteps, tid, qpre);  // the serial chain, wave 0
   __syncthreads();
-#ifdef MPPI_STAMPS
-  FIN_STAMP(21);
-#endif
   for (int t = tid; t < nsteps; t += nthreads) {  // heights + wheel contacts, all lanes
     const float4 ca = reinterpret_cast<const float4*>(chain)[2 * t], cb = reinterpret_cast<const float4*>(chain)[2 * t + 1];
     const float ch[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};  // x, y, n, heading
@@ -2306,9 +2167,6 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
     uo[tid < H ? tid : PS + (tid - H)] = (ures * f.ok) * one_m_a;
   }
   __syncthreads();
-#ifdef MPPI_STAMPS
-  FIN_STAMP(2);
-#endif
   Dem dem;
   dem.init(f.Z, f.rows, f.grid, f.x_min, f.y_min, f.res, f.rinv_res, f.cdiv_res);
   dem.N = f.ntab;
@@ -2361,14 +2219,7 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[4 + k] = B[k];
-#ifdef MPPI_STAMPS
-        if (t == 0) FIN_STAMP(7);
-        if (t == 32) FIN_STAMP(8);
-#endif
       }
-#ifdef MPPI_STAMPS
-      FIN_STAMP(14);
-#endif
       const float* pf = reinterpret_cast<const float*>(p);
       float* qf = reinterpret_cast<float*>(q);
       for (int k = 0; t < H; ++t, ++k) {
@@ -2376,9 +2227,6 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
         qf[k] = x;
       }
     }
-#ifdef MPPI_STAMPS
-    FIN_STAMP(12);
-#endif
   } else if (wave == nthreads / 64 - 1 && f.mode == 2) {
     if (lane == 0) {  // step 0 of the optimal rollout needs only the first filter step
       const float L0 = f.wl * f.oa + uo[0], R0 = f.wr * f.oa + uo[PS];
@@ -2410,21 +2258,12 @@ __device__ __forceinline__ void finish_phase2(const FinishArgs& f, float ures, u
     }
   }
   __syncthreads();
-#ifdef MPPI_STAMPS
-  FIN_STAMP(3);
-#endif
   // mode 1: the whole optimal rollout; mode 2: its first step only (the pose the
   // closed loop needs now), the rest runs in mppi_tail_kernel on a side stream
   if (f.mode != 2) optimal_rollout(f, dem, in4, chain, H, ostage + 4 * H, tid, nthreads, qpre);
   __syncthreads();
   for (int i = tid; i < nout; i += nthreads) store_out(f.out + i, ostage[i]);
-#ifdef MPPI_STAMPS
-  FIN_STAMP(4);
-#endif
   signal_done(f);
-#ifdef MPPI_STAMPS
-  FIN_STAMP(5);
-#endif
 }
 
 __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishArgs f) {
@@ -2432,9 +2271,6 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
   const int tid = threadIdx.x;
   const int H = f.H;
   const int E = 2 * H + 2;
-#ifdef MPPI_STAMPS
-  if (blockIdx.x == 0) FIN_STAMP(0);
-#endif
   // ---------------- (1) tree
   // LDS during the tree: [FIN_LDS_NODES][E] doubles, then PairScale table
   double* lnode = reinterpret_cast<double*>(smem_raw);
@@ -2464,9 +2300,6 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
       __syncthreads();
       base += w;
     }
-#ifdef MPPI_STAMPS
-    if (b == 0) FIN_STAMP(9);
-#endif
     // device-scope stores write through the XCD's L2, so no fence has to write the whole
     // (rollout-dirty) L2 back: completion of these stores (vmcnt) orders them before the count
     for (int j = tid; j < E; j += FIN_THREADS) {
@@ -2478,9 +2311,6 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-#ifdef MPPI_STAMPS
-    if (b == 0) FIN_STAMP(10);
-#endif
     int* flag = reinterpret_cast<int*>(lm + 16);
     if (tid == 0) {
       const unsigned prev = __hip_atomic_fetch_add(f.level1_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2490,9 +2320,6 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
     }
     __syncthreads();
     if (!flag[0]) return;
-#ifdef MPPI_STAMPS
-    FIN_STAMP(13);
-#endif
     // the level-1 records, read at device scope (past any stale copy in this XCD's L2)
     n = gridDim.x;
     if (tid < 16) lm[tid] = (tid < n) ? (float)__hip_atomic_load(f.level1 + (size_t)tid * E, __ATOMIC_RELAXED,
@@ -2513,9 +2340,6 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
         __syncthreads();
         base2 += w;
       }
-#ifdef MPPI_STAMPS
-      FIN_STAMP(6);
-#endif
       for (int j = tid; j < E; j += FIN_THREADS) {
         double v[16];
 #pragma unroll
@@ -2526,9 +2350,6 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
       }
       n = 1;
       __syncthreads();
-#ifdef MPPI_STAMPS
-      FIN_STAMP(1);
-#endif
       goto root_ready;
     }
     __threadfence();  // more than 256 level-1 records: the general passes below read them plainly
@@ -2616,9 +2437,6 @@ __global__ __launch_bounds__(FIN_THREADS) void mppi_finish_kernel(const FinishAr
     for (int j = tid; j < n * E; j += FIN_THREADS) lnode[j] = cur[j];
   }
   __syncthreads();
-#ifdef MPPI_STAMPS
-  FIN_STAMP(1);
-#endif
 root_ready:
   // root = lnode[0..E) (n == 1) or empty (n == 0)
   if (f.mode == 0) {
@@ -2670,9 +2488,6 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
   // (profiles/r04_notes.md).  Not in the resident server (RECS_WT), whose noise runs in its own
   // workgroups after their records (there the priority measured no gain, r02_notes.md).
   if constexpr (!RECS_WT) __builtin_amdgcn_s_setprio(3);
-#ifdef MPPI_STAMPS
-  if (blk == 0) FIN_STAMP(0);
-#endif
   const int tid = thread_id<RECS_WT, FIN_THREADS>();
   const int H = f.H;
   const int E = 2 * H + 2;
@@ -2695,9 +2510,6 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
   const int L = P > FIN_THREADS ? P / FIN_THREADS : 1;  // 1, 2 or 4 (P <= COLFIN_PMAX)
   const int T = P / L;
   float lm[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
-#ifdef MPPI_STAMPS
-  if (blk == 0) FIN_STAMP(18);
-#endif
   // (2) pair scales: first the node minima (the m pair_scale forms; level l of the minima at
   //     mlev + 2P - (2P >> l), level 0 the records): a thread's own records, then lane shuffles
   //     inside the wave, then the waves' minima on wave 0 (two barriers, not log2 P); then every
@@ -2765,10 +2577,6 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
     ++ml;
     if (tid < T && (tid & (2 * k - 1)) == 0) lev(ml)[tid / (2 * k)] = mm;
   }
-#ifdef MPPI_STAMPS
-  if (blk == 0 && (tid & 63) == 0)  // each wave's arrival at the barrier: FINWG slot 3 of "workgroup" wave
-    g_dbg_stamps[64 * 16 * 6 + 1024 * 2 + 64 * 8 + 64 + 4 * (tid >> 6) + 3] = __builtin_amdgcn_s_memrealtime();
-#endif
   if (T > 64) {
     __syncthreads();  // the waves' minima (level ml, T / 64 of them)
     if (tid < 64) {
@@ -2784,10 +2592,6 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
     }
   }
   __syncthreads();
-#ifdef MPPI_STAMPS
-  if (blk == 0) FIN_STAMP(16);
-  if (blk == 0) FIN_STAMP(17);
-#endif
   const int log2P = 31 - __clz(P);
   for (int g = tid; g < P - 1; g += FIN_THREADS) {
     const int r = P - g;  // level l holds nodes g with P >> (l + 1) < P - g <= P >> l
@@ -2802,11 +2606,6 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
     lps[dst] = pair_scale(s[2 * i], s[2 * i + 1], f.T);
   }
   __syncthreads();
-#ifdef MPPI_STAMPS
-  if (blk == 0) FIN_STAMP(9);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (blk == 0) FIN_STAMP(11);
-#endif
   // (3) the 4 lowest levels of every item in registers, each level's pair scales read together
   //     ahead of its arithmetic (one LDS round trip per level, not two per pair), then the
   //     scales of the shuffle levels, all at once.  (Deeper prefetch raised the fused step
@@ -2829,9 +2628,6 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
     for (int q = 0; q < 6; ++q)
       if ((1 << q) < NGW) sh[q] = ld_scale(lps + colfin_level_base(P, 4 + q) + (it_g >> (q + 1)));
   }
-#ifdef MPPI_STAMPS
-  if (blk == 0) FIN_STAMP(15);
-#endif
   // (4a) the next levels inside a wave: a column's NG (<= 64 at a time) consecutive lanes
   //      combine by lane shuffles, left child = the lane with the bit clear (no barrier)
   int lvl = 4;
@@ -2858,9 +2654,6 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
     }
     __syncthreads();
   }
-#ifdef MPPI_STAMPS
-  if (blk == 0) FIN_STAMP(10);
-#endif
   // root of slot c: part[c * NG]
   if (f.mode == 0) {
     for (int c = tid; c < nc; c += FIN_THREADS) f.record_out[c0 + c] = part[c * NG];
@@ -2888,9 +2681,6 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
                            __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-#ifdef MPPI_STAMPS
-    FINWG_STAMP(blk, 0);
-#endif
     if (blk != nblk - 1) return true;
     int late = 0;
     if (tid < 2 * H) {  // bounded (2 s of the 100 MHz clock): a lost slice cannot hang the device
@@ -2909,20 +2699,10 @@ __device__ __forceinline__ bool colfin_body(const FinishArgs& f, int P, int ncol
     }
     // a slice that never came: publish nothing (the host's wait reports the step as failed)
     if (__syncthreads_or(late)) return false;
-#ifdef MPPI_STAMPS
-    FINWG_STAMP(blk, 1);
-#endif
     // every finish workgroup has passed its record wait (resident server): re-arm the count
     if (RECS_WT && tid == 0) __hip_atomic_store(rec_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-#ifdef MPPI_STAMPS
-  FIN_STAMP(13);
-#endif
   __syncthreads();  // the tree's LDS is dead from here on
-#ifdef MPPI_STAMPS
-  FIN_STAMP(6);
-  FIN_STAMP(1);
-#endif
   finish_phase2(f, ures, smem_raw, tid, FIN_THREADS, qpre);
   return true;
 }
