@@ -861,6 +861,87 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
   float* wbuf = reinterpret_cast<float*>(scratch);                           // [TB]
   float* wave_m = wbuf + TB;                                                 // [NWL]
   double* red = reinterpret_cast<double*>(scratch + ((TB + NWL) * 4 + 15) / 16 * 16);  // [NL][E]
+  // rows (leaf, j), j in [1, E): the pairwise tree over the leaf's 256 trajectories in index
+  // order = (half 0) + (half 1), half = ((line 0 + line 1) + (line 2 + line 3)), line = 32
+  // trajectories (8 float4 groups, a pairwise tree of its own).  One LINE per thread and round, its
+  // loads issued before any is used: the re-read normals rows come from HBM / MALL (all workgroups'
+  // leaves at once), and the first round's loads are issued before the weights are formed, so their
+  // latency overlaps the weight phase (round 6).  A wave holds 8 rows x 8 lines: lane = 8 k + (row & 7)
+  // for line k of the row, so the eight units of a row sit 8 lanes apart and combine by lane shuffles
+  // (xor 8, 16, 32) in the same order, and the lanes that an LDS read serves together (8 consecutive)
+  // read 8 different rows of the control cache (row stride UCACHE_ROW: 4 banks apart, conflict-free)
+  // or the same weights (a broadcast); with the eight lines of one row in 8 consecutive lanes every
+  // 16-byte read hit the same 4 banks 8 times.
+  const int NR = NL * (E - 1);
+  const int NU = ((NR + 7) >> 3) << 6;       // unit slots: 8 rows per wave (the last wave partly empty)
+  struct Unit {
+    float4 uq[8];
+    int j;
+    bool cached;
+    float nom, sg, lo, hi;
+    const float4* w4;
+  };
+  auto load = [&](int it, Unit& U) __attribute__((always_inline)) {  // unit slot: row 8 (it >> 6) + (it & 7), line (it >> 3) & 7
+    const int k = (it >> 3) & 7;
+    const int r = min(((it >> 6) << 3) + (it & 7), NR - 1);
+    const int half = k >> 2, line = k & 3;
+    const int leaf = r / (E - 1), j = 1 + r - leaf * (E - 1);
+    U.j = j;
+    const int tr0 = 256 * leaf + 128 * half + 32 * line;  // first trajectory of the line
+    U.w4 = reinterpret_cast<const float4*>(wbuf + tr0);
+    const float4* u4 = reinterpret_cast<const float4*>(ub_block + (size_t)(j >= 2 ? j - 2 : 0) * TB + tr0);
+    U.cached = false;  // the sampled controls of this row are in LDS (no normals re-read)
+    U.nom = U.sg = U.lo = U.hi = 0.f;
+    if constexpr (EPS) {  // rows hold the normals: u = clamp(u_nom[t+1] + sigma*eps) as sampled
+      const int c = (j - 2) >= H ? 1 : 0;
+      const int t = max(j - 2, 0) - c * H;
+      const int ti = min(t + 1, H - 1);
+      U.nom = unom[c * H + ti];
+      U.sg = c ? a.s2 : a.s1;
+      U.lo = c ? a.min_u2 : a.min_u1;
+      U.hi = c ? a.max_u2 : a.max_u1;
+      if (j >= 2 && t < uc_steps) {
+        U.cached = true;
+        u4 = reinterpret_cast<const float4*>(ucache + (size_t)(c * uc_steps + t) * UCACHE_ROW + tr0);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 8; ++g) U.uq[g] = (j >= 2) ? u4[g] : make_float4(1.f, 1.f, 1.f, 1.f);
+  };
+  auto reduce = [&](int it, const Unit& U) __attribute__((always_inline)) {
+    const int j = U.j;
+    double gs[8];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const float4 w = U.w4[g];
+      float4 u = U.uq[g];
+      if (EPS && !U.cached) {
+        u.x = clampf(U.nom + U.sg * u.x, U.lo, U.hi);
+        u.y = clampf(U.nom + U.sg * u.y, U.lo, U.hi);
+        u.z = clampf(U.nom + U.sg * u.z, U.lo, U.hi);
+        u.w = clampf(U.nom + U.sg * u.w, U.lo, U.hi);
+      }
+      if (j < 2) u = make_float4(1.f, 1.f, 1.f, 1.f);  // j == 1: S, the weights alone
+      // (w0 u0 + w1 u1) + (w2 u2 + w3 u3) in float64: a product of two floats is exact in a
+      // double, so fma(w0, u0, w1 u1) is the rounded sum of the exact products (one product and
+      // one fma instead of two products and an add per pair; same bits)
+      const double x = __builtin_fma((double)w.x, (double)u.x, (double)w.y * (double)u.y);
+      const double y = __builtin_fma((double)w.z, (double)u.z, (double)w.w * (double)u.w);
+      gs[g] = x + y;
+    }
+    const double ls = ((gs[0] + gs[1]) + (gs[2] + gs[3])) + ((gs[4] + gs[5]) + (gs[6] + gs[7]));
+    // (line 0 + line 1), (line 2 + line 3): left + right; then the half; then the row
+    const double s2 = ls + __shfl_xor(ls, 8, 64);
+    const double hs = s2 + __shfl_xor(s2, 16, 64);
+    const double rs = hs + __shfl_xor(hs, 32, 64);
+    const int r = ((it >> 6) << 3) + (it & 7);
+    if (r < NR && ((it >> 3) & 7) == 0) {
+      const int leaf = r / (E - 1);
+      red[leaf * E + j] = rs;
+    }
+  };
+  Unit first;
+  if (tid < NU) load(tid, first);
   if (wave < NWL) {
     const float wm = wave_min(cost_lds[tid]);
     if (lane == 0) wave_m[wave] = wm;
@@ -874,93 +955,11 @@ __device__ __forceinline__ void leaf_records(const RolloutArgs& a, const float* 
     wbuf[j] = (c < INFINITY) ? dm_expf(-((c - m) / a.T)) : 0.0f;
   }
   __syncthreads();
-  // rows (leaf, j), j in [1, E): the pairwise tree over the leaf's 256 trajectories in index
-  // order = (half 0) + (half 1), half = ((line 0 + line 1) + (line 2 + line 3)), line = 32
-  // trajectories (8 float4 groups, a pairwise tree of its own).  One LINE per thread, the loads
-  // of all of a thread's lines issued before any is used: the re-read normals rows come from HBM /
-  // MALL, and one line after another per thread left that latency exposed 4 times.  A wave holds
-  // 8 rows x 8 lines: lane = 8 k + (row & 7) for line k of the row, so the eight units of a row sit
-  // 8 lanes apart and combine by lane shuffles (xor 8, 16, 32) in the same order, and the lanes that
-  // an LDS read serves together (8 consecutive) read 8 different rows of the control cache (row
-  // stride UCACHE_ROW: 4 banks apart, conflict-free) or the same weights (a broadcast); with the
-  // eight lines of one row in 8 consecutive lanes every 16-byte read hit the same 4 banks 8 times.
-  const int NR = NL * (E - 1);
-  const int NU = ((NR + 7) >> 3) << 6;       // unit slots: 8 rows per wave (the last wave partly empty)
-  constexpr int LR = 1;                      // lines in flight per thread
-  for (int u0 = 0; u0 < NU; u0 += LR * NT) {
-    float4 uq[LR][8];
-    int jr[LR];
-    bool cached_r[LR];
-    float nom_r[LR], sg_r[LR], lo_r[LR], hi_r[LR];
-    const float4* w4r[LR];
-#pragma unroll
-    for (int q = 0; q < LR; ++q) {
-      const int it = u0 + q * NT + tid;      // unit slot: row 8 (it >> 6) + (it & 7), line (it >> 3) & 7
-      const int k = (it >> 3) & 7;
-      const int r = min(((it >> 6) << 3) + (it & 7), NR - 1);
-      const int half = k >> 2, line = k & 3;
-      const int leaf = r / (E - 1), j = 1 + r - leaf * (E - 1);
-      jr[q] = j;
-      const int tr0 = 256 * leaf + 128 * half + 32 * line;  // first trajectory of the line
-      w4r[q] = reinterpret_cast<const float4*>(wbuf + tr0);
-      const float4* u4 = reinterpret_cast<const float4*>(ub_block + (size_t)(j >= 2 ? j - 2 : 0) * TB + tr0);
-      bool cached = false;  // the sampled controls of this row are in LDS (no normals re-read)
-      float nom = 0.f, sg = 0.f, lo = 0.f, hi = 0.f;
-      if constexpr (EPS) {  // rows hold the normals: u = clamp(u_nom[t+1] + sigma*eps) as sampled
-        const int c = (j - 2) >= H ? 1 : 0;
-        const int t = max(j - 2, 0) - c * H;
-        const int ti = min(t + 1, H - 1);
-        nom = unom[c * H + ti];
-        sg = c ? a.s2 : a.s1;
-        lo = c ? a.min_u2 : a.min_u1;
-        hi = c ? a.max_u2 : a.max_u1;
-        if (j >= 2 && t < uc_steps) {
-          cached = true;
-          u4 = reinterpret_cast<const float4*>(ucache + (size_t)(c * uc_steps + t) * UCACHE_ROW + tr0);
-        }
-      }
-      cached_r[q] = cached;
-      nom_r[q] = nom;
-      sg_r[q] = sg;
-      lo_r[q] = lo;
-      hi_r[q] = hi;
-#pragma unroll
-      for (int g = 0; g < 8; ++g) uq[q][g] = (j >= 2) ? u4[g] : make_float4(1.f, 1.f, 1.f, 1.f);
-    }
-#pragma unroll
-    for (int q = 0; q < LR; ++q) {
-      const int it = u0 + q * NT + tid;
-      const int j = jr[q];
-      double gs[8];
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        const float4 w = w4r[q][g];
-        float4 u = uq[q][g];
-        if (EPS && !cached_r[q]) {
-          u.x = clampf(nom_r[q] + sg_r[q] * u.x, lo_r[q], hi_r[q]);
-          u.y = clampf(nom_r[q] + sg_r[q] * u.y, lo_r[q], hi_r[q]);
-          u.z = clampf(nom_r[q] + sg_r[q] * u.z, lo_r[q], hi_r[q]);
-          u.w = clampf(nom_r[q] + sg_r[q] * u.w, lo_r[q], hi_r[q]);
-        }
-        if (j < 2) u = make_float4(1.f, 1.f, 1.f, 1.f);  // j == 1: S, the weights alone
-        // (w0 u0 + w1 u1) + (w2 u2 + w3 u3) in float64: a product of two floats is exact in a
-        // double, so fma(w0, u0, w1 u1) is the rounded sum of the exact products (one product and
-        // one fma instead of two products and an add per pair; same bits)
-        const double a = __builtin_fma((double)w.x, (double)u.x, (double)w.y * (double)u.y);
-        const double b = __builtin_fma((double)w.z, (double)u.z, (double)w.w * (double)u.w);
-        gs[g] = a + b;
-      }
-      const double ls = ((gs[0] + gs[1]) + (gs[2] + gs[3])) + ((gs[4] + gs[5]) + (gs[6] + gs[7]));
-      // (line 0 + line 1), (line 2 + line 3): left + right; then the half; then the row
-      const double s2 = ls + __shfl_xor(ls, 8, 64);
-      const double hs = s2 + __shfl_xor(s2, 16, 64);
-      const double rs = hs + __shfl_xor(hs, 32, 64);
-      const int r = ((it >> 6) << 3) + (it & 7);
-      if (r < NR && ((it >> 3) & 7) == 0) {
-        const int leaf = r / (E - 1);
-        red[leaf * E + jr[q]] = rs;
-      }
-    }
+  if (tid < NU) reduce(tid, first);
+  for (int it = NT + tid; it < NU; it += NT) {
+    Unit U;
+    load(it, U);
+    reduce(it, U);
   }
   __syncthreads();
   for (int j = tid; j < E; j += NT) {
