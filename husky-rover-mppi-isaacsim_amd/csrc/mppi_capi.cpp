@@ -304,7 +304,7 @@ Plan make_plan(const mppi_ctx* c) {
   pl.roles = c->roles < 0 ? pl.blocks <= c->num_cus : c->roles != 0;
   pl.block = (pl.roles ? ROLES_WAVES_PER_TRAJ_WAVE : 2) * TB;
   const size_t scratch = ((size_t)(TB + TB / 64) * 4 + 15) / 16 * 16 + (size_t)(TB / 256) * (2 * H + 2) * sizeof(double);
-  const size_t ring_rows = pl.roles ? (size_t)(4 + 4) * PAIR_RING + 2 : (size_t)(PAIR_RING_IN + 4) * PAIR_RING + 1;
+  const size_t ring_rows = pl.roles ? (size_t)4 * PAIR_RING + 4 * ROLES_RING_OUT + 2 : (size_t)(PAIR_RING_IN + 4) * PAIR_RING + 1;
   pl.lds_bytes = ring_rows * TB * sizeof(float) + 4 * (TB / 64) * sizeof(int) +
                  (size_t)((2 * H + 3) & ~3) * sizeof(float) + scratch;
   // only at one workgroup per CU (the role-split kernel always: beyond one block per CU its

@@ -149,6 +149,9 @@ constexpr int PAIR_RING = 6;  // = PAIR_D in mppi_kernels.hip
 // floats per trajectory and step, side -> chain: (v, sin, cos, 1 - cos) of the Rodrigues angle,
 // computed by the side wave at production, off the chain's serial path
 constexpr int PAIR_RING_IN = 4;
+// the role-split kernel's ring_out depth (x, y, cx, cy of each step, chain -> wheel and cost waves):
+// round 6, 8 and 10 (two control-cache steps fewer each) measured within noise of 6 or below it
+constexpr int ROLES_RING_OUT = 6;
 hipError_t launch_rollout_pair(const RolloutArgs& a, int blocks, size_t lds, hipStream_t st, int proj,
                                int mode, bool dump, bool roles = false);
 // The role-split rollout kernel (mppi_rollout_roles_kernel): the same 256 trajectories per

@@ -1041,7 +1041,7 @@ __device__ __forceinline__ void lds_wait_ge(const int* f, int target, int& seen)
   seen = v;
 }
 
-template <int TB, int NC, bool DUMP>
+template <int TB, int NC, bool DUMP, int DO = PAIR_D>
 __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem& dem, const Traj& s, int tj,
                                               bool valid, int64_t kl, const float* ring_in, float* ring_out,
                                               const int* f_prod, int* f_chain, const int* const (&f_cons)[NC],
@@ -1142,9 +1142,9 @@ __device__ __forceinline__ void chain_wave_3d(const RolloutArgs& a, const Dem& d
         }
         if constexpr (EVEN) {
 #pragma unroll
-          for (int c = 0; c < NC; ++c) lds_wait_ge(f_cons[c], t - D + 2, seen_cons[c]);
+          for (int c = 0; c < NC; ++c) lds_wait_ge(f_cons[c], t - DO + 2, seen_cons[c]);
         }
-        float* ro = ring_out + (t % D) * 4 * TB + tj;
+        float* ro = ring_out + (t % DO) * 4 * TB + tj;
         ro[0] = pX.x;
         ro[TB] = pX.y;
         ro[2 * TB] = cxy.x;
@@ -1540,11 +1540,12 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
   constexpr int NT = NROLES * TB;
   constexpr int NG = TB / 64;  // trajectory groups (waves per role)
   constexpr int D = PAIR_D;
+  constexpr int DO = ROLES_RING_OUT;  // ring_out's depth (the consumers' slack behind the chain)
   constexpr int RI = 4;
   static_assert(TB == 256, "UCACHE_ROW assumes 256 trajectories per workgroup");
   float* ring_in = reinterpret_cast<float*>(smem_raw);   // [D][4][TB]: v, sin, cos, 1 - cos
-  float* ring_out = ring_in + D * RI * TB;               // [D][4][TB]: x, y, cx, cy
-  float* cost_lds = ring_out + D * 4 * TB;               // [TB]
+  float* ring_out = ring_in + D * RI * TB;               // [DO][4][TB]: x, y, cx, cy
+  float* cost_lds = ring_out + DO * 4 * TB;              // [TB]
   float* sw_lds = cost_lds + TB;                         // [TB] slope critic (WHEEL -> COST)
   int* flags = reinterpret_cast<int*>(sw_lds + TB);      // [4][NG]: produced, chained, wheel, cost
   float* unom_lds = reinterpret_cast<float*>(flags + 4 * NG);  // [2H] u_nom1 | u_nom2 (padded to 4)
@@ -1625,20 +1626,20 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
     if constexpr (PROJ == 3) {
       const int* cons[2] = {f_wheel, f_cost};
       int seen_cons[2] = {0, 0};
-      chain_wave_3d<TB, 2, DUMP>(a, dem, s, tj, valid, kl, ring_in, ring_out, f_prod, f_chain, cons, seen_prod,
+      chain_wave_3d<TB, 2, DUMP, DO>(a, dem, s, tj, valid, kl, ring_in, ring_out, f_prod, f_chain, cons, seen_prod,
                                  seen_cons);
     } else
     for (int sc = 0; sc < H; ++sc) {  // 2D (projection_warp.py:373-382): no normal, wheels zero
       wait_ge(f_prod, sc + 1, seen_prod);
-      wait_ge(f_wheel, sc - D + 1, seen_wheel);
-      wait_ge(f_cost, sc - D + 1, seen_cost);
+      wait_ge(f_wheel, sc - DO + 1, seen_wheel);
+      wait_ge(f_cost, sc - DO + 1, seen_cost);
       const float* ri = ring_in + (sc % D) * RI * TB + tj;
       const float v = ri[0], sn = ri[TB], cs = ri[2 * TB];
       const float cx = 0.f, cy = 0.f;
       StepOut o;
       step2d<false>(dem, a.dt, v, sn, cs, s, o, nobad);
       const float z = o.z;
-      float* ro = ring_out + (sc % D) * 4 * TB + tj;
+      float* ro = ring_out + (sc % DO) * 4 * TB + tj;
       ro[0] = s.x;
       ro[TB] = s.y;
       ro[2 * TB] = cx;
@@ -1743,7 +1744,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
     auto contacts = [&](int sc, float& lx, float& ly, float& lz, float& rx, float& ry, float& rz)
         __attribute__((always_inline)) {
       wait_ge(f_chain, sc + 1, seen_chain);
-      const float* ro = ring_out + (sc % D) * 4 * TB + tj;
+      const float* ro = ring_out + (sc % DO) * 4 * TB + tj;
       const float x = ro[0], y = ro[TB], cx = ro[2 * TB], cy = ro[3 * TB];
       lx = ly = lz = rx = ry = rz = 0.f;
       if constexpr (PROJ == 3) {
@@ -1814,7 +1815,7 @@ __device__ __forceinline__ int roles_body(const RolloutArgs& a, int blk, unsigne
     rcm.b = a.res_c;
     auto cstep = [&](int sc, float& cm_mine, float& cm_prev) __attribute__((always_inline)) {
       wait_ge(f_chain, sc + 1, seen_chain);
-      const float* ro = ring_out + (sc % D) * 4 * TB + tj;
+      const float* ro = ring_out + (sc % DO) * 4 * TB + tj;
       const float x = ro[0], y = ro[TB];
       cm_mine = a.cm[costmap_index<false>(a.cm_size, a.hw, rcm, x, y, nobad, a.rinv_res_c, a.cdiv_res_c)];
       const float pft = pf_sum + 10.0f * (fabsf(x - a.gx) + fabsf(y - a.gy));

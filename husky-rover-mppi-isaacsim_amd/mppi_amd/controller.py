@@ -182,7 +182,8 @@ class MPPI_Controller:
     Extra (optional) config section ``engine:`` — ``seed`` (Philox key, default
     42 as default_rng(42) at :409), ``device`` (HIP device, default 0),
     ``max_loops`` (run(), default 3500 as :763), ``async_tail``, ``resident`` (the resident
-    step server, default true; mppi_set_option "resident"; env MPPI_RESIDENT wins when set),
+    step server: true / 1 for back-to-back calls (default), 2 always, false / 0 never;
+    mppi_set_option "resident"; env MPPI_RESIDENT wins when set),
     ``resident_idle_us`` (how long an idle server stays resident, 200: DESIGN.md §3.5).
     """
 
@@ -223,7 +224,7 @@ class MPPI_Controller:
         # the resident step server and its idle limit (mppi_set_option); the environment's
         # MPPI_RESIDENT, when set, takes precedence over the config (profiling runs turn it off)
         self.resident = None if os.environ.get("MPPI_RESIDENT") is not None or "resident" not in eng \
-            else bool(eng["resident"])
+            else int(eng["resident"])  # (true / false, or 0 / 1 / 2: mppi_set_option "resident")
         self.resident_idle_us = eng.get("resident_idle_us")
         self.step_index = 0          # Philox step counter (replaces rng.integers at :517)
         self.engine = None
@@ -246,7 +247,7 @@ class MPPI_Controller:
         self.engine = _lib.Engine(self._params(), self.device)
         self.engine.set_async_tail(self.async_tail)
         if self.resident is not None:
-            self.engine.set_option("resident", 1 if self.resident else 0)
+            self.engine.set_option("resident", self.resident)
         if self.resident_idle_us is not None:
             self.engine.set_option("resident_idle_us", int(self.resident_idle_us))
         self._tail_fresh = True
