@@ -505,9 +505,10 @@ def cadence_bench(torch, device, proj, frames=40):
     2 ms: round 4's default, whose idle server holds every CU's LDS past the step) and "separate" (0).
     `slowdown` = the stand-in kernels' time beside the schedule / alone.  C3 (the headline K) and
     K=1000 (config.yaml's number_of_trajectories).  Rows with "sim_first" launch the frame's stand-in
-    BEFORE the step (the simulator's kernels still in flight when the controller is called).  The
-    schedules of one (K, gap) group run frame-interleaved on contexts of their own (server_idle2000
-    alone), so that their latencies compare under the same drift."""
+    BEFORE the step (the simulator's kernels still in flight when the controller is called).  Every
+    schedule runs alone on a context of its own (frame-interleaved contexts share the process's
+    hardware queues, and a step then queued behind another context's idle server); "default" and
+    "separate" in A B B A order ("pass" 1 / 2)."""
     from mppi_amd import _lib
     dev = torch.device("cuda", device)
     src = torch.ones(1 << 28, dtype=torch.float32, device=dev)
@@ -556,46 +557,45 @@ def cadence_bench(torch, device, proj, frames=40):
             eng.step(proj, i, copy=False)
         return eng
 
-    def run(K, scheds, gap_ms, sim_first):
-        """The schedules' frames interleaved (frame f of every schedule, then frame f + 1): the rows of
-        one group see the same clock and thermal drift, so their latencies compare pairwise."""
-        engs = [engine(K, opts) for _, opts in scheds]
-        lat, wk = [[] for _ in scheds], [[] for _ in scheds]
-        i0 = [e.launch_info() for e in engs]
-        step = 10
-        for _ in range(frames):
-            for j, eng in enumerate(engs):
-                if sim_first:
-                    world_launch()
-                t0 = time.perf_counter()
-                eng.step(proj, step, copy=False)
-                t1 = time.perf_counter()
-                lat[j].append((t1 - t0) * 1e3)
-                wk[j].append(world_wait() if sim_first else world_step())
-                while (time.perf_counter() - t1) * 1e3 < gap_ms:
-                    time.sleep(0.0002)
-            step += 1
-        for j, ((sched, _), eng) in enumerate(zip(scheds, engs)):
-            i1 = eng.launch_info()
-            w = np.median(np.array(wk[j]), axis=0)
-            la = np.array(lat[j])
-            out["rows"].append({
-                "K": K, "schedule": sched, "sim_first": sim_first, "gap_ms": gap_ms, "frames": frames,
-                "latency_ms_p50": round(float(np.median(la)), 4),
-                "latency_ms_p90": round(float(np.percentile(la, 90)), 4),
-                "copy_ms": round(float(w[0]), 4), "gemm_ms": round(float(w[1]), 4),
-                "copy_slowdown": round(float(w[0] / alone[0]), 3),
-                "gemm_slowdown": round(float(w[1] / alone[1]), 3),
-                **{k: i1[k] - i0[j][k] for k in keys}})
-            eng.close()
+    def run(K, sched, opts, gap_ms, sim_first, rep):
+        """One schedule alone on a context of its own (several contexts at once share the process's
+        hardware queues: a step then queues behind another context's idle server)."""
+        eng = engine(K, opts)
+        lat, wk = [], []
+        i0 = eng.launch_info()
+        for f in range(frames):
+            if sim_first:
+                world_launch()
+            t0 = time.perf_counter()
+            eng.step(proj, 10 + f, copy=False)
+            t1 = time.perf_counter()
+            lat.append((t1 - t0) * 1e3)
+            wk.append(world_wait() if sim_first else world_step())
+            while (time.perf_counter() - t1) * 1e3 < gap_ms:
+                time.sleep(0.0002)
+        i1 = eng.launch_info()
+        eng.close()
+        w = np.median(np.array(wk), axis=0)
+        la = np.array(lat)
+        out["rows"].append({
+            "K": K, "schedule": sched, "pass": rep, "sim_first": sim_first, "gap_ms": gap_ms, "frames": frames,
+            "latency_ms_p50": round(float(np.median(la)), 4),
+            "latency_ms_p90": round(float(np.percentile(la, 90)), 4),
+            "copy_ms": round(float(w[0]), 4), "gemm_ms": round(float(w[1]), 4),
+            "copy_slowdown": round(float(w[0] / alone[0]), 3),
+            "gemm_slowdown": round(float(w[1] / alone[1]), 3),
+            **{k: i1[k] - i0[k] for k in keys}})
 
     for K in (65536, 1000):
         for gap_ms in (2.0, 16.0):
-            run(K, (("default", {}), ("separate", {"resident": 0}), ("server_always", {"resident": 2})), gap_ms, False)
-            # (alone: its idle server holds every CU's LDS for 2 ms after each step, which the other
-            # schedules' steps would wait out)
-            run(K, (("server_idle2000", {"resident": 2, "resident_idle_us": 2000}),), gap_ms, False)
-        run(K, (("default", {}), ("separate", {"resident": 0})), 2.0, True)
+            # default and separate in A B B A order (at a frame cadence they run the same launches)
+            for rep, (sched, opts) in enumerate((("default", {}), ("separate", {"resident": 0}),
+                                                 ("separate", {"resident": 0}), ("default", {}))):
+                run(K, sched, opts, gap_ms, False, rep // 2 + 1)
+            run(K, "server_always", {"resident": 2}, gap_ms, False, 1)
+            run(K, "server_idle2000", {"resident": 2, "resident_idle_us": 2000}, gap_ms, False, 1)
+        for rep, (sched, opts) in enumerate((("default", {}), ("separate", {"resident": 0}))):
+            run(K, sched, opts, 2.0, True, 1)
     return out
 
 
