@@ -140,6 +140,7 @@ struct mppi_ctx {
   bool srv_exiting = false;   // a stop was posted and the launch may not have retired yet
   unsigned srv_launch_id = 0;  // the running (or last) launch's id: its stop word
   double last_return_us = 0;  // host time the last step returned (0: none yet)
+  int b2b_calls = 0;          // consecutive back-to-back steps (resident 1)
   int64_t srv_fallbacks = 0;  // server steps whose finish gave up, rerun as separate launches
   int64_t cadence_steps = 0;  // steps the server's plan fits that ran as separate launches (resident 1)
   int srv_proj = 0;
@@ -1194,10 +1195,14 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   if (resident && c->resident == 1) {
     // the caller's cadence: a call more than half the idle limit after the last step returned (a
     // simulator frame) runs as separate launches, and a server that has been idle that long is told
-    // to leave (the launches queue behind it); back-to-back calls keep or start the server
+    // to leave (the launches queue behind it); back-to-back calls keep the server, and start one when
+    // the last step ran on a server (stopped by another call since, e.g. a synchronize) or the call is
+    // the second back-to-back one in a row (a lone back-to-back call after a frame-cadence step would
+    // pay a server launch for one step: separate launches are cheaper there)
     const double now = now_us(), half = 0.5 * (double)c->srv_idle_us;
     const bool back_to_back = c->last_return_us > 0 && now - c->last_return_us <= half;
-    if (c->srv_running ? now - c->srv_last_us > half : !back_to_back) {
+    c->b2b_calls = back_to_back ? c->b2b_calls + 1 : 0;
+    if (c->srv_running ? now - c->srv_last_us > half : !(back_to_back && (c->last_resident || c->b2b_calls >= 2))) {
       post_stop(c);
       resident = false;
       ++c->cadence_steps;

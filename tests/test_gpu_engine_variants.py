@@ -264,15 +264,19 @@ def test_server_finish_gives_up_then_falls_back():
 def test_cadence_policy():
     """"resident" 1 (the default): back-to-back calls run on the server, a call more than half the idle
     limit after the last step returned (a simulator frame) runs as separate launches and lets the server
-    go (launch_info["cadence_steps"]).  Every step equals the separate launches."""
-    ref = _run(65536, 24, opts={"resident": 0}, steps=8, async_tail=True, states=True)
+    go (launch_info["cadence_steps"]); after such a step the server starts again with the second
+    back-to-back call in a row, or at once when the last step ran on a server that another call
+    stopped (sync).  Every step equals the separate launches."""
+    ref = _run(65536, 24, opts={"resident": 0}, steps=10, async_tail=True, states=True)
     # (an idle limit of 1 ms: half of it leaves room for this loop's host work between calls)
     eng = _engine(65536, 24, opts={"resident": 1, "resident_idle_us": 1000}, async_tail=True)
     outs, sched = [], []
     try:
-        for i in range(8):
+        for i in range(10):
             if i in (3, 6):
                 time.sleep(0.005)  # a frame gap (10x half the idle limit)
+            if i == 9:
+                eng.sync()  # stops the server that ran step 8
             eng.set_state(_state(i))
             eng.step("3d", i, copy=False)
             sched.append(eng.launch_info()["resident"])
@@ -283,9 +287,10 @@ def test_cadence_policy():
     finally:
         eng.close()
     _same((outs, costs), ref, "cadence policy")
-    # step 0 has no previous return; 3 and 6 follow a frame gap; the others are back to back
-    assert sched == [0, 1, 1, 0, 1, 1, 0, 1], sched
-    assert info["cadence_steps"] == 8 - sum(sched) and info["server_failed_steps"] == 0, info
+    # step 0 has no previous return; 3 and 6 follow a frame gap; 1, 4, 7 are the first back-to-back
+    # call after a separate-launch step, 2, 5, 8 the second; 9 restarts the server a sync stopped
+    assert sched == [0, 0, 1, 0, 0, 1, 0, 0, 1, 1], sched
+    assert info["cadence_steps"] == 10 - sum(sched) and info["server_failed_steps"] == 0, info
 
 
 def _hold(groups, lds, us):
