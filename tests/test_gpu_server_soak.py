@@ -92,4 +92,5 @@ def test_server_mixed_cadence_equals_separate_launches(resident, soak_ref):
         assert info["server_steps"] == n and info["cadence_steps"] == 0, info
     else:
         assert info["server_steps"] + info["cadence_steps"] == n, info
-        assert info["server_steps"] > n // 8 and info["cadence_steps"] > n // 4, info
+        # (both schedules many times: how many of each depends on the host's timing)
+        assert info["server_steps"] > n // 20 and info["cadence_steps"] > n // 4, info
