@@ -165,6 +165,13 @@ struct mppi_ctx {
   // some) would wait for them, while the workgroups it has hold theirs: past the bound the step is
   // rerun as separate launches, which need no co-residency (step_impl)
   uint64_t fin_wait_ticks = 100000ull;
+  // where the next steps' normals are ordered on the context stream (separate launches, partial
+  // steps): after the rollout (an event marker between the rollout and the finish, ~5 us on the
+  // step's path) or after the finish (the noise then runs into the next rollout of a back-to-back
+  // caller).  eps_after: -1 by the call's cadence (default: after the finish for a call more than
+  // half the idle limit after the last one returned, a simulator frame), 0 / 1 forced (mppi_set_option)
+  int eps_after = -1;
+  bool eps_late = false;  // this step's choice
   // the server's tail of the last step, launched once its completion word was seen (at the next
   // step's command, or when its outputs are wanted): no kernel waits on the GPU for its inputs
   bool tail_deferred = false;
@@ -807,7 +814,8 @@ int speculate_eps(mppi_ctx* c, const Plan& pl, uint64_t step, int used, hipEvent
 
 // Enqueue the rollout kernel for the current state / nominal sequence.
 int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl,
-                    const float* unom, const mppi_state& st, const RolloutArgs* dump_args) {
+                    const float* unom, const mppi_state& st, const RolloutArgs* dump_args,
+                    int* spec_slot = nullptr) {
   if (proj != MPPI_PROJ_2D && proj != MPPI_PROJ_3D) return fail(MPPI_EINVAL, "proj must be 2 or 3");
   int rc = ensure_nodes(c, pl.blocks);
   if (rc) return rc;
@@ -849,11 +857,23 @@ int enqueue_rollout(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& 
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     c->ev_roll_pending = true;
   }
+  if (eps_slot >= 0 && !dump_args && spec_slot && c->eps_late) {
+    *spec_slot = eps_slot;  // (speculate_after: once the caller has enqueued the finish)
+    return MPPI_OK;
+  }
   if (eps_slot >= 0 && !dump_args) {  // the next steps' normals on the noise stream after this rollout
     HIP_TRY(hipEventRecord(c->ev_prev_roll, c->stream));
     return speculate_eps(c, pl, step, eps_slot, c->ev_prev_roll);
   }
   return MPPI_OK;
+}
+
+// The next steps' normals of a rollout enqueued with spec_slot set, ordered after what the context
+// stream holds now (the finish): no event marker between the rollout and the finish.
+int speculate_after(mppi_ctx* c, const Plan& pl, uint64_t step, int spec_slot) {
+  if (spec_slot < 0) return MPPI_OK;
+  HIP_TRY(hipEventRecord(c->ev_prev_roll, c->stream));
+  return speculate_eps(c, pl, step, spec_slot, c->ev_prev_roll);
 }
 
 // Finish arguments for `mode` (0: rank record, 1: finish; 1 becomes 2 with the deferred
@@ -1178,10 +1198,13 @@ int server_step(mppi_ctx* c, int proj, uint64_t step, const Plan& pl, int P, int
 
 // The launches of one step (rollout + finish + tail) outside the server.
 int enqueue_step(mppi_ctx* c, int proj, uint64_t step, int mode, const Plan& pl) {
-  int rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr);
+  int spec = -1;
+  int rc = enqueue_rollout(c, proj, step, mode, pl, c->u_nom[c->cur], c->st, nullptr, &spec);
   if (rc) return rc;
   trace_mark(c, 3);
-  return enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 1, nullptr, true);
+  rc = enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 1, nullptr, true);
+  if (rc) return rc;
+  return speculate_after(c, pl, step, spec);
 }
 
 int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out) {
@@ -1192,6 +1215,10 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
   int sP = 0, scol = 0, sgroups = 0;
   size_t slds = 0;
   bool resident = server_shape(c, pl, mode, &sP, &scol, &sgroups, &slds);
+  const double now = now_us(), half = 0.5 * (double)c->srv_idle_us;
+  const bool back_to_back = c->last_return_us > 0 && now - c->last_return_us <= half;
+  c->b2b_calls = back_to_back ? c->b2b_calls + 1 : 0;
+  c->eps_late = c->eps_after < 0 ? !back_to_back : c->eps_after == 1;
   if (resident && c->resident == 1) {
     // the caller's cadence: a call more than half the idle limit after the last step returned (a
     // simulator frame) runs as separate launches, and a server that has been idle that long is told
@@ -1199,9 +1226,6 @@ int step_impl(mppi_ctx* c, int proj, uint64_t step, int mode, mppi_outputs* out)
     // the last step ran on a server (stopped by another call since, e.g. a synchronize) or the call is
     // the second back-to-back one in a row (a lone back-to-back call after a frame-cadence step would
     // pay a server launch for one step: separate launches are cheaper there)
-    const double now = now_us(), half = 0.5 * (double)c->srv_idle_us;
-    const bool back_to_back = c->last_return_us > 0 && now - c->last_return_us <= half;
-    c->b2b_calls = back_to_back ? c->b2b_calls + 1 : 0;
     if (c->srv_running ? now - c->srv_last_us > half : !(back_to_back && (c->last_resident || c->b2b_calls >= 2))) {
       post_stop(c);
       resident = false;
@@ -1687,10 +1711,14 @@ int mppi_step_partial(mppi_ctx* c, int32_t proj, uint64_t step, double* record_d
   if (!record_dev) return fail(MPPI_EINVAL, "null record buffer");
   const Plan pl = make_plan(c);
   c->last_resident = false;
-  rc = enqueue_rollout(c, proj, step, 0, pl, c->u_nom[c->cur], c->st, nullptr);
+  int spec = -1;
+  c->eps_late = c->eps_after == 1;  // (a group's or rank's partial steps: back to back)
+  rc = enqueue_rollout(c, proj, step, 0, pl, c->u_nom[c->cur], c->st, nullptr, &spec);
   if (rc) return rc;
   remember(c, proj, step, 0, pl);
-  return enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 0, record_dev, false);
+  rc = enqueue_finish(c, pl, c->st, c->nodes, pl.blocks, 0, record_dev, false);
+  if (rc) return rc;
+  return speculate_after(c, pl, step, spec);
 }
 
 int mppi_step_finish(mppi_ctx* c, const double* records_dev, int32_t n, mppi_outputs* out) {
@@ -1778,6 +1806,11 @@ int mppi_set_option(mppi_ctx* c, const char* name, int64_t value) {
   if (n == "server_exit_after") {  // test hook: the next server launch's head leaves after this many commands
     if (value < 0 || value > 1000000) return fail(MPPI_EINVAL, "server_exit_after must be in [0, 1e6]");
     c->srv_exit_after = (unsigned)value;
+    return MPPI_OK;
+  }
+  if (n == "eps_after") {  // the next steps' normals after the finish (1), the rollout (0), by cadence (-1)
+    if (value < -1 || value > 1) return fail(MPPI_EINVAL, "eps_after must be -1, 0 or 1");
+    c->eps_after = (int)value;
     return MPPI_OK;
   }
   if (n == "finish_wait_ticks") {  // the server finish's record wait bound (100 MHz ticks; 0: give up at once)

@@ -307,6 +307,13 @@ int mppi_set_timing(mppi_ctx* ctx, int32_t enable);
  *                        its counters and runs the step again as separate launches (same
  *                        results, launch_info[16]; 0: give up at once, the test hook).  A server
  *                        that does not retire within 10 s of its stop fails the call (MPPI_EHIP).
+ *   "eps_after"          where separate launches and partial steps order the next steps' normals
+ *                        (noise kernel, side stream): -1 (default) by the call's cadence, after the
+ *                        finish for a call more than half "resident_idle_us" after the last step
+ *                        returned (no event marker between the rollout and the finish: ~5 us less
+ *                        latency per frame) and after the rollout for back-to-back calls and partial
+ *                        steps (the noise then ends before the next rollout); 0 / 1: always after the
+ *                        rollout / the finish.  Results are the same bits either way.
  *   "record_tree_finish" 1: the record-tree finish (mppi_finish_kernel) at every record count
  *                        (default 0: the column-split finish wherever its shape fits).
  *   "server_exit_after"  test hook: the next server launch leaves at its poll after serving this
