@@ -85,11 +85,14 @@ def _same(got, ref, tag):
 
 
 @pytest.mark.parametrize("K,H", [(65536, 24), (262144, 16)])
-@pytest.mark.parametrize("variant", ["separate-launches", "pair-kernel", "role-split-kernel", "record-tree"])
+@pytest.mark.parametrize("variant", ["separate-launches", "noise-after-rollout", "noise-after-finish", "pair-kernel",
+                                     "role-split-kernel", "record-tree"])
 def test_variant_bitwise_equal(K, H, variant):
     env, opts = {}, {}
     if variant == "separate-launches":
         opts = {"resident": 0}
+    elif variant.startswith("noise-after"):  # the next steps' noise ordered after the rollout / the finish
+        opts = {"resident": 0, "eps_after": 0 if variant.endswith("rollout") else 1}
     elif variant == "pair-kernel":
         env = {"MPPI_ROLES": "0"}
     elif variant == "role-split-kernel":
@@ -104,7 +107,7 @@ def test_variant_bitwise_equal(K, H, variant):
         assert i_ref["resident"] == 1 and i_ref["server_steps"] == 3, i_ref
     else:
         assert i_ref["resident"] == 0, i_ref
-    if variant in ("separate-launches", "pair-kernel", "record-tree"):
+    if variant != "role-split-kernel":
         assert i_got["resident"] == 0, i_got
 
 
