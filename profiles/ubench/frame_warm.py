@@ -1,4 +1,5 @@
-"""Diagnostic (round 6): the role-split rollout's cache warm-up (mppi_set_option "warm") at a frame
+"""Diagnostic (round 6, for the experiment build only: the "warm" option and its warm-up code were removed
+after this measurement, profiles/r06_notes.md): the role-split rollout's cache warm-up at a frame
 cadence beside the bench's simulator stand-in (1 GiB copy + bf16 GEMM, waited for), alternating
 warm 0 / 1: call latency p50 / p90, the chain's cycles per step; and back to back (separate launches,
 warm 0 / 2).  Usage (GPU box): python profiles/ubench/frame_warm.py [rounds]"""
