@@ -208,6 +208,21 @@ def test_step_counter_jumps(resident):
     _same(got, ref, f"jumps resident={resident}")
 
 
+def test_option_validation():
+    """mppi_set_option refuses values outside each option's range (the context keeps its setting)."""
+    eng = _engine(2048, 8)
+    try:
+        for name, bad in (("resident", 3), ("resident", -1), ("eps_after", 2), ("eps_after", -2),
+                          ("resident_idle_us", 50), ("finish_wait_ticks", -1), ("no_such_option", 1)):
+            with pytest.raises(RuntimeError, match="mppi_set_option"):
+                eng.set_option(name, bad)
+        for name, good in (("resident", 0), ("eps_after", -1), ("eps_after", 0), ("eps_after", 1)):
+            eng.set_option(name, good)
+        eng.step("3d", 0, copy=False)
+    finally:
+        eng.close()
+
+
 def test_timing_modes():
     """mppi_set_timing: mode 2 times the rollout only (no host wait), mode 1 also the finish and
     the deferred tail (both as separate launches: timing is off the server); other modes are
